@@ -1,0 +1,230 @@
+"""Benchmark: SDF queries/s on 256^3 grids (+ DDPM sample steps/s), 1..8 MI355X.
+
+One "step" = decode of ``--batch`` synthetic shapes on a ``--grid``^3 grid (config 4:
+B=64, 256^3), z-slab sharded over the ranks with one RCCL all-gather of the volume
+(SURVEY.md §8(e)).  Total work is fixed as N grows (``scaling: strong``); ``value`` =
+all queries of the step / max-over-ranks step time.
+
+Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Rank 0 prints ONE JSON line.  Extra objects: ``roofline`` (dominant kernel, HIP events on its
+stream), ``cpu_baseline`` (oracle/ref_cpu.py fp32 on this host's cores, bounded sample),
+``ddpm`` (config 3: 1000-step sampling of 8 latents, hipGraph replay, steps/s).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "latent-diffusion-models-for-shape-sdfs_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FLOPS_PER_QUERY = 2 * (3 * 512 + 2 * 512 * 512 + 512 * 253 + 256 * 512 + 3 * 512 * 512 + 512)
+PEAK_TFLOPS = {"bf16": 2516.6, "fp16": 2516.6, "fp32": 157.3}   # MI355X dense (MICROARCH guide)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ddpm", action="store_true")
+    ap.add_argument("--ddpm-batch", type=int, default=8)
+    return ap.parse_args()
+
+
+def cpu_baseline_decode(grid: int, budget_s: float):
+    """oracle decode (torch CPU fp32, all affine cores) of whole z-slices of the grid until
+    ``budget_s`` of work; q/s is flat in N."""
+    from oracle import ref_cpu as R
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    p = R.make_decoder_params(seed=1234, dtype=torch.float32)
+    z = torch.randn(1, 256, generator=torch.Generator().manual_seed(0)) * 0.1
+    pts = 0
+    t0 = time.perf_counter()
+    k = 0
+    while k < grid:
+        R.decode_grid(p, z, grid, k, k + 1)
+        pts += grid * grid
+        k += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": pts / dt, "unit": "queries/s", "cores": cores, "kind": "port",
+            "sample": f"{k} z-slices x {grid}x{grid} of the {grid}^3 grid ({pts} queries), "
+                      f"1 shape, fp32 torch-CPU oracle, {dt:.1f}s"}
+
+
+def cpu_baseline_sampling(budget_s: float, B: int):
+    from oracle import ref_cpu as R
+    p = R.make_denoiser_params(seed=4321, dtype=torch.float32)
+    tab = R.ddpm_tables()
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128))
+    x = torch.randn(B, 256)
+    noise = torch.randn(1000, B, 256)
+    t0 = time.perf_counter()
+    steps = 0
+    with torch.inference_mode():
+        for t in range(999, -1, -1):
+            eps = R.denoiser_forward(p, x, torch.full((B,), t), emb)
+            x = R.ddpm_step(tab, x, eps, noise[t], t)
+            steps += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "steps/s", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"{steps} reverse steps, B={B}, fp32 torch-CPU oracle"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    import ldm_sdf
+    from ldm_sdf import ops
+    from ldm_sdf.dist import slab_bounds
+
+    ldm_sdf.load_library()
+    N, B = args.grid, args.batch
+    decoder = ldm_sdf.SDFDecoder(256, seed=1234)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    latents = torch.randn(B, 256, device=dev, generator=gen) * 0.1
+    pack = decoder.device_pack(args.dtype, dev)
+    desc = pack["desc"]
+    k0, k1, S = slab_bounds(rank, world, N)
+    npts_local = (k1 - k0) * N * N
+    out = torch.empty(B, N, N, N, device=dev)
+    kern_ms = []
+    stream = torch.cuda.current_stream(dev)
+
+    def step(timed: bool):
+        beta = ops.decoder_fold(desc, latents)
+
+        def slab(a, b, dst):
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                ops.decoder_grid_fwd(desc, beta, N, a, b, out=dst)
+                e1.record(stream)
+                kern_ms.append((e0, e1))
+            else:
+                ops.decoder_grid_fwd(desc, beta, N, a, b, out=dst)
+
+        if world == 1:
+            slab(0, N, out)
+        else:
+            ldm_sdf.dist.decode_sharded(slab, B, N, dev, group=group, out=out)
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt)
+    kms = sum(a.elapsed_time(b) for a, b in kern_ms) / max(1, len(kern_ms))
+    total_q = B * N ** 3 * args.steps
+    value = total_q / elapsed
+    ach = FLOPS_PER_QUERY * B * npts_local / (kms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    prof_traffic = None
+    tf = os.path.join(ROOT, "profiles", "decoder_traffic.json")
+    if os.path.exists(tf):
+        try:
+            prof_traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+        except Exception:
+            prof_traffic = None
+
+    res = None
+    if rank == 0:
+        res = {
+            "metric": "SDF queries/sec on 256^3 grid (+ DDPM sample steps/sec)",
+            "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic (latents N(0,0.1^2) seed 0, He-normal decoder seed 1234)",
+            "config": {"workload": f"config4: decode B={B} shapes on a {N}^3 grid, z-slab sharded "
+                                   f"over {world} rank(s) + RCCL all-gather of the volume",
+                       "batch": B, "grid": N, "latent_dim": 256, "decoder": "DeepSDF 8x512 skip@4",
+                       "parallelism": f"zslab{world}"},
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                         "frac": ach / peak, "traffic": prof_traffic,
+                         "kernel": "dec_mfma_kernel (+aux_pack, <0.1%)",
+                         "flops_per_query": FLOPS_PER_QUERY,
+                         "queries_per_launch": B * npts_local, "avg_launch_ms": kms},
+        }
+    if rank == 0 and not args.no_ddpm:
+        den = ldm_sdf.MLPDenoiser(seed=4321)
+        sch = ldm_sdf.DDPMSchedule()
+        nb = args.ddpm_batch
+        sampler = ldm_sdf.Sampler(den, sch, nb, dtype="bf16", device=dev)
+        xT = torch.randn(nb, 256, device=dev, generator=gen)
+        noise = torch.randn(1000, nb, 256, device=dev, generator=gen)
+        sampler.run(xT, noise)            # capture + first replay
+        torch.cuda.synchronize()
+        reps = 3
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            sampler.run(xT, noise)
+        torch.cuda.synchronize()
+        sps = 1000 * reps / (time.perf_counter() - t1)
+        # sample -> decode on 128^3 (config 3) for the end-to-end latency
+        t2 = time.perf_counter()
+        lat = sampler.run(xT, noise)
+        ldm_sdf.decode(decoder, lat, 128, dtype=args.dtype)
+        torch.cuda.synchronize()
+        wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nb * den.D * 4
+        res["ddpm"] = {"metric": "DDPM sample steps/sec", "value": sps, "unit": "steps/s",
+                       "batch": nb, "T": 1000, "shape_steps_per_s": sps * nb,
+                       "graph": "hipGraph of 1000 fused steps (6 kernels each)",
+                       "roofline": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
+                                    "peak": 8000.0, "unit": "GB/s",
+                                    "frac": sps * wbytes / 8e12,
+                                    "bytes_per_step": wbytes},
+                       "config3_sample_plus_decode128_s": time.perf_counter() - t2}
+    if rank == 0 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_decode(N, args.cpu_seconds)
+        if "ddpm" in res:
+            res["ddpm"]["cpu_baseline"] = cpu_baseline_sampling(min(5.0, args.cpu_seconds), args.ddpm_batch)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

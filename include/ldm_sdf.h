@@ -1,0 +1,189 @@
+/*
+ * ldm_sdf.h -- C ABI of libldm_sdf.so, the MI355X (gfx950) hot path of latent diffusion
+ * over DeepSDF shape codes.
+ *
+ * The reference project (SGI-2022/Latent-Diffusion-Models-for-Shape-SDFs) ships no code:
+ * /root/reference/README.md:1 is its only line, so it has no FFI to mirror.  Every entry
+ * point below is the build-defined boundary of SURVEY.md §8(b); each cites the §8(a) row it
+ * implements (and, for the Python side, the ldm_sdf/api.py function that calls it).
+ *
+ * Conventions:
+ *   - All buffers are caller-owned DEVICE pointers (torch tensors), contiguous, 16-byte aligned
+ *     (the shim checks alignment).  The library never allocates or frees device memory.
+ *   - Every launch is asynchronous on the caller's stream; no hidden synchronisation, no
+ *     hipMalloc / hipMemcpy (so calls can be captured into a hipGraph).
+ *   - Return 0 on success, a negative LDM_E* code for an argument error, or a positive
+ *     hipError_t.  ldm_last_error() returns a thread-local message for the last failure.
+ *   - One device per process (the current HIP device, as set by torch).
+ */
+#ifndef LDM_SDF_H
+#define LDM_SDF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDM_ABI_VERSION 1
+
+/* dtypes */
+#define LDM_F32 0
+#define LDM_BF16 1
+#define LDM_F16 2
+
+/* argument errors */
+#define LDM_EINVAL (-22)
+#define LDM_EALIGN (-14)
+#define LDM_ENOSYS (-38)
+#define LDM_ENOSPC (-28)
+
+/* workspace ops for ldm_workspace_bytes() */
+#define LDM_OP_DECODER_GRID 1
+#define LDM_OP_DECODER_POINTS 2
+
+typedef void* ldm_stream_t; /* hipStream_t; NULL = the null stream */
+
+/*
+ * DeepSDF decoder weights, packed on the host by ldm_sdf/pack.py.
+ * The hot kernels support hidden == 512 with 8 hidden layers and the latent re-injected at
+ * layer 4 (DeepSDF); skip_width is the output width of layer 3: 253 (DeepSDF, L=256) or 512
+ * (the "widen-skip" variant used for L >= H, config 5).  Layouts: DESIGN.md §3.
+ */
+typedef struct ldm_decoder {
+    int32_t abi_version;  /* must equal LDM_ABI_VERSION */
+    int32_t dtype;        /* LDM_F32 (parity kernel) / LDM_BF16 / LDM_F16 (MFMA kernel) */
+    int32_t hidden;       /* H (512) */
+    int32_t skip_width;   /* 253 or 512 */
+    int32_t latent_dim;   /* L */
+    int32_t n_stages;     /* bf16/f16: number of 8 KiB weight stages per tile; f32: 0 */
+    const void* weights;  /* bf16/f16: stage blob [n_stages][8][64][8]; f32: fp32 blob */
+    const float* wz;      /* fp32 [2][H][L]  latent columns of layer 0 and layer 4 */
+    const float* bz;      /* fp32 [2][H]     biases of layer 0 and layer 4 */
+    const float* wxyz;    /* fp32 [2][H][3]  xyz columns of layer 0 and layer 4 */
+    const float* w_last;  /* fp32 [H] final 512->1 weights (bf16/f16: MFMA-row permuted) */
+    float b_last;         /* final bias */
+    int32_t reserved;
+} ldm_decoder_t;
+
+/* DDPM tables, fp32 device arrays of length T. */
+typedef struct ldm_sched {
+    int32_t abi_version;
+    int32_t T;
+    const float* sqrt_ab;   /* sqrt(abar_t) */
+    const float* sqrt_1mab; /* sqrt(1 - abar_t) */
+    const float* c1;        /* 1/sqrt(alpha_t) */
+    const float* c2;        /* beta_t / sqrt(1 - abar_t) */
+    const float* sigma;     /* sqrt(beta_t) */
+} ldm_sched_t;
+
+#define LDM_MAX_BLOCKS 8
+
+/*
+ * MLP denoiser (ldm_sdf/models.py MLPDenoiser).
+ * Weights are [out][in] row-major in `dtype` (LDM_F32 or LDM_BF16); biases fp32.
+ * w_blk[k] is [H][2H] = [W_k | U_k] acting on [h || temb].
+ * e_tab[k] (inference only) is fp32 [T][H] = U_k temb(t) + b_k for every t.
+ */
+typedef struct ldm_denoiser {
+    int32_t abi_version;
+    int32_t dtype;
+    int32_t D, H, n_blocks, TE, T;
+    int32_t reserved;
+    const void* w_in;   const float* b_in;    /* [H][D] */
+    const void* w_t1;   const float* b_t1;    /* [H][TE] */
+    const void* w_t2;   const float* b_t2;    /* [H][H] */
+    const void* w_blk[LDM_MAX_BLOCKS];
+    const float* b_blk[LDM_MAX_BLOCKS];       /* [H] */
+    const float* e_tab[LDM_MAX_BLOCKS];       /* [T][H] */
+    const void* w_out;  const float* b_out;   /* [D][H] */
+    const float* emb_table;                   /* [T][TE] sinusoidal (A5) */
+} ldm_denoiser_t;
+
+/* ---- library -------------------------------------------------------------------------- */
+int ldm_abi_version(void);
+const char* ldm_last_error(void);
+/* Device bytes of workspace an op needs (B shapes, n = N (grid) or P (points)). */
+size_t ldm_workspace_bytes(int op, int B, int n, int dtype);
+
+/* ---- decoder: A1 grid coords, A2 latent fold, A3 fused MLP ----------------------------- */
+/* A1 standalone: xyz_out fp32 [(k1-k0)*N*N][3], z slowest, x fastest, x = fl32(fl32(i*vs)+origin). */
+int ldm_grid_coords(int N, int k0, int k1, float vs, float origin, float* xyz_out,
+                    ldm_stream_t s);
+/* A2: beta_out fp32 [B][2][H]; z fp32 [B][L]. */
+int ldm_decoder_fold(const ldm_decoder_t* w, const float* z, int B, float* beta_out,
+                     ldm_stream_t s);
+/* A1+A3 grid mode: out fp32 [B][(k1-k0)*N*N] (the z-slab [k0,k1) of each shape's N^3 grid). */
+int ldm_decoder_grid_fwd(const ldm_decoder_t* w, const float* beta, int B, int N, int k0,
+                         int k1, float vs, float origin, float* out, void* ws,
+                         size_t ws_bytes, ldm_stream_t s);
+/* A3 point-list mode: xyz fp32 [B][P][3] -> out fp32 [B][P]. */
+int ldm_decoder_points_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz,
+                           int B, int P, float* out, void* ws, size_t ws_bytes,
+                           ldm_stream_t s);
+
+/* ---- DDPM: A8 reverse step, A9 q_sample + eps-MSE ------------------------------------ */
+/* x_out[i] = c1[t]*(x[i] - c2[t]*eps[i]) + sigma[t]*z[i]  (z ignored at t == 0). n elements. */
+int ldm_ddpm_step(const ldm_sched_t* sc, const float* x, const float* eps, const float* z,
+                  int t, int n, float* x_out, ldm_stream_t s);
+/* x_t[b][d] = sqrt_ab[t_b] x0 + sqrt_1mab[t_b] eps.  t int32 [B]. */
+int ldm_q_sample(const ldm_sched_t* sc, const float* x0, const float* eps, const int32_t* t,
+                 int B, int D, float* xt_out, ldm_stream_t s);
+/* loss_out[0] = mean((eps_hat - eps)^2); grad_out = d loss / d eps_hat (may be NULL). */
+int ldm_eps_mse_loss(const float* eps_hat, const float* eps, int n, float* loss_out,
+                     float* grad_out, ldm_stream_t s);
+
+/* ---- denoiser: A6 forward (sampling: uniform t) and the sampling step ------------------ */
+/* eps_out fp32 [B][D] = net(x, t) for one timestep t shared by the batch (B <= 16), using
+ * the tabulated e_tab.  ws: fp32 scratch of at least 2*B*H floats. */
+int ldm_denoiser_fwd_uniform_t(const ldm_denoiser_t* w, const float* x, int t, int B,
+                               float* eps_out, float* ws, ldm_stream_t s);
+/* One DDPM reverse step fused with the denoiser (A6 + A8, the A10 loop body):
+ * x_out = c1[t] (x - c2[t] net(x,t)) + sigma[t] z  (z ignored at t = 0).  x_out != x. */
+int ldm_sample_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x,
+                    const float* z, int t, int B, float* x_out, float* ws, ldm_stream_t s);
+
+/* ---- generic fused linear (A6/A7 building block, training) ---------------------------- */
+/* acc[b][m] = sum_{k<K} X[b][k] W[m][k]  +  sum_{k<K2} X2[b][k] W2[m][k]   (K2 may be 0)
+ * with arbitrary element strides, so the forward (X W^T), input-gradient (G W) and
+ * weight-gradient (G^T X) products -- and the block's [h || temb] [W_k | U_k]^T -- are all
+ * this one call.  Epilogues (pre = acc + bias, bias optional):
+ *   LDM_EPI_BIAS        Y = pre
+ *   LDM_EPI_SILU        Y = SiLU(pre);      A_out = pre (if A_out)
+ *   LDM_EPI_RESID_SILU  Y = R + SiLU(pre);  A_out = pre (if A_out)      (A6 block)
+ *   LDM_EPI_ACCUM       Y = Y + pre
+ *   LDM_EPI_ADD_R       Y = R + pre                                     (A7 dh = dy + W^T g)
+ * w_dtype: LDM_F32 or LDM_BF16 (elements of W and W2). */
+#define LDM_EPI_BIAS 0
+#define LDM_EPI_SILU 1
+#define LDM_EPI_RESID_SILU 2
+#define LDM_EPI_ACCUM 3
+#define LDM_EPI_ADD_R 4
+typedef struct ldm_linear_args {
+    int32_t Bn, M, K, K2;
+    int32_t epi;
+    int32_t w_dtype;
+    const float* X;  int64_t sxb, sxk;
+    const void* W;   int64_t swm, swk;
+    const float* X2; int64_t sx2b, sx2k;
+    const void* W2;  int64_t sw2m, sw2k;
+    const float* bias;               /* [M] or NULL */
+    const float* R;  int64_t srb;    /* residual rows (col stride 1) */
+    float* Y;        int64_t syb, sym;
+    float* A_out;    int64_t sab;    /* pre-activation rows (col stride 1) */
+} ldm_linear_args_t;
+int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s);
+
+/* SiLU backward on the block pre-activation: g = dy * silu'(a)  (A7). n elements. */
+int ldm_silu_bwd(const float* dy, const float* a, int n, float* g_out, ldm_stream_t s);
+/* Column sums: out[m] (+)= sum_b G[b][m]  (bias gradients).  accumulate != 0 adds. */
+int ldm_colsum(const float* G, int Bn, int M, float* out, int accumulate, ldm_stream_t s);
+/* Row gather: out[b][:] = table[idx[b]][:] (timestep-embedding lookup, A5). */
+int ldm_gather_rows(const float* table, const int32_t* idx, int Bn, int C, float* out,
+                    ldm_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDM_SDF_H */

@@ -1,0 +1,55 @@
+// Internal helpers shared by the libldm_sdf.so translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/ldm_sdf.h"
+
+namespace ldm {
+
+// ---- error plumbing (ldm_last_error is thread-local, see ldm_capi.cpp) -----------------
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define LDM_REQUIRE(cond, code, ...)         \
+    do {                                     \
+        if (!(cond)) {                       \
+            ::ldm::set_error(__VA_ARGS__);   \
+            return (code);                   \
+        }                                    \
+    } while (0)
+
+#define LDM_ALIGNED(p, a) ((((uintptr_t)(p)) & ((a) - 1)) == 0)
+
+inline int launch_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+        return (int)e;
+    }
+    return 0;
+}
+
+// ---- fragment types ---------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// Decoder kernel geometry.  One 8 KiB "stage" = 8 MFMA A-fragments
+// (8 output m-chunks of 32 rows x one 16-wide k-step), 1 KiB each: [chunk][lane][8 elem].
+constexpr int kHidden = 512;
+constexpr int kStageBytes = 8192;
+constexpr int kTilePoints = 128;   // points per workgroup tile (4 waves x 32)
+
+// Number of 8 KiB stages per tile for skip width S (256 padded from 253, or 512).
+__host__ __device__ constexpr int dec_n_stages(int S) {
+    return 2 /*L0*/ + 66 /*L1*/ + 66 /*L2*/ + (S / 256) * 33 /*L3*/ + 2 * (S / 16 + 1) /*L4*/ +
+           3 * 66 /*L5-7*/;
+}
+__host__ __device__ constexpr int dec_base4(int S) { return 2 + 66 + 66 + (S / 256) * 33; }
+
+}  // namespace ldm

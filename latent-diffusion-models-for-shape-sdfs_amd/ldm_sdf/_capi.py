@@ -1,0 +1,134 @@
+"""ctypes binding of ``libldm_sdf.so`` (C ABI: ``include/ldm_sdf.h``).
+
+torch is imported first so that the HIP runtime torch bundles (``libamdhip64.so.7``) is the
+one the library binds to (same SONAME; SURVEY.md §7 'One HIP runtime per process').
+The library is built in-tree by ``__graft_entry__.build()`` (``csrc/Makefile``).  There is
+no fallback: if the library is missing or a call fails, this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import torch  # noqa: F401  (must precede the CDLL load)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldm_sdf.so")
+HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                            "..", "..", "include", "ldm_sdf.h"))
+
+ABI_VERSION = 1
+LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
+LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
+EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R = 0, 1, 2, 3, 4
+MAX_BLOCKS = 8
+
+DTYPE_CODES = {"fp32": LDM_F32, "bf16": LDM_BF16, "fp16": LDM_F16}
+
+_vp = C.c_void_p
+_fp = C.c_void_p  # device float* passed as raw address
+
+
+class Decoder(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("dtype", C.c_int32), ("hidden", C.c_int32),
+                ("skip_width", C.c_int32), ("latent_dim", C.c_int32), ("n_stages", C.c_int32),
+                ("weights", _vp), ("wz", _vp), ("bz", _vp), ("wxyz", _vp), ("w_last", _vp),
+                ("b_last", C.c_float), ("reserved", C.c_int32)]
+
+
+class Sched(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("T", C.c_int32), ("sqrt_ab", _vp),
+                ("sqrt_1mab", _vp), ("c1", _vp), ("c2", _vp), ("sigma", _vp)]
+
+
+class Denoiser(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("dtype", C.c_int32), ("D", C.c_int32),
+                ("H", C.c_int32), ("n_blocks", C.c_int32), ("TE", C.c_int32), ("T", C.c_int32),
+                ("reserved", C.c_int32),
+                ("w_in", _vp), ("b_in", _vp), ("w_t1", _vp), ("b_t1", _vp), ("w_t2", _vp),
+                ("b_t2", _vp), ("w_blk", _vp * MAX_BLOCKS), ("b_blk", _vp * MAX_BLOCKS),
+                ("e_tab", _vp * MAX_BLOCKS), ("w_out", _vp), ("b_out", _vp),
+                ("emb_table", _vp)]
+
+
+class LinearArgs(C.Structure):
+    _fields_ = [("Bn", C.c_int32), ("M", C.c_int32), ("K", C.c_int32), ("K2", C.c_int32),
+                ("epi", C.c_int32), ("w_dtype", C.c_int32),
+                ("X", _vp), ("sxb", C.c_int64), ("sxk", C.c_int64),
+                ("W", _vp), ("swm", C.c_int64), ("swk", C.c_int64),
+                ("X2", _vp), ("sx2b", C.c_int64), ("sx2k", C.c_int64),
+                ("W2", _vp), ("sw2m", C.c_int64), ("sw2k", C.c_int64),
+                ("bias", _vp), ("R", _vp), ("srb", C.c_int64),
+                ("Y", _vp), ("syb", C.c_int64), ("sym", C.c_int64),
+                ("A_out", _vp), ("sab", C.c_int64)]
+
+
+# (name, restype, argtypes) -- every symbol include/ldm_sdf.h declares.
+_i, _sz, _f = C.c_int, C.c_size_t, C.c_float
+SIGNATURES = [
+    ("ldm_abi_version", _i, []),
+    ("ldm_last_error", C.c_char_p, []),
+    ("ldm_workspace_bytes", _sz, [_i, _i, _i, _i]),
+    ("ldm_grid_coords", _i, [_i, _i, _i, _f, _f, _fp, _vp]),
+    ("ldm_decoder_fold", _i, [C.POINTER(Decoder), _fp, _i, _fp, _vp]),
+    ("ldm_decoder_grid_fwd", _i, [C.POINTER(Decoder), _fp, _i, _i, _i, _i, _f, _f, _fp, _vp,
+                                  _sz, _vp]),
+    ("ldm_decoder_points_fwd", _i, [C.POINTER(Decoder), _fp, _fp, _i, _i, _fp, _vp, _sz, _vp]),
+    ("ldm_ddpm_step", _i, [C.POINTER(Sched), _fp, _fp, _fp, _i, _i, _fp, _vp]),
+    ("ldm_q_sample", _i, [C.POINTER(Sched), _fp, _fp, _vp, _i, _i, _fp, _vp]),
+    ("ldm_eps_mse_loss", _i, [_fp, _fp, _i, _fp, _fp, _vp]),
+    ("ldm_denoiser_fwd_uniform_t", _i, [C.POINTER(Denoiser), _fp, _i, _i, _fp, _fp, _vp]),
+    ("ldm_sample_step", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _i, _i, _fp,
+                             _fp, _vp]),
+    ("ldm_linear", _i, [C.POINTER(LinearArgs), _vp]),
+    ("ldm_silu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),
+    ("ldm_colsum", _i, [_fp, _i, _i, _fp, _i, _vp]),
+    ("ldm_gather_rows", _i, [_fp, _vp, _i, _i, _fp, _vp]),
+]
+
+_lib: Optional[C.CDLL] = None
+
+
+class LdmError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    """Load libldm_sdf.so (raises if it is not built -- there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LdmError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                           f"(make -C csrc).  The HIP path has no fallback.")
+        lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.ldm_abi_version() != ABI_VERSION:
+            raise LdmError(f"libldm_sdf ABI {lib.ldm_abi_version()} != {ABI_VERSION}")
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().ldm_last_error().decode(errors="replace")
+        raise LdmError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device: Optional[torch.device] = None) -> Optional[int]:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise LdmError("ldm_sdf runs on the GPU only (HIP kernels); got a CPU tensor. "
+                           "The CPU restatement lives in oracle/ and is test infrastructure.")

@@ -1,0 +1,238 @@
+"""Public train / sample / decode API (SURVEY.md §8(b) 'Python API').
+
+The reference (/root/reference/README.md:1, a title only) defines no API; this is the
+build-defined surface a caller drops in:
+
+    decode(decoder, latents[B,L], resolution, *, bbox, dtype, group)  -> sdf[B,N,N,N]
+    decode_points(decoder, latents[B,L], xyz[B,P,3], *, dtype)        -> sdf[B,P]
+    sample(denoiser, schedule, n, *, steps, dtype, x_T, noise, ...)    -> latents[n,D]
+    train(denoiser, schedule, latents[M,D], *, steps, batch, lr, ...)  -> TrainState
+
+All tensors live on the GPU.  Every op runs in libldm_sdf.so (HIP, gfx950); there is no CPU
+path in the product (the CPU restatement is oracle/, test infrastructure only).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _capi as capi
+from . import dist as ldist
+from . import ops
+from .models import DDPMSchedule, MLPDenoiser, SDFDecoder
+
+
+# ---------------------------------------------------------------------------------- decode
+def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
+           bbox: Tuple[float, float] = (-1.0, 1.0), dtype: str = "bf16", group=None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """SDF of every shape on a dense ``resolution^3`` grid over ``bbox^3``.
+
+    Layout ``[B, z, y, x]`` (z slowest).  With an initialised process group the grid is
+    z-slab sharded over its ranks and all-gathered (every rank returns the full volume).
+    """
+    capi.require_device(latents)
+    if latents.dim() == 1:
+        latents = latents[None]
+    if latents.shape[1] != decoder.latent_dim:
+        raise ValueError(f"latents must be [B, {decoder.latent_dim}]")
+    N = int(resolution)
+    if N < 2:
+        raise ValueError("resolution must be >= 2")
+    pack = decoder.device_pack(dtype, latents.device)
+    desc = pack["desc"]
+    beta = ops.decoder_fold(desc, latents.float().contiguous())
+    B = latents.shape[0]
+    world, _ = ldist.world_and_rank(group)
+
+    def slab(k0: int, k1: int, dst: torch.Tensor) -> None:
+        ops.decoder_grid_fwd(desc, beta, N, k0, k1, bbox, out=dst)
+
+    if world == 1:
+        vol = out if out is not None else torch.empty(B, N, N, N, device=latents.device)
+        slab(0, N, vol)
+        return vol
+    return ldist.decode_sharded(slab, B, N, latents.device, group=group, out=out)
+
+
+def decode_points(decoder: SDFDecoder, latents: torch.Tensor, xyz: torch.Tensor, *,
+                  dtype: str = "bf16") -> torch.Tensor:
+    """SDF at arbitrary points: xyz ``[B, P, 3]`` (or ``[P, 3]`` shared) -> ``[B, P]``."""
+    capi.require_device(latents, xyz)
+    if latents.dim() == 1:
+        latents = latents[None]
+    B = latents.shape[0]
+    if xyz.dim() == 2:
+        xyz = xyz[None].expand(B, -1, -1)
+    pack = decoder.device_pack(dtype, latents.device)
+    beta = ops.decoder_fold(pack["desc"], latents.float().contiguous())
+    return ops.decoder_points_fwd(pack["desc"], beta, xyz.float().contiguous())
+
+
+# ---------------------------------------------------------------------------------- sample
+class Sampler:
+    """A10: the T-step reverse loop for a fixed (n, steps, dtype), captured once as a HIP
+    graph (``torch.cuda.CUDAGraph`` = hipGraph on ROCm) and replayed.  Each step is the
+    fused ``ldm_sample_step`` (in-projection, n_blocks residual blocks, out-projection with
+    the DDPM update in its epilogue)."""
+
+    def __init__(self, denoiser: MLPDenoiser, schedule: DDPMSchedule, n: int, *,
+                 steps: Optional[int] = None, dtype: str = "bf16", device=None,
+                 use_graph: bool = True):
+        self.device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
+        self.model, self.schedule, self.n = denoiser, schedule, n
+        self.T = schedule.T
+        self.steps = self.T if steps is None else int(steps)
+        if not (1 <= self.steps <= self.T):
+            raise ValueError("steps must be in [1, T]")
+        self.dev = denoiser.device_pack(dtype, self.device)
+        self.sd = schedule.device(self.device)
+        D, H = denoiser.D, denoiser.H
+        self.x = [torch.empty(n, D, device=self.device) for _ in range(2)]
+        self.noise = torch.empty(self.T, n, D, device=self.device)
+        self.ws = torch.empty(2 * n * H, device=self.device)
+        self.graph = None
+        self.use_graph = use_graph
+
+    def _loop(self) -> None:
+        cur = 0
+        for t in range(self.T - 1, self.T - 1 - self.steps, -1):
+            ops.sample_step(self.dev["desc"], self.sd["desc"], self.x[cur], self.noise[t], t,
+                            self.x[cur ^ 1], self.ws)
+            cur ^= 1
+
+    @property
+    def result(self) -> torch.Tensor:
+        return self.x[self.steps & 1]
+
+    def run(self, x_T: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
+        self.x[0].copy_(x_T)
+        self.noise[:noise.shape[0]].copy_(noise)
+        if not self.use_graph:
+            self._loop()
+            return self.result
+        if self.graph is None:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._loop()          # warm-up (module load, first-launch costs)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.x[0].copy_(x_T)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._loop()
+            self.graph = g
+        self.graph.replay()
+        return self.result
+
+
+def sample(denoiser: MLPDenoiser, schedule: DDPMSchedule, n: int, *,
+           steps: Optional[int] = None, dtype: str = "bf16", x_T: Optional[torch.Tensor] = None,
+           noise: Optional[torch.Tensor] = None, generator: Optional[torch.Generator] = None,
+           device=None, use_graph: bool = True, group=None) -> torch.Tensor:
+    """DDPM ancestral sampling (DDPM Alg. 2) of ``n`` latent codes.
+
+    ``x_T [n, D]`` and ``noise [T, n, D]`` may be given (parity mode: the same numbers the
+    CPU oracle consumes); otherwise they are drawn on the device.  With a process group the
+    batch is sharded over ranks and the latents all-gathered.
+    """
+    device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
+    world, rank = ldist.world_and_rank(group)
+    lo, hi = ldist.batch_shard(n, rank, world)
+    nl = hi - lo
+    D, T = denoiser.D, schedule.T
+    if x_T is None:
+        x_T = torch.randn(n, D, device=device, generator=generator)
+    if noise is None:
+        noise = torch.randn(T, n, D, device=device, generator=generator)
+    x_T = x_T.to(device, torch.float32)[lo:hi].contiguous()
+    noise = noise.to(device, torch.float32)[:, lo:hi].contiguous()
+    out = Sampler(denoiser, schedule, nl, steps=steps, dtype=dtype, device=device,
+                  use_graph=use_graph).run(x_T, noise).clone()
+    if world == 1:
+        return out
+    # equal shards are required by all_gather_into_tensor: pad to ceil(n/W)
+    per = -(-n // world)
+    buf = torch.zeros(per, D, device=device)
+    buf[:nl] = out
+    gathered = torch.empty(world * per, D, device=device)
+    torch.distributed.all_gather_into_tensor(gathered, buf, group=group)
+    rows = []
+    for r in range(world):
+        a, b = ldist.batch_shard(n, r, world)
+        rows.append(gathered[r * per:r * per + (b - a)])
+    return torch.cat(rows)
+
+
+# ---------------------------------------------------------------------------------- train
+@dataclass
+class TrainState:
+    step: int = 0
+    losses: List[float] = field(default_factory=list)
+    optimizer: Optional[torch.optim.Optimizer] = None
+    masters: Optional[Dict[str, torch.Tensor]] = None
+
+
+def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
+               t: torch.Tensor, eps: torch.Tensor, *, dtype: str = "bf16",
+               grads: Optional[Dict[str, torch.Tensor]] = None,
+               group=None) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """One DDPM training forward/backward (Alg. 1): q_sample -> eps_hat -> MSE -> grads.
+    Returns (loss [1], grads) -- gradients are averaged over ranks when a group is given."""
+    device = x0.device
+    dev = denoiser.device_pack(dtype, device, with_tables=False)
+    sd = schedule.device(device)
+    xt = ops.q_sample(sd["desc"], x0.contiguous(), eps.contiguous(), t.to(torch.int32).contiguous())
+    eps_hat, sv = ops.denoiser_forward_train(denoiser, dev, xt, t.to(torch.int32).contiguous())
+    loss, g_out = ops.eps_mse_loss(eps_hat, eps.contiguous())
+    if grads is None:
+        grads = {n: torch.empty_like(denoiser.params[n], device=device) for n in denoiser.names()}
+    ops.denoiser_backward_train(denoiser, dev, sv, g_out, grads)
+    ldist.allreduce_mean_([grads[n] for n in denoiser.names()], group=group)
+    return loss, grads
+
+
+def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, *, steps: int,
+          batch: Optional[int] = None, lr: float = 1e-4, weight_decay: float = 0.0,
+          dtype: str = "bf16", generator: Optional[torch.Generator] = None,
+          state: Optional[TrainState] = None, group=None) -> TrainState:
+    """Train the denoiser on latent codes ``[M, D]`` (DDPM Alg. 1, eps-prediction, AdamW).
+
+    fp32 master weights; forward/backward GEMMs read ``dtype`` copies (bf16 by default).
+    Data parallel over the group's ranks (each rank its shard of every batch; gradients
+    all-reduced in one bucket).
+    """
+    capi.require_device(latents)
+    device = latents.device
+    world, rank = ldist.world_and_rank(group)
+    M, D = latents.shape
+    batch = M if batch is None else batch
+    if state is None:
+        denoiser.to_device(device)
+        state = TrainState()
+        state.masters = {n: denoiser.params[n] for n in denoiser.names()}
+        for v in state.masters.values():
+            v.requires_grad_(False)
+        state.optimizer = torch.optim.AdamW(list(state.masters.values()), lr=lr,
+                                            weight_decay=weight_decay)
+    grads = {n: torch.empty_like(v) for n, v in state.masters.items()}
+    T = schedule.T
+    for _ in range(steps):
+        idx = torch.randint(0, M, (batch,), device=device, generator=generator) \
+            if batch != M else torch.arange(M, device=device)
+        t = torch.randint(0, T, (batch,), device=device, generator=generator, dtype=torch.int32)
+        eps = torch.randn(batch, D, device=device, generator=generator)
+        lo, hi = ldist.batch_shard(batch, rank, world)
+        x0 = latents[idx[lo:hi]].contiguous()
+        loss, grads = train_step(denoiser, schedule, x0, t[lo:hi], eps[lo:hi], dtype=dtype,
+                                 grads=grads, group=group)
+        for n, p in state.masters.items():
+            p.grad = grads[n]
+        state.optimizer.step()
+        denoiser.invalidate()
+        state.step += 1
+        state.losses.append(loss)
+    state.losses = [float(l) if isinstance(l, torch.Tensor) else l for l in state.losses]
+    return state

@@ -1,0 +1,331 @@
+"""Thin wrappers: one Python function per ``libldm_sdf.so`` entry point (include/ldm_sdf.h).
+
+Every wrapper checks devices/shapes/contiguity on the host, launches on torch's current
+stream and raises ``LdmError`` on a non-zero status.  No compute happens here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _capi as capi
+
+
+def _contig(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if t is not None and not t.is_contiguous():
+            raise capi.LdmError("tensors passed to libldm_sdf must be contiguous")
+
+
+def _f32(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if t is not None and t.dtype != torch.float32:
+            raise capi.LdmError(f"expected float32, got {t.dtype}")
+
+
+# ---------------------------------------------------------------------------------------- A1
+def grid_coords(N: int, k0: int = 0, k1: Optional[int] = None, bbox=(-1.0, 1.0),
+                device=None) -> torch.Tensor:
+    """Device grid coordinates ``[(k1-k0)*N*N, 3]`` (z slowest, x fastest)."""
+    k1 = N if k1 is None else k1
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((k1 - k0) * N * N, 3, device=device, dtype=torch.float32)
+    vs, origin = voxel_size(N, bbox), float(bbox[0])
+    capi.check(capi.load().ldm_grid_coords(N, k0, k1, vs, origin, out.data_ptr(),
+                                           capi.stream_handle(device)), "ldm_grid_coords")
+    return out
+
+
+def voxel_size(N: int, bbox=(-1.0, 1.0)) -> float:
+    """fl32((hi - lo)/(N - 1)), computed on the host (A1; never divided on the device)."""
+    import numpy as np
+    return float(np.float32((bbox[1] - bbox[0]) / (N - 1))) if N > 1 else 0.0
+
+
+# ---------------------------------------------------------------------------------------- A2
+def decoder_fold(desc: capi.Decoder, z: torch.Tensor) -> torch.Tensor:
+    capi.require_device(z)
+    _f32(z)
+    _contig(z)
+    B = z.shape[0]
+    beta = torch.empty(B, 2, desc.hidden, device=z.device, dtype=torch.float32)
+    capi.check(capi.load().ldm_decoder_fold(C.byref(desc), z.data_ptr(), B, beta.data_ptr(),
+                                            capi.stream_handle(z.device)), "ldm_decoder_fold")
+    return beta
+
+
+# ---------------------------------------------------------------------------------------- A3
+def decoder_grid_fwd(desc: capi.Decoder, beta: torch.Tensor, N: int, k0: int, k1: int,
+                     bbox=(-1.0, 1.0), out: Optional[torch.Tensor] = None,
+                     ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    capi.require_device(beta)
+    _contig(beta)
+    B = beta.shape[0]
+    npts = (k1 - k0) * N * N
+    if out is None:
+        out = torch.empty(B, k1 - k0, N, N, device=beta.device, dtype=torch.float32)
+    if out.numel() != B * npts or not out.is_contiguous():
+        raise capi.LdmError("decoder_grid_fwd: out must be a contiguous [B, k1-k0, N, N]")
+    lib = capi.load()
+    wsb = lib.ldm_workspace_bytes(capi.LDM_OP_DECODER_GRID, B, N, desc.dtype)
+    if ws is None or ws.numel() < wsb:
+        ws = torch.empty(max(wsb, 16), device=beta.device, dtype=torch.uint8)
+    capi.check(lib.ldm_decoder_grid_fwd(C.byref(desc), beta.data_ptr(), B, N, k0, k1,
+                                        voxel_size(N, bbox), float(bbox[0]), out.data_ptr(),
+                                        ws.data_ptr(), ws.numel(),
+                                        capi.stream_handle(beta.device)), "ldm_decoder_grid_fwd")
+    return out
+
+
+def decoder_points_fwd(desc: capi.Decoder, beta: torch.Tensor, xyz: torch.Tensor,
+                       out: Optional[torch.Tensor] = None,
+                       ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    capi.require_device(beta, xyz)
+    _f32(xyz)
+    _contig(beta, xyz)
+    B, P = xyz.shape[0], xyz.shape[1]
+    if xyz.shape != (B, P, 3) or beta.shape[0] != B:
+        raise capi.LdmError("decoder_points_fwd: xyz must be [B, P, 3] matching beta [B, 2, H]")
+    if out is None:
+        out = torch.empty(B, P, device=xyz.device, dtype=torch.float32)
+    lib = capi.load()
+    wsb = lib.ldm_workspace_bytes(capi.LDM_OP_DECODER_POINTS, B, P, desc.dtype)
+    if ws is None or ws.numel() < wsb:
+        ws = torch.empty(max(wsb, 16), device=xyz.device, dtype=torch.uint8)
+    capi.check(lib.ldm_decoder_points_fwd(C.byref(desc), beta.data_ptr(), xyz.data_ptr(), B, P,
+                                          out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                          capi.stream_handle(xyz.device)),
+               "ldm_decoder_points_fwd")
+    return out
+
+
+# ---------------------------------------------------------------------------------------- A8/A9
+def ddpm_step(sched_desc: capi.Sched, x: torch.Tensor, eps: torch.Tensor,
+              z: Optional[torch.Tensor], t: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    capi.require_device(x, eps)
+    _contig(x, eps, z)
+    out = torch.empty_like(x) if out is None else out
+    capi.check(capi.load().ldm_ddpm_step(C.byref(sched_desc), x.data_ptr(), eps.data_ptr(),
+                                         capi.ptr(z), int(t), x.numel(), out.data_ptr(),
+                                         capi.stream_handle(x.device)), "ldm_ddpm_step")
+    return out
+
+
+def q_sample(sched_desc: capi.Sched, x0: torch.Tensor, eps: torch.Tensor,
+             t: torch.Tensor) -> torch.Tensor:
+    capi.require_device(x0, eps, t)
+    _contig(x0, eps, t)
+    if t.dtype != torch.int32:
+        raise capi.LdmError("t must be int32")
+    B, D = x0.shape
+    out = torch.empty_like(x0)
+    capi.check(capi.load().ldm_q_sample(C.byref(sched_desc), x0.data_ptr(), eps.data_ptr(),
+                                        t.data_ptr(), B, D, out.data_ptr(),
+                                        capi.stream_handle(x0.device)), "ldm_q_sample")
+    return out
+
+
+def eps_mse_loss(eps_hat: torch.Tensor, eps: torch.Tensor,
+                 with_grad: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    capi.require_device(eps_hat, eps)
+    _contig(eps_hat, eps)
+    loss = torch.empty(1, device=eps.device, dtype=torch.float32)
+    grad = torch.empty_like(eps_hat) if with_grad else None
+    capi.check(capi.load().ldm_eps_mse_loss(eps_hat.data_ptr(), eps.data_ptr(), eps.numel(),
+                                            loss.data_ptr(), capi.ptr(grad),
+                                            capi.stream_handle(eps.device)), "ldm_eps_mse_loss")
+    return loss, grad
+
+
+# ---------------------------------------------------------------------------------------- A6
+def denoiser_fwd_uniform_t(desc: capi.Denoiser, x: torch.Tensor, t: int,
+                           ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    capi.require_device(x)
+    _contig(x)
+    B = x.shape[0]
+    if ws is None:
+        ws = torch.empty(2 * B * desc.H, device=x.device, dtype=torch.float32)
+    eps = torch.empty(B, desc.D, device=x.device, dtype=torch.float32)
+    capi.check(capi.load().ldm_denoiser_fwd_uniform_t(C.byref(desc), x.data_ptr(), int(t), B,
+                                                      eps.data_ptr(), ws.data_ptr(),
+                                                      capi.stream_handle(x.device)),
+               "ldm_denoiser_fwd_uniform_t")
+    return eps
+
+
+def sample_step(desc: capi.Denoiser, sched_desc: capi.Sched, x: torch.Tensor,
+                z: Optional[torch.Tensor], t: int, out: torch.Tensor, ws: torch.Tensor) -> None:
+    capi.check(capi.load().ldm_sample_step(C.byref(desc), C.byref(sched_desc), x.data_ptr(),
+                                           capi.ptr(z), int(t), x.shape[0], out.data_ptr(),
+                                           ws.data_ptr(), capi.stream_handle(x.device)),
+               "ldm_sample_step")
+
+
+# ---------------------------------------------------------------------------------------- GEMM
+def linear(X: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, *, epi: int = capi.EPI_BIAS,
+           bias: Optional[torch.Tensor] = None, X2: Optional[torch.Tensor] = None,
+           W2: Optional[torch.Tensor] = None, R: Optional[torch.Tensor] = None,
+           A_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``Y = epi(X @ W.T [+ X2 @ W2.T] + bias)`` on strided 2-D views (any strides).
+
+    X: [Bn, K] view, W: [M, K] view (fp32 or bf16), Y: [Bn, M] view.  Transposed views give
+    the backward products, e.g. ``linear(G.T, X.T, dW)`` = ``G^T X``.
+    """
+    Bn, K = X.shape
+    M = W.shape[0]
+    if W.shape[1] != K or Y.shape != (Bn, M):
+        raise capi.LdmError(f"linear: shapes X{tuple(X.shape)} W{tuple(W.shape)} Y{tuple(Y.shape)}")
+    a = capi.LinearArgs()
+    a.Bn, a.M, a.K = Bn, M, K
+    a.epi = epi
+    if W.dtype == torch.bfloat16:
+        a.w_dtype = capi.LDM_BF16
+    elif W.dtype == torch.float32:
+        a.w_dtype = capi.LDM_F32
+    else:
+        raise capi.LdmError(f"linear: W dtype {W.dtype}")
+    _f32(X, Y, bias, R, A_out, X2)
+    a.X, a.sxb, a.sxk = X.data_ptr(), X.stride(0), X.stride(1)
+    a.W, a.swm, a.swk = W.data_ptr(), W.stride(0), W.stride(1)
+    if X2 is not None:
+        if W2 is None or W2.dtype != W.dtype or X2.shape[0] != Bn or W2.shape != (M, X2.shape[1]):
+            raise capi.LdmError("linear: bad second segment")
+        if (X2.stride(1) == 1) != (X.stride(1) == 1) or (W2.stride(1) == 1) != (W.stride(1) == 1):
+            raise capi.LdmError("linear: both segments must share contiguity")
+        a.K2 = X2.shape[1]
+        a.X2, a.sx2b, a.sx2k = X2.data_ptr(), X2.stride(0), X2.stride(1)
+        a.W2, a.sw2m, a.sw2k = W2.data_ptr(), W2.stride(0), W2.stride(1)
+    if bias is not None:
+        a.bias = bias.data_ptr()
+    if R is not None:
+        if R.stride(1) != 1:
+            raise capi.LdmError("linear: R rows must be contiguous")
+        a.R, a.srb = R.data_ptr(), R.stride(0)
+    a.Y, a.syb, a.sym = Y.data_ptr(), Y.stride(0), Y.stride(1)
+    if A_out is not None:
+        if A_out.stride(1) != 1:
+            raise capi.LdmError("linear: A_out rows must be contiguous")
+        a.A_out, a.sab = A_out.data_ptr(), A_out.stride(0)
+    capi.check(capi.load().ldm_linear(C.byref(a), capi.stream_handle(Y.device)), "ldm_linear")
+    return Y
+
+
+def silu_bwd(dy: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _contig(dy, a)
+    out = torch.empty_like(dy) if out is None else out
+    capi.check(capi.load().ldm_silu_bwd(dy.data_ptr(), a.data_ptr(), dy.numel(), out.data_ptr(),
+                                        capi.stream_handle(dy.device)), "ldm_silu_bwd")
+    return out
+
+
+def colsum(G: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    _contig(G)
+    Bn, M = G.shape
+    capi.check(capi.load().ldm_colsum(G.data_ptr(), Bn, M, out.data_ptr(), int(accumulate),
+                                      capi.stream_handle(G.device)), "ldm_colsum")
+    return out
+
+
+def gather_rows(table: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    _contig(table, idx)
+    Bn, Cc = idx.shape[0], table.shape[1]
+    out = torch.empty(Bn, Cc, device=table.device, dtype=torch.float32)
+    capi.check(capi.load().ldm_gather_rows(table.data_ptr(), idx.data_ptr(), Bn, Cc,
+                                           out.data_ptr(), capi.stream_handle(table.device)),
+               "ldm_gather_rows")
+    return out
+
+
+# ---------------------------------------------------------------------------------------- A5
+def temb_forward(dev: Dict[str, object], e: torch.Tensor, H: int,
+                 save: Optional[dict] = None) -> torch.Tensor:
+    """temb = Wt2 SiLU(Wt1 e + bt1) + bt2 for a batch of embeddings e [Bn, TE]."""
+    Bn = e.shape[0]
+    u = torch.empty(Bn, H, device=e.device, dtype=torch.float32)
+    a_t = torch.empty_like(u) if save is not None else None
+    linear(e, dev["Wt1"], u, epi=capi.EPI_SILU, bias=dev["bt1"], A_out=a_t)
+    temb = torch.empty(Bn, H, device=e.device, dtype=torch.float32)
+    linear(u, dev["Wt2"], temb, epi=capi.EPI_BIAS, bias=dev["bt2"])
+    if save is not None:
+        save.update(e=e, u=u, a_t=a_t, temb=temb)
+    return temb
+
+
+def build_e_tables(model, dev: Dict[str, object], dtype: str) -> List[torch.Tensor]:
+    """A5 inference tables: ``E_k[t] = U_k temb(t) + b_k`` for every t (fp32 [T, H])."""
+    H, T = model.H, model.T
+    emb = dev["emb_table"]
+    temb = temb_forward(dev, emb, H)
+    tabs = []
+    for k in range(model.n_blocks):
+        W = dev[f"Wblk{k}"]
+        E = torch.empty(T, H, device=emb.device, dtype=torch.float32)
+        linear(temb, W[:, H:], E, epi=capi.EPI_BIAS, bias=dev[f"bblk{k}"])
+        tabs.append(E)
+    return tabs
+
+
+# ---------------------------------------------------------------------------------------- A6/A7
+def denoiser_forward_train(model, dev: Dict[str, object], xt: torch.Tensor,
+                           t: torch.Tensor) -> Tuple[torch.Tensor, dict]:
+    """Training forward (per-sample t) saving what the backward needs."""
+    H, nb = model.H, model.n_blocks
+    Bn = xt.shape[0]
+    sv: dict = {"xt": xt}
+    e = gather_rows(dev["emb_table"], t)
+    temb = temb_forward(dev, e, H, save=sv)
+    h = torch.empty(Bn, H, device=xt.device, dtype=torch.float32)
+    linear(xt, dev["Win"], h, epi=capi.EPI_BIAS, bias=dev["bin"])
+    hs, pre = [h], []
+    for k in range(nb):
+        W = dev[f"Wblk{k}"]
+        a = torch.empty(Bn, H, device=xt.device, dtype=torch.float32)
+        hn = torch.empty(Bn, H, device=xt.device, dtype=torch.float32)
+        linear(h, W[:, :H], hn, epi=capi.EPI_RESID_SILU, bias=dev[f"bblk{k}"], X2=temb,
+               W2=W[:, H:], R=h, A_out=a)
+        hs.append(hn)
+        pre.append(a)
+        h = hn
+    eps_hat = torch.empty(Bn, model.D, device=xt.device, dtype=torch.float32)
+    linear(h, dev["Wout"], eps_hat, epi=capi.EPI_BIAS, bias=dev["bout"])
+    sv.update(hs=hs, pre=pre)
+    return eps_hat, sv
+
+
+def denoiser_backward_train(model, dev: Dict[str, object], sv: dict,
+                            g_out: torch.Tensor, grads: Dict[str, torch.Tensor]) -> None:
+    """A7: gradients of every parameter given dL/d eps_hat (written into ``grads``)."""
+    H, nb = model.H, model.n_blocks
+    Bn = g_out.shape[0]
+    hs, pre = sv["hs"], sv["pre"]
+    # eps_hat = Wout h + bout
+    linear(g_out.T, hs[-1].T, grads["Wout"])
+    colsum(g_out, grads["bout"])
+    dh = torch.empty(Bn, H, device=g_out.device, dtype=torch.float32)
+    linear(g_out, dev["Wout"].T, dh)
+    dtemb = torch.zeros(Bn, H, device=g_out.device, dtype=torch.float32)
+    g = torch.empty_like(dh)
+    for k in range(nb - 1, -1, -1):
+        W = dev[f"Wblk{k}"]
+        silu_bwd(dh, pre[k], out=g)                                  # g = dh * silu'(a)
+        dW = grads[f"Wblk{k}"]
+        linear(g.T, hs[k].T, dW[:, :H])                              # dW_k = g^T h_k
+        linear(g.T, sv["temb"].T, dW[:, H:])                         # dU_k = g^T temb
+        colsum(g, grads[f"bblk{k}"])
+        linear(g, W[:, H:].T, dtemb, epi=capi.EPI_ACCUM)             # dtemb += g U_k
+        dh_new = torch.empty_like(dh)
+        linear(g, W[:, :H].T, dh_new, epi=capi.EPI_ADD_R, R=dh)      # dh = dh + g W_k
+        dh = dh_new
+    # h0 = Win xt + bin
+    linear(dh.T, sv["xt"].T, grads["Win"])
+    colsum(dh, grads["bin"])
+    # temb = Wt2 u + bt2 ; u = silu(a_t) ; a_t = Wt1 e + bt1
+    linear(dtemb.T, sv["u"].T, grads["Wt2"])
+    colsum(dtemb, grads["bt2"])
+    du = torch.empty(Bn, H, device=g_out.device, dtype=torch.float32)
+    linear(dtemb, dev["Wt2"].T, du)
+    gt = silu_bwd(du, sv["a_t"])
+    linear(gt.T, sv["e"].T, grads["Wt1"])
+    colsum(gt, grads["bt1"])

@@ -1,0 +1,96 @@
+"""Generate the committed golden fixtures under tests/golden/ from the CPU oracle.
+
+The reference (/root/reference) ships no code and no fixtures, so these vectors are the
+oracle's own outputs (fp64 unless noted) on fixed seeds: they pin the GPU path to the oracle
+on the GPU box, and ``tests/test_golden.py`` re-derives them on the CPU so that the oracle
+and the fixtures cannot drift apart silently.
+
+Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import ref_cpu as R  # noqa: E402
+
+DEC_SEED, LAT_SEED, PTS_SEED = 1234, 0, 7
+DEN_SEED, SAMPLE_SEED = 4321, 11
+
+
+def decoder_case():
+    p = R.make_decoder_params(seed=DEC_SEED)
+    z = (torch.randn(2, 256, generator=torch.Generator().manual_seed(LAT_SEED),
+                     dtype=torch.float64) * 0.1)
+    N = 32
+    grid = R.grid_coords_np(N)
+    sdf_grid = R.decoder_forward(p, z, torch.from_numpy(grid).double()).numpy()
+    g = torch.Generator().manual_seed(PTS_SEED)
+    pts = (torch.rand(2, 1000, 3, generator=g, dtype=torch.float64) * 2.2 - 1.1).float()
+    sdf_pts = R.decoder_forward(p, z, pts.double()).numpy()
+    return dict(z=z.float().numpy(), N=np.int32(N), grid=grid, sdf_grid=sdf_grid.astype(np.float64),
+                pts=pts.numpy(), sdf_pts=sdf_pts)
+
+
+def widen_case():
+    p = R.make_decoder_params(L=1024, widen_skip=True, seed=DEC_SEED + 1)
+    z = (torch.randn(1, 1024, generator=torch.Generator().manual_seed(LAT_SEED + 1),
+                     dtype=torch.float64) * 0.1)
+    g = torch.Generator().manual_seed(PTS_SEED + 1)
+    pts = (torch.rand(1, 777, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
+    return dict(z=z.float().numpy(), pts=pts.numpy(),
+                sdf_pts=R.decoder_forward(p, z, pts.double()).numpy())
+
+
+def sampling_case(steps=20, B=4):
+    p = R.make_denoiser_params(seed=DEN_SEED)
+    tab = R.ddpm_tables(1000)
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    g = torch.Generator().manual_seed(SAMPLE_SEED)
+    x_T = torch.randn(B, 256, generator=g, dtype=torch.float32)
+    noise = torch.zeros(1000, B, 256, dtype=torch.float32)
+    noise[1000 - steps:] = torch.randn(steps, B, 256, generator=g, dtype=torch.float32)
+    x, traj = R.sample_loop(p, tab, emb, x_T.double(), noise.double(), steps=steps,
+                            return_traj=True)
+    eps0 = R.denoiser_forward(p, x_T.double(), torch.full((B,), 999), emb)
+    return dict(x_T=x_T.numpy(), noise_tail=noise[1000 - steps:].numpy(),
+                traj=torch.stack(traj).numpy(), eps_t999=eps0.numpy(), steps=np.int32(steps))
+
+
+def train_case(B=64):
+    p = R.make_denoiser_params(seed=DEN_SEED)
+    tab = R.ddpm_tables(1000)
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    g = torch.Generator().manual_seed(SAMPLE_SEED + 1)
+    x0 = torch.randn(B, 256, generator=g, dtype=torch.float32) * 0.5
+    eps = torch.randn(B, 256, generator=g, dtype=torch.float32)
+    t = torch.randint(0, 1000, (B,), generator=g)
+    loss, grads = R.train_step_grads(p, tab, emb, x0.double(), eps.double(), t)
+    out = dict(x0=x0.numpy(), eps=eps.numpy(), t=t.numpy().astype(np.int32),
+               loss=np.float64(loss))
+    for k, v in grads.items():
+        out["g_" + k] = (v if k.startswith("b") else v[:8]).numpy()   # bias grads, W[:8]
+        out["gnorm_" + k] = np.float64(v.norm())
+    return out
+
+
+CASES = {"decoder_small": decoder_case, "decoder_widen": widen_case,
+         "sampling_20": sampling_case, "train_step": train_case}
+
+
+def main():
+    for name, fn in CASES.items():
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **fn())
+        print(f"wrote {path} ({os.path.getsize(path)} bytes)")
+
+
+if __name__ == "__main__":
+    main()

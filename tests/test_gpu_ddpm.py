@@ -1,0 +1,170 @@
+"""T2 DDPM-side parity on the MI355X: step / q_sample bit-exact vs the fp32 oracle, the fused
+linear kernel vs torch, denoiser forward + 20-step sampling trajectory + training gradients
+vs the fp64 oracle / goldens."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ldm_sdf
+    ldm_sdf.load_library()
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def den():
+    from ldm_sdf import MLPDenoiser
+    from oracle import ref_cpu as R
+    p = R.make_denoiser_params(seed=4321)
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"] = p.Wblk[k]
+        params[f"bblk{k}"] = p.bblk[k]
+    return MLPDenoiser(params=params), p
+
+
+def test_ddpm_step_bit_exact(dev):
+    from ldm_sdf import DDPMSchedule, ops
+    from oracle import ref_cpu as R
+    sch = DDPMSchedule()
+    tab = R.ddpm_tables()
+    g = torch.Generator().manual_seed(0)
+    x, e, z = (torch.randn(8, 256, generator=g) for _ in range(3))
+    for t in (0, 1, 500, 999):
+        got = ops.ddpm_step(sch.device(dev)["desc"], x.to(dev), e.to(dev), z.to(dev), t).cpu()
+        want = R.ddpm_step(tab, x, e, z, t)
+        assert torch.equal(got, want), t
+
+
+def test_q_sample_bit_exact(dev):
+    from ldm_sdf import DDPMSchedule, ops
+    from oracle import ref_cpu as R
+    sch = DDPMSchedule()
+    tab = R.ddpm_tables()
+    g = torch.Generator().manual_seed(1)
+    x0, e = torch.randn(64, 256, generator=g), torch.randn(64, 256, generator=g)
+    t = torch.randint(0, 1000, (64,), generator=g, dtype=torch.int32)
+    got = ops.q_sample(sch.device(dev)["desc"], x0.to(dev), e.to(dev), t.to(dev)).cpu()
+    assert torch.equal(got, R.q_sample(tab, x0, e, t))
+
+
+def test_loss_and_grad(dev):
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(2)
+    a, b = torch.randn(1000, 256, generator=g), torch.randn(1000, 256, generator=g)
+    loss, grad = ops.eps_mse_loss(a.to(dev), b.to(dev))
+    ad = a.double()
+    want = ((ad - b.double()) ** 2).mean()
+    assert abs(float(loss) - float(want)) / float(want) < 1e-6
+    assert torch.allclose(grad.cpu().double(), 2 * (ad - b.double()) / a.numel(), rtol=1e-6,
+                          atol=1e-12)
+
+
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Bn,M,K,K2", [(1000, 1024, 1024, 0), (37, 100, 70, 0),
+                                       (64, 256, 256, 128), (1, 8, 16, 0)])
+def test_linear_forward_and_transposes(dev, wdt, Bn, M, K, K2):
+    from ldm_sdf import ops, _capi as capi
+    g = torch.Generator().manual_seed(Bn + M)
+    X = torch.randn(Bn, K, generator=g).to(dev)
+    W = torch.randn(M, K, generator=g).to(dev).to(wdt)
+    b = torch.randn(M, generator=g).to(dev)
+    Y = torch.empty(Bn, M, device=dev)
+    kw = {}
+    ref = X.double() @ W.double().T + b.double()
+    if K2:
+        X2 = torch.randn(Bn, K2, generator=g).to(dev)
+        W2 = torch.randn(M, K2, generator=g).to(dev).to(wdt)
+        kw = dict(X2=X2, W2=W2)
+        ref = ref + X2.double() @ W2.double().T
+    ops.linear(X, W, Y, bias=b, **kw)
+    tol = 1e-5 * (K + K2) ** 0.5
+    assert (Y.double() - ref).abs().max() < tol
+    # transposed operands (G^T X and G W forms)
+    G = torch.randn(Bn, M, generator=g).to(dev)
+    dW = torch.empty(M, K, device=dev)
+    ops.linear(G.T, X.T, dW)
+    assert (dW.double() - G.double().T @ X.double()).abs().max() < 1e-5 * Bn ** 0.5
+    dX = torch.empty(Bn, K, device=dev)
+    ops.linear(G, W.T, dX)
+    assert (dX.double() - G.double() @ W.double()).abs().max() < 1e-5 * M ** 0.5
+    # epilogues
+    R_ = torch.randn(Bn, M, generator=g).to(dev)
+    A = torch.empty(Bn, M, device=dev)
+    ops.linear(X, W, Y, epi=capi.EPI_RESID_SILU, bias=b, R=R_, A_out=A, **kw)
+    pre = ref
+    assert (A.double() - pre).abs().max() < tol
+    want = R_.double() + pre * torch.sigmoid(pre)
+    assert (Y.double() - want).abs().max() < 2 * tol
+    Y0 = torch.randn(Bn, M, generator=g).to(dev)
+    Y1 = Y0.clone()
+    ops.linear(X, W, Y1, epi=capi.EPI_ACCUM, **kw)
+    assert (Y1.double() - (Y0.double() + ref - b.double())).abs().max() < tol
+
+
+def test_denoiser_forward_vs_golden(dev, den):
+    from ldm_sdf import ops
+    model, p = den
+    g = dict(np.load(os.path.join(GOLD, "sampling_20.npz")))
+    pk = model.device_pack("fp32", dev)
+    eps = ops.denoiser_fwd_uniform_t(pk["desc"], torch.from_numpy(g["x_T"]).to(dev), 999)
+    want = g["eps_t999"]
+    err = np.abs(eps.cpu().double().numpy() - want).max()
+    assert err < 1e-4 * max(1.0, np.abs(want).max()), err
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_sampling_20_steps_vs_golden(dev, den, use_graph):
+    import ldm_sdf
+    model, p = den
+    g = dict(np.load(os.path.join(GOLD, "sampling_20.npz")))
+    steps = int(g["steps"])
+    noise = torch.zeros(1000, 4, 256)
+    noise[1000 - steps:] = torch.from_numpy(g["noise_tail"])
+    x = ldm_sdf.sample(model, ldm_sdf.DDPMSchedule(), 4, steps=steps, dtype="fp32",
+                       x_T=torch.from_numpy(g["x_T"]), noise=noise, device=dev,
+                       use_graph=use_graph)
+    want = g["traj"][-1]
+    err = np.abs(x.cpu().double().numpy() - want).max()
+    assert err < 1e-4, err
+
+
+def test_sampling_graph_equals_eager_bf16(dev, den):
+    import ldm_sdf
+    model, _ = den
+    gen = torch.Generator().manual_seed(5)
+    xT = torch.randn(8, 256, generator=gen)
+    noise = torch.randn(1000, 8, 256, generator=gen)
+    sch = ldm_sdf.DDPMSchedule()
+    a = ldm_sdf.sample(model, sch, 8, steps=50, x_T=xT, noise=noise, device=dev, use_graph=False)
+    b = ldm_sdf.sample(model, sch, 8, steps=50, x_T=xT, noise=noise, device=dev, use_graph=True)
+    assert torch.equal(a, b)
+    assert torch.isfinite(a).all()
+
+
+def test_train_step_grads_vs_golden(dev, den):
+    import ldm_sdf
+    model, _ = den
+    g = dict(np.load(os.path.join(GOLD, "train_step.npz")))
+    model.to_device(dev)
+    loss, grads = ldm_sdf.train_step(model, ldm_sdf.DDPMSchedule(),
+                                     torch.from_numpy(g["x0"]).to(dev),
+                                     torch.from_numpy(g["t"]).to(dev),
+                                     torch.from_numpy(g["eps"]).to(dev), dtype="fp32")
+    assert abs(float(loss) - float(g["loss"])) / float(g["loss"]) < 1e-5
+    for k, v in grads.items():
+        want_norm = float(g["gnorm_" + k])
+        assert abs(float(v.double().norm()) - want_norm) <= 1e-4 * want_norm + 1e-9, k
+        want = g["g_" + k]
+        got = v.cpu().double().numpy()
+        got = got if k.startswith("b") else got[:8]
+        assert np.abs(got - want).max() <= 1e-4 * np.abs(want).max() + 1e-9, k

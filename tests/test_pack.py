@@ -1,0 +1,68 @@
+"""Host packing (C4) checked on the CPU: the fragment-level emulation of the MFMA kernel
+(tests/mfma_emulator.py) fed with ldm_sdf.pack output must reproduce the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from ldm_sdf import pack
+from oracle import ref_cpu as R
+from tests.mfma_emulator import emulate
+
+
+def test_perm_is_accumulator_row_order():
+    # element j of lane half h of k-step 2i+s is accumulator row 16s + 8(j>>2) + 4h + (j&3)
+    for h in range(2):
+        for j in range(8):
+            assert pack.PERM[8 * h + j] == 8 * (j >> 2) + 4 * h + (j & 3)
+    assert sorted(pack.PERM.tolist()) == list(range(16))
+
+
+@pytest.mark.parametrize("sw", [253, 512])
+def test_stage_plan_matches_kernel_constants(sw):
+    S = pack.skip_pad(sw)
+    plan = pack.stage_plan(sw)
+    base4 = 2 + 66 + 66 + (S // 256) * 33
+    assert len(plan) == base4 + 2 * (S // 16 + 1) + 3 * 66      # csrc dec_n_stages
+    per = [i for i, s in enumerate(plan) if s.per_shape]
+    assert per == [0, 1, base4 + S // 16, base4 + 2 * (S // 16) + 1]   # kernel aux4a/aux4b
+
+
+def test_w_last_permutation_roundtrip():
+    w = torch.arange(512, dtype=torch.float32)
+    wl = pack.permute_w_last(w)
+    assert sorted(wl.tolist()) == list(range(512))
+
+
+def test_fp32_blob_size():
+    p = R.make_decoder_params()
+    blob = pack.pack_f32_blob(pack.canonical_pieces(p.weights, p.biases, 256))
+    # W1..W7 (5 of 512x512, W3 512x253, W4 253x512) + b1,b2,b3(253),b4(zeros),b5,b6,b7
+    n = 5 * 512 * 512 + 2 * 512 * 253 + 6 * 512 + 253
+    assert blob.numel() == n
+
+
+@pytest.mark.parametrize("dtype,tol", [("bf16", 1.5e-2), ("fp16", 3e-3)])
+def test_emulated_kernel_matches_oracle(dtype, tol):
+    p = R.make_decoder_params(seed=1234)
+    g = torch.Generator().manual_seed(0)
+    z = torch.randn(2, 256, generator=g, dtype=torch.float64) * 0.1
+    xyz = (torch.rand(2, 64, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
+    want = R.decoder_forward(p, z, xyz.double()).numpy()
+    packed = pack.pack_decoder(p.weights, p.biases, 256, dtype)
+    beta = R.latent_fold(p, z).float().numpy()
+    got = emulate(packed, beta, xyz.numpy(), dtype)
+    err = np.abs(got - want).max()
+    assert err < tol, err
+    # and it is not trivially close: outputs vary
+    assert want.std() > 0.005
+
+
+def test_emulated_widen_skip_fp16():
+    p = R.make_decoder_params(L=1024, widen_skip=True, seed=5)
+    g = torch.Generator().manual_seed(1)
+    z = torch.randn(1, 1024, generator=g, dtype=torch.float64) * 0.1
+    xyz = (torch.rand(1, 32, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
+    want = R.decoder_forward(p, z, xyz.double()).numpy()
+    packed = pack.pack_decoder(p.weights, p.biases, 1024, "fp16")
+    got = emulate(packed, R.latent_fold(p, z).float().numpy(), xyz.numpy(), "fp16")
+    assert np.abs(got - want).max() < 3e-3
