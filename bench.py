@@ -47,11 +47,21 @@ def parse():
     return ap.parse_args()
 
 
+def host_cores() -> int:
+    """Cores this job may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU box
+    exposes the whole machine in the mask but allots each 1-GPU job a 16-core share)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
 def cpu_baseline_decode(grid: int, budget_s: float):
-    """oracle decode (torch CPU fp32, all affine cores) of whole z-slices of the grid until
+    """oracle decode (torch CPU fp32, this job's cores) of whole z-slices of the grid until
     ``budget_s`` of work; q/s is flat in N."""
     from oracle import ref_cpu as R
-    cores = len(os.sched_getaffinity(0))
+    cores = host_cores()
     torch.set_num_threads(cores)
     p = R.make_decoder_params(seed=1234, dtype=torch.float32)
     z = torch.randn(1, 256, generator=torch.Generator().manual_seed(0)) * 0.1

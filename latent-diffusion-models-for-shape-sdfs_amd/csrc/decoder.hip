@@ -13,6 +13,7 @@
 #include "ldm_internal.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 namespace ldm {
 namespace {
@@ -148,8 +149,13 @@ constexpr int RING = 10;                  // LDS ring slots
 constexpr int DEPTH = 8;                  // stages issued ahead (DEPTH <= RING - 2)
 #define LDM_VM_STEADY 10                  // 2 * (DEPTH - 3)
 #define LDM_VM_PROLOGUE 12                // 2 * (DEPTH - 2)
+#define LDM_VM_PAIR 8                     // SCHED 1: 4 * (DEPTH/2 - 2) (pairs P+2..P+3 younger)
+#define LDM_VM_PROLOGUE_PAIR 14           // SCHED 1 prologue: 16 issued, stage 0 = oldest 2
 static_assert(2 * (DEPTH - 3) == LDM_VM_STEADY, "vmcnt");
 static_assert(2 * (DEPTH - 2) == LDM_VM_PROLOGUE, "vmcnt");
+static_assert(4 * (DEPTH / 2 - 2) == LDM_VM_PAIR && DEPTH % 2 == 0 && RING % 2 == 0, "pairs");
+static_assert(DEPTH / 2 <= RING / 2 - 1, "pair WAR distance");
+static_assert(2 * DEPTH - 2 == LDM_VM_PROLOGUE_PAIR, "vmcnt");
 constexpr int LDS_RING = RING * kStageBytes;
 constexpr int LDS_TMP = 4 * 16 * 1024;    // per-wave spill of a layer's first-pass output
 constexpr int LDS_WL = 16 * 2 * 16 * 4;   // final-layer weights (permuted)
@@ -207,6 +213,7 @@ struct DecArgs {
 struct Pipe {
     const uint8_t* blob;
     const uint8_t* aux;
+    int g;          // stage being computed (WG-local sequence number; parity drives SCHED 1)
     int islot;      // ring slot of the next issue
     int cslot;      // ring slot of the stage whose fragments are being read next
     int is;         // stage-within-tile of the next issue
@@ -257,31 +264,54 @@ __device__ __forceinline__ void read_stage(const char* smem, int slot, int lane,
     for (int i = 0; i < 8; ++i) a[i] = s[i * 64 + lane];
 }
 
-// One pipeline step: certify the next stage (vmcnt + barrier), refill the ring, prefetch
+// One pipeline step: certify the next stage(s) (vmcnt + barrier), refill the ring, prefetch
 // the next stage's fragments and run this stage's 8 MFMAs.
-template <typename T, bool FIRST>
+//   SCHED 0: one barrier + one stage of DMA per step.
+//   SCHED 1: one barrier + two stages of DMA every EVEN step (pair P = stages 2P, 2P+1; the
+//            barrier of step 2P certifies pair P+1), and the step's first MFMA is issued
+//            before the barrier so the barrier wait overlaps matrix work.  DESIGN.md §4.
+template <typename T, bool FIRST, int SCHED>
 __device__ __forceinline__ void step(Pipe& p, const char* smem, uint32_t ring_lds, int wave,
                                      int lane, u32x4 (&acur)[8], const u32x4 bfrag,
                                      f32x16 (&acc)[8]) {
-    asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_STEADY) ")\n\ts_barrier" ::: "memory");
-    pipe_issue(p, ring_lds, wave, lane);
-    p.cslot = (p.cslot + 1 == RING) ? 0 : p.cslot + 1;
-    u32x4 an[8];
-    read_stage(smem, p.cslot, lane, an);
     const f32x16 zero = {};
+    if (SCHED == 0) {
+        asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_STEADY) ")\n\ts_barrier" ::: "memory");
+        pipe_issue(p, ring_lds, wave, lane);
+        p.cslot = (p.cslot + 1 == RING) ? 0 : p.cslot + 1;
+        u32x4 an[8];
+        read_stage(smem, p.cslot, lane, an);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
+        for (int i = 0; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acur[i] = an[i];
+        for (int i = 0; i < 8; ++i) acur[i] = an[i];
+    } else {
+        acc[0] = Elem<T>::mfma(acur[0], bfrag, FIRST ? zero : acc[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((p.g & 1) == 0) {
+            asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PAIR) ")\n\ts_barrier" ::: "memory");
+            pipe_issue(p, ring_lds, wave, lane);
+            pipe_issue(p, ring_lds, wave, lane);
+        }
+        p.g++;
+        p.cslot = (p.cslot + 1 == RING) ? 0 : p.cslot + 1;
+        u32x4 an[8];
+        read_stage(smem, p.cslot, lane, an);
+#pragma unroll
+        for (int i = 1; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acur[i] = an[i];
+    }
 }
 
-template <typename T, int KS>
+template <typename T, int KS, int SCHED>
 __device__ __forceinline__ void kloop(Pipe& p, const char* smem, uint32_t ring_lds, int wave,
                                       int lane, u32x4 (&acur)[8], const u32x4 (&hb)[32],
                                       f32x16 (&acc)[8]) {
-    step<T, true>(p, smem, ring_lds, wave, lane, acur, hb[0], acc);
+    step<T, true, SCHED>(p, smem, ring_lds, wave, lane, acur, hb[0], acc);
 #pragma unroll
-    for (int ks = 1; ks < KS; ++ks) step<T, false>(p, smem, ring_lds, wave, lane, acur, hb[ks], acc);
+    for (int ks = 1; ks < KS; ++ks)
+        step<T, false, SCHED>(p, smem, ring_lds, wave, lane, acur, hb[ks], acc);
 }
 
 // ReLU in the 16-bit domain: both bf16 and f16 order like sign-magnitude, so max with +0 as
@@ -304,7 +334,7 @@ __device__ __forceinline__ void acc_to_frags(const f32x16& a, u32x4& f0, u32x4& 
     }
 }
 
-template <typename T, int S, bool POINTS>
+template <typename T, int S, bool POINTS, int SCHED>
 __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, int aux4a,
                                                           int aux4b) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_TOTAL];
@@ -322,6 +352,7 @@ __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, in
     Pipe p;
     p.blob = a.blob;
     p.aux = a.aux;
+    p.g = 0;
     p.islot = 0;
     p.cslot = 0;
     p.is = 0;
@@ -334,9 +365,14 @@ __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, in
     p.tps = a.tiles_per_shape;
     p.tstride = gridDim.x;
 
+    // prologue: SCHED 0 prefetches DEPTH-1 stages, SCHED 1 DEPTH/2 whole pairs; both then
+    // wait for stage 0 (2 x DEPTH-2 younger DMAs resp. 4 x (DEPTH/2-1) = the same 12).
 #pragma unroll 1
-    for (int j = 0; j < DEPTH - 1; ++j) pipe_issue(p, ring_lds, wave, lane);
-    asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE) ")\n\ts_barrier" ::: "memory");
+    for (int j = 0; j < (SCHED ? DEPTH : DEPTH - 1); ++j) pipe_issue(p, ring_lds, wave, lane);
+    if (SCHED)
+        asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE_PAIR) ")\n\ts_barrier" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE) ")\n\ts_barrier" ::: "memory");
     u32x4 acur[8];
     read_stage(smem, 0, lane, acur);
 
@@ -379,13 +415,13 @@ __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, in
         for (int pi = 0; pi < Passes<S>::NP; ++pi) {
             const int ks = Passes<S>::ks(pi);
             if (ks == 32) {
-                kloop<T, 32>(p, smem, ring_lds, wave, lane, acur, hb, acc);
-                step<T, false>(p, smem, ring_lds, wave, lane, acur, bfrag, acc);
+                kloop<T, 32, SCHED>(p, smem, ring_lds, wave, lane, acur, hb, acc);
+                step<T, false, SCHED>(p, smem, ring_lds, wave, lane, acur, bfrag, acc);
             } else if (ks == 16) {
-                kloop<T, 16>(p, smem, ring_lds, wave, lane, acur, hb, acc);
-                step<T, false>(p, smem, ring_lds, wave, lane, acur, bfrag, acc);
+                kloop<T, 16, SCHED>(p, smem, ring_lds, wave, lane, acur, hb, acc);
+                step<T, false, SCHED>(p, smem, ring_lds, wave, lane, acur, bfrag, acc);
             } else {
-                step<T, true>(p, smem, ring_lds, wave, lane, acur, bfrag, acc);
+                step<T, true, SCHED>(p, smem, ring_lds, wave, lane, acur, bfrag, acc);
             }
             const int mode = Passes<S>::mode(pi);
             if (mode == M_LO) {
@@ -588,18 +624,30 @@ int check_decoder(const ldm_decoder_t* w) {
     return 0;
 }
 
-template <typename T, int S>
-void launch_mfma(const DecArgs& a, bool points, hipStream_t s, int grid) {
+// Schedule variant (development A/B knob; LDM_DECODER_SCHED=0|1, default 1).
+int decoder_sched() {
+    const char* e = getenv("LDM_DECODER_SCHED");   // read per launch: same-process A/B
+    return (e && e[0] == '0') ? 0 : 1;
+}
+
+template <typename T, int S, int SCHED>
+void launch_mfma_s(const DecArgs& a, bool points, hipStream_t s, int grid) {
     const int nst = dec_n_stages(S);
     const int b4 = dec_base4(S);
     const int aux4a = b4 + S / 16;
     const int aux4b = b4 + 2 * (S / 16) + 1;
     if (points)
-        hipLaunchKernelGGL((dec_mfma_kernel<T, S, true>), dim3(grid), dim3(256), 0, s, a, nst,
-                           aux4a, aux4b);
+        hipLaunchKernelGGL((dec_mfma_kernel<T, S, true, SCHED>), dim3(grid), dim3(256), 0, s, a,
+                           nst, aux4a, aux4b);
     else
-        hipLaunchKernelGGL((dec_mfma_kernel<T, S, false>), dim3(grid), dim3(256), 0, s, a, nst,
-                           aux4a, aux4b);
+        hipLaunchKernelGGL((dec_mfma_kernel<T, S, false, SCHED>), dim3(grid), dim3(256), 0, s, a,
+                           nst, aux4a, aux4b);
+}
+
+template <typename T, int S>
+void launch_mfma(const DecArgs& a, bool points, hipStream_t s, int grid) {
+    if (decoder_sched() == 0) launch_mfma_s<T, S, 0>(a, points, s, grid);
+    else launch_mfma_s<T, S, 1>(a, points, s, grid);
 }
 
 int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int B, int npts,

@@ -1,0 +1,45 @@
+"""Same-process A/B of decoder schedule variants (cdna guide §5.4 rule 24): interleaved
+rounds, median + min per variant.  Usage: python scripts/ab_decoder.py [B] [N] [rounds]"""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "latent-diffusion-models-for-shape-sdfs_amd")]
+import torch  # noqa: E402
+import ldm_sdf  # noqa: E402
+from ldm_sdf import ops  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+VARIANTS = os.environ.get("AB_VARIANTS", "0,1").split(",")
+FLOPS = 3146752
+dev = torch.device("cuda", 0)
+dec = ldm_sdf.SDFDecoder(256, seed=1234)
+for dtype in os.environ.get("AB_DTYPES", "bf16").split(","):
+    pk = dec.device_pack(dtype, dev)
+    z = torch.randn(B, 256, device=dev) * 0.1
+    beta = ops.decoder_fold(pk["desc"], z)
+    out = torch.empty(B, N, N, N, device=dev)
+    ref = None
+    times = {v: [] for v in VARIANTS}
+    for r in range(R + 1):
+        for v in VARIANTS:
+            os.environ["LDM_DECODER_SCHED"] = v
+            e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+            e0.record()
+            ops.decoder_grid_fwd(pk["desc"], beta, N, 0, N, out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            if r > 0:
+                times[v].append(e0.elapsed_time(e1))
+            if ref is None:
+                ref = out.clone()
+            else:
+                assert torch.equal(out, ref), f"variant {v} output differs"
+    for v in VARIANTS:
+        med = statistics.median(times[v])
+        q = B * N ** 3
+        print(f"{dtype} sched={v}: median {med:.2f} ms  min {min(times[v]):.2f} ms  "
+              f"{q / med * 1e3:.3e} q/s  {q * FLOPS / med / 1e9:.1f} TF/s")
