@@ -80,8 +80,11 @@ struct Elem;
 template <>
 struct Elem<__bf16> {
     static __device__ __forceinline__ unsigned pack(float a, float b) {
-        bf16x2 v = {(__bf16)a, (__bf16)b};
-        return __builtin_bit_cast(unsigned, v);
+        // one v_cvt_pk_bf16_f32 (RNE); the element-wise {(__bf16)a, (__bf16)b} form costs two
+        // single conversions + a v_perm
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 v = {a, b};
+        return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
     }
     static __device__ __forceinline__ float round(float x) { return (float)(__bf16)x; }
     static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
@@ -220,6 +223,8 @@ struct Pipe {
     int itile;      // tile of the next issue
     int ishape;     // shape of itile
     int nst, aux4a, aux4b, n_tiles, tps, tstride;
+    const uint8_t* isrc;   // SCHED 3: source of the next issue
+    int inext;             // SCHED 3: next stage index where the source pattern changes
 };
 
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
@@ -258,11 +263,69 @@ __device__ __forceinline__ void pipe_issue(Pipe& p, uint32_t ring_lds, int wave,
     }
 }
 
+// SCHED 3 issue path: the common case is "next 8 KiB of the blob"; the source pattern only
+// changes at 8 boundaries per tile (per-shape aux stages 0,1,aux4a,aux4b; their successors;
+// the tile wrap), handled by pipe_boundary().
+__device__ __forceinline__ void pipe_boundary(Pipe& p) {
+    if (p.is == p.nst) {
+        p.is = 0;
+        p.itile += p.tstride;
+        p.ishape = p.itile / p.tps;
+    }
+    const int s = p.is;
+    const int ai = (s < 2) ? s : (s == p.aux4a ? 2 : (s == p.aux4b ? 3 : -1));
+    p.isrc = (ai >= 0) ? p.aux + ((size_t)p.ishape * 4 + ai) * kStageBytes
+                       : p.blob + (size_t)s * kStageBytes;
+    p.inext = (s < 2) ? s + 1
+            : (s < p.aux4a) ? p.aux4a
+            : (s == p.aux4a) ? p.aux4a + 1
+            : (s < p.aux4b) ? p.aux4b
+            : (s == p.aux4b) ? p.aux4b + 1 : p.nst;
+}
+
+// Two consecutive 1 KiB LDS-DMA pieces with one M0 save/restore.  The second piece gets
+// its own address register (an instruction offset would also move the LDS destination).
+__device__ __forceinline__ void glds16x2(const uint8_t* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    const uint8_t* g2 = gsrc + 1024;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_add_u32 m0, %3, 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "v"(g2), "s"(lds_dst)
+        : "memory");
+}
+
+__device__ __forceinline__ void pipe_issue_lean(Pipe& p, uint32_t ring_lds, int wave, int lane) {
+    const uint8_t* src = (p.itile < p.n_tiles) ? p.isrc : p.blob;   // dummy past the end
+    glds16x2(src + wave * 2048 + lane * 16,
+             ring_lds + (uint32_t)p.islot * kStageBytes + (uint32_t)wave * 2048u);
+    p.islot = (p.islot + 1 == RING) ? 0 : p.islot + 1;
+    p.isrc += kStageBytes;
+    if (++p.is == p.inext) pipe_boundary(p);
+}
+
 __device__ __forceinline__ void read_stage(const char* smem, int slot, int lane, u32x4 (&a)[8]) {
     const u32x4* s = reinterpret_cast<const u32x4*>(smem + slot * kStageBytes);
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = s[i * 64 + lane];
 }
+
+// Lean schedules: barrier period Q, prefetch depth D (stages issued ahead).
+// WAR: the slot refilled at step g held stage g+D-RING, read at step g+D-RING-1; the last
+// barrier (>= g-Q+1) must follow it  =>  RING >= D + Q - 1.
+// RAW: the barrier at step b certifies stages <= b+Q; stages b+Q+1..b+D-1 may still be in
+// flight  =>  vmcnt(2*(D-1-Q)) (2 DMAs per wave per stage); flight time D-Q steps.
+template <int SCHED> struct SchedCfg { static constexpr int Q = 2, D = 8, VM_STEADY = 2 * (D - 1 - Q); };
+template <> struct SchedCfg<4> { static constexpr int Q = 4, D = 7, VM_STEADY = 2 * (D - 1 - Q); };
+static_assert(RING >= SchedCfg<3>::D + SchedCfg<3>::Q - 1, "WAR distance");   // Q=2, D=8
+static_assert(RING >= SchedCfg<4>::D + SchedCfg<4>::Q - 1, "WAR distance");
 
 // One pipeline step: certify the next stage(s) (vmcnt + barrier), refill the ring, prefetch
 // the next stage's fragments and run this stage's 8 MFMAs.
@@ -285,20 +348,51 @@ __device__ __forceinline__ void step(Pipe& p, const char* smem, uint32_t ring_ld
         for (int i = 0; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) acur[i] = an[i];
-    } else {
+    } else if (SCHED == 2) {
+        // explicit register double buffer: next stage's 8 fragment reads are issued before
+        // this stage's MFMAs (which only touch acur), so LDS latency hides under matrix work.
         acc[0] = Elem<T>::mfma(acur[0], bfrag, FIRST ? zero : acc[0]);
+        acc[1] = Elem<T>::mfma(acur[1], bfrag, FIRST ? zero : acc[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((p.g & 1) == 0)
+            asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PAIR) ")\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        p.cslot = (p.cslot + 1 == RING) ? 0 : p.cslot + 1;
+        u32x4 an[8];
+        read_stage(smem, p.cslot, lane, an);
         __builtin_amdgcn_sched_barrier(0);
         if ((p.g & 1) == 0) {
-            asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PAIR) ")\n\ts_barrier" ::: "memory");
             pipe_issue(p, ring_lds, wave, lane);
             pipe_issue(p, ring_lds, wave, lane);
         }
         p.g++;
+#pragma unroll
+        for (int i = 2; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acur[i] = an[i];
+    } else {
+        // SCHED 3/4: barrier every Q steps certifying the stages read until the next one,
+        // one lean DMA stage per step (stage g+D into the slot of stage g+D-RING), fragment
+        // double buffer, scalar issue work pinned between MFMAs (it fills their issue gaps).
+        constexpr int Q = SchedCfg<SCHED>::Q;
+        constexpr int VM = SchedCfg<SCHED>::VM_STEADY;
+        acc[0] = Elem<T>::mfma(acur[0], bfrag, FIRST ? zero : acc[0]);
+        acc[1] = Elem<T>::mfma(acur[1], bfrag, FIRST ? zero : acc[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((p.g & (Q - 1)) == 0)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(VM) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
         p.cslot = (p.cslot + 1 == RING) ? 0 : p.cslot + 1;
         u32x4 an[8];
         read_stage(smem, p.cslot, lane, an);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[2] = Elem<T>::mfma(acur[2], bfrag, FIRST ? zero : acc[2]);
+        __builtin_amdgcn_sched_barrier(0);
+        pipe_issue_lean(p, ring_lds, wave, lane);
+        p.g++;
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 1; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
+        for (int i = 3; i < 8; ++i) acc[i] = Elem<T>::mfma(acur[i], bfrag, FIRST ? zero : acc[i]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) acur[i] = an[i];
     }
@@ -367,12 +461,23 @@ __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, in
 
     // prologue: SCHED 0 prefetches DEPTH-1 stages, SCHED 1 DEPTH/2 whole pairs; both then
     // wait for stage 0 (2 x DEPTH-2 younger DMAs resp. 4 x (DEPTH/2-1) = the same 12).
+    p.is = 0;
+    p.inext = 0;
+    p.isrc = p.blob;
+    if (SCHED >= 3) {
+        constexpr int D = SchedCfg<SCHED >= 3 ? SCHED : 3>::D;
+        pipe_boundary(p);
 #pragma unroll 1
-    for (int j = 0; j < (SCHED ? DEPTH : DEPTH - 1); ++j) pipe_issue(p, ring_lds, wave, lane);
-    if (SCHED)
-        asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE_PAIR) ")\n\ts_barrier" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE) ")\n\ts_barrier" ::: "memory");
+        for (int j = 0; j < D; ++j) pipe_issue_lean(p, ring_lds, wave, lane);
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * (D - 1)) : "memory");
+    } else {
+#pragma unroll 1
+        for (int j = 0; j < (SCHED ? DEPTH : DEPTH - 1); ++j) pipe_issue(p, ring_lds, wave, lane);
+        if (SCHED)
+            asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE_PAIR) ")\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(" LDM_STR(LDM_VM_PROLOGUE) ")\n\ts_barrier" ::: "memory");
+    }
     u32x4 acur[8];
     read_stage(smem, 0, lane, acur);
 
@@ -405,9 +510,7 @@ __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, in
             bfrag[3] = h ? 0u : w3;
         }
 
-        u32x4 hb[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) hb[i] = (u32x4){0u, 0u, 0u, 0u};
+        u32x4 hb[32];   // every k-step is written by an epilogue before a k-loop reads it
         f32x16 acc[8];
         float part = 0.f;
 
@@ -627,7 +730,7 @@ int check_decoder(const ldm_decoder_t* w) {
 // Schedule variant (development A/B knob; LDM_DECODER_SCHED=0|1, default 1).
 int decoder_sched() {
     const char* e = getenv("LDM_DECODER_SCHED");   // read per launch: same-process A/B
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 4;
 }
 
 template <typename T, int S, int SCHED>
@@ -646,8 +749,13 @@ void launch_mfma_s(const DecArgs& a, bool points, hipStream_t s, int grid) {
 
 template <typename T, int S>
 void launch_mfma(const DecArgs& a, bool points, hipStream_t s, int grid) {
-    if (decoder_sched() == 0) launch_mfma_s<T, S, 0>(a, points, s, grid);
-    else launch_mfma_s<T, S, 1>(a, points, s, grid);
+    switch (decoder_sched()) {
+        case 0: launch_mfma_s<T, S, 0>(a, points, s, grid); break;
+        case 2: launch_mfma_s<T, S, 2>(a, points, s, grid); break;
+        case 4: launch_mfma_s<T, S, 4>(a, points, s, grid); break;
+        case 3: launch_mfma_s<T, S, 3>(a, points, s, grid); break;
+        default: launch_mfma_s<T, S, 4>(a, points, s, grid); break;
+    }
 }
 
 int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int B, int npts,
