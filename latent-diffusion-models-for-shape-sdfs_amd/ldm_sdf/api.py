@@ -151,19 +151,7 @@ def sample(denoiser: MLPDenoiser, schedule: DDPMSchedule, n: int, *,
     noise = noise.to(device, torch.float32)[:, lo:hi].contiguous()
     out = Sampler(denoiser, schedule, nl, steps=steps, dtype=dtype, device=device,
                   use_graph=use_graph).run(x_T, noise).clone()
-    if world == 1:
-        return out
-    # equal shards are required by all_gather_into_tensor: pad to ceil(n/W)
-    per = -(-n // world)
-    buf = torch.zeros(per, D, device=device)
-    buf[:nl] = out
-    gathered = torch.empty(world * per, D, device=device)
-    torch.distributed.all_gather_into_tensor(gathered, buf, group=group)
-    rows = []
-    for r in range(world):
-        a, b = ldist.batch_shard(n, r, world)
-        rows.append(gathered[r * per:r * per + (b - a)])
-    return torch.cat(rows)
+    return ldist.all_gather_rows(out, n, group=group)
 
 
 # ---------------------------------------------------------------------------------- train

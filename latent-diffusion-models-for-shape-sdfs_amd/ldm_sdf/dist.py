@@ -54,8 +54,10 @@ def decode_sharded(compute_slab: Callable[[int, int, torch.Tensor], None], B: in
     if world == 1:
         vol = local
     else:
-        gathered = torch.empty(world, B, S, N, N, device=device, dtype=torch.float32)
+        # output as [W*B, S, N, N] (dim-0 concatenation: the form gloo and RCCL both take)
+        gathered = torch.empty(world * B, S, N, N, device=device, dtype=torch.float32)
         dist.all_gather_into_tensor(gathered, local, group=group)
+        gathered = gathered.view(world, B, S, N, N)
         if B == 1:
             vol = gathered.view(1, world * S, N, N)
         else:
@@ -72,6 +74,25 @@ def batch_shard(n: int, rank: int, world: int) -> Tuple[int, int]:
     base, rem = divmod(n, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+def all_gather_rows(local: torch.Tensor, n: int, group=None) -> torch.Tensor:
+    """Reassemble a batch of n rows sharded by ``batch_shard`` (uneven shards allowed):
+    pad each shard to ceil(n/W) rows, one ``all_gather_into_tensor``, drop the padding."""
+    world, rank = world_and_rank(group)
+    if world == 1:
+        return local
+    per = -(-n // world)
+    buf = torch.zeros((per,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
+    buf[:local.shape[0]] = local
+    gathered = torch.empty((world * per,) + tuple(local.shape[1:]), device=local.device,
+                           dtype=local.dtype)
+    dist.all_gather_into_tensor(gathered, buf, group=group)
+    rows = []
+    for r in range(world):
+        a, b = batch_shard(n, r, world)
+        rows.append(gathered[r * per:r * per + (b - a)])
+    return torch.cat(rows)
 
 
 def allreduce_mean_(tensors, group=None) -> None:
