@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ddpm", action="store_true")
     ap.add_argument("--ddpm-batch", type=int, default=8)
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--train-steps", type=int, default=20)
     ap.add_argument("--config3", action="store_true",
                     help="also time sample(8) -> decode 128^3 end to end (adds a decoder "
                          "launch of another size to the profile)")
@@ -230,6 +232,24 @@ def main():
                                     "frac": sps * wbytes / 8e12,
                                     "bytes_per_step": wbytes},
                        "config3_sample_plus_decode128_s": e2e}
+    if rank == 0 and not args.no_train:
+        # config 2: DDPM training on 1k synthetic 256-d latents, MLP denoiser, bf16, batch 1000
+        den_t = ldm_sdf.MLPDenoiser(seed=4321)
+        sch_t = ldm_sdf.DDPMSchedule()
+        lat_t = torch.randn(1000, 256, device=dev, generator=gen) * 0.5
+        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16")   # warm-up
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=args.train_steps, batch=1000,
+                           dtype="bf16", state=st)
+        torch.cuda.synchronize()
+        dtt = (time.perf_counter() - t3) / args.train_steps
+        H, D, nb = den_t.H, den_t.D, den_t.n_blocks
+        macs = 1000 * (H * 128 + H * H + H * D + nb * H * 2 * H + D * H)   # forward MACs
+        res["train"] = {"metric": "DDPM training steps/sec (config 2)", "value": 1.0 / dtt,
+                        "unit": "steps/s", "batch": 1000, "ms_per_step": dtt * 1e3,
+                        "tflops_fwd_bwd": 3 * 2 * macs / dtt / 1e12,
+                        "loss_first_last": [st.losses[0], st.losses[-1]]}
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_decode(N, args.cpu_seconds)
         if "ddpm" in res:

@@ -15,6 +15,7 @@
 #include "ldm_internal.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 namespace ldm {
 namespace {
@@ -172,8 +173,243 @@ __global__ __launch_bounds__(256) void small_linear_kernel(SmallArgs a) {
     }
 }
 
+// v2: one wave per block owns R rows.  All weight and activation loads are issued up front
+// (registers, no LDS staging, no barrier), then R*MB partial dot products per lane are
+// reduce-scattered across the wave (each butterfly level exchanges only the half a lane gives
+// away: 32 shuffles for 4 rows x 8 samples instead of 192), and the lanes that end up owning a
+// (row, sample) total run the fused epilogue.  Latency-bound by design.
+template <typename TW, int EPI, int R, int MB>
+__global__ __launch_bounds__(64) void small_linear_v2(SmallArgs a) {
+    constexpr int V = R * MB;                 // values to reduce per lane (power of 2, <= 64)
+    static_assert((V & (V - 1)) == 0 && V <= 64, "R*MB must be a power of two <= 64");
+    const int lane = threadIdx.x;
+    const int m0 = blockIdx.x * R;
+    const int nch = a.K >> 3;                 // 8-element chunks; lane takes c = lane + 64 j
+    constexpr int MAXJ = 4;                   // K <= 2048
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int c = lane + 64 * j;
+        if (64 * j >= nch) break;             // uniform
+        const bool on = c < nch;
+        float w[R][8];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int m = (m0 + r < a.M) ? m0 + r : a.M - 1;
+            if (sizeof(TW) == 2) {
+                uint4 u = {0, 0, 0, 0};
+                if (on) u = *reinterpret_cast<const uint4*>(
+                    reinterpret_cast<const unsigned short*>(a.W) + (size_t)m * a.ldw + c * 8);
+                w[r][0] = bf16_to_f32(u.x & 0xffff); w[r][1] = bf16_to_f32(u.x >> 16);
+                w[r][2] = bf16_to_f32(u.y & 0xffff); w[r][3] = bf16_to_f32(u.y >> 16);
+                w[r][4] = bf16_to_f32(u.z & 0xffff); w[r][5] = bf16_to_f32(u.z >> 16);
+                w[r][6] = bf16_to_f32(u.w & 0xffff); w[r][7] = bf16_to_f32(u.w >> 16);
+            } else {
+                f32x4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
+                if (on) {
+                    const float* wp = reinterpret_cast<const float*>(a.W) + (size_t)m * a.ldw + c * 8;
+                    w0 = *reinterpret_cast<const f32x4*>(wp);
+                    w1 = *reinterpret_cast<const f32x4*>(wp + 4);
+                }
+                w[r][0] = w0[0]; w[r][1] = w0[1]; w[r][2] = w0[2]; w[r][3] = w0[3];
+                w[r][4] = w1[0]; w[r][5] = w1[1]; w[r][6] = w1[2]; w[r][7] = w1[3];
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+            f32x4 x0 = {0, 0, 0, 0}, x1 = {0, 0, 0, 0};
+            if (on && b < a.B) {
+                x0 = *reinterpret_cast<const f32x4*>(a.X + (size_t)b * a.K + c * 8);
+                x1 = *reinterpret_cast<const f32x4*>(a.X + (size_t)b * a.K + c * 8 + 4);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                float s = acc[r * MB + b];
+                s = fmaf(w[r][0], x0[0], s); s = fmaf(w[r][1], x0[1], s);
+                s = fmaf(w[r][2], x0[2], s); s = fmaf(w[r][3], x0[3], s);
+                s = fmaf(w[r][4], x1[0], s); s = fmaf(w[r][5], x1[1], s);
+                s = fmaf(w[r][6], x1[2], s); s = fmaf(w[r][7], x1[3], s);
+                acc[r * MB + b] = s;
+            }
+        }
+    }
+    // reduce-scatter: at level lv (offset o = 32 >> lv) a lane keeps the half of its n = V >> lv
+    // values selected by lane & o and adds its partner's copy of that half.
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        const int o = 32 >> lv;
+        const int n = V >> lv;                // compile-time after unrolling
+        const bool upper = (lane & o) != 0;
+        if (n > 1) {
+            const int half = n >> 1;
+#pragma unroll
+            for (int i = 0; i < half; ++i) {
+                const float send = upper ? acc[i] : acc[i + half];
+                const float keep = upper ? acc[i + half] : acc[i];
+                acc[i] = keep + __shfl_xor(send, o);
+            }
+        } else {
+            acc[0] += __shfl_xor(acc[0], o);
+        }
+    }
+    // lane owns value index idx = (lane >> (6 - log2 V)) in natural order: idx = r*MB + b
+    constexpr int LV = (V >= 64) ? 6 : (V >= 32) ? 5 : (V >= 16) ? 4 : (V >= 8) ? 3 : (V >= 4) ? 2 : (V >= 2) ? 1 : 0;
+    const int idx = lane >> (6 - LV);
+    const bool writer = (lane & ((1 << (6 - LV)) - 1)) == 0;
+    const int r = idx / MB, b = idx - (idx / MB) * MB;
+    const int m = m0 + r;
+    if (writer && b < a.B && m < a.M) {
+        const float pre = acc[0] + a.bias[m];
+        const size_t i = (size_t)b * a.M + m;
+        if (EPI == SE_BIAS) {
+            a.Y[i] = pre;
+        } else if (EPI == SE_BLOCK) {
+            a.Y[i] = a.X[(size_t)b * a.K + m] + silu(pre);
+        } else {
+            const bool noise = a.t > 0;
+            a.Y[i] = ddpm_update(a.xlat[i], pre, noise ? a.z[i] : 0.f, a.c1t[a.t], a.c2t[a.t],
+                                 a.sgt[a.t], noise);
+        }
+    }
+}
+
+// v3: v1's shape (one wave per output row, 4 rows per 256-thread block, activations staged
+// once per block in LDS) with the row's weight loads issued BEFORE the activation staging and
+// its barrier (the two memory latencies overlap), and a reduce-scatter over the MB samples.
+template <typename TW, int EPI, int MB>
+__global__ __launch_bounds__(256) void small_linear_v3(SmallArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];   // [B][K]
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int mm = m < a.M ? m : a.M - 1;
+    const int nch = a.K >> 3;
+    constexpr int MAXJ = 4;                    // K <= 2048
+    float w[MAXJ][8];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int c = lane + 64 * j;
+        const bool on = c < nch;
+        if (sizeof(TW) == 2) {
+            uint4 u = {0, 0, 0, 0};
+            if (on) u = *reinterpret_cast<const uint4*>(
+                reinterpret_cast<const unsigned short*>(a.W) + (size_t)mm * a.ldw + c * 8);
+            w[j][0] = bf16_to_f32(u.x & 0xffff); w[j][1] = bf16_to_f32(u.x >> 16);
+            w[j][2] = bf16_to_f32(u.y & 0xffff); w[j][3] = bf16_to_f32(u.y >> 16);
+            w[j][4] = bf16_to_f32(u.z & 0xffff); w[j][5] = bf16_to_f32(u.z >> 16);
+            w[j][6] = bf16_to_f32(u.w & 0xffff); w[j][7] = bf16_to_f32(u.w >> 16);
+        } else {
+            f32x4 w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
+            if (on) {
+                const float* wp = reinterpret_cast<const float*>(a.W) + (size_t)mm * a.ldw + c * 8;
+                w0 = *reinterpret_cast<const f32x4*>(wp);
+                w1 = *reinterpret_cast<const f32x4*>(wp + 4);
+            }
+            w[j][0] = w0[0]; w[j][1] = w0[1]; w[j][2] = w0[2]; w[j][3] = w0[3];
+            w[j][4] = w1[0]; w[j][5] = w1[1]; w[j][6] = w1[2]; w[j][7] = w1[3];
+        }
+    }
+    const int nx = a.B * a.K;
+    for (int i = threadIdx.x * 4; i < nx; i += 256 * 4)
+        *reinterpret_cast<f32x4*>(xs + i) = *reinterpret_cast<const f32x4*>(a.X + i);
+    __syncthreads();
+    float acc[MB];
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[b] = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int c = lane + 64 * j;
+        if (64 * j >= nch) break;
+        if (c < nch) {
+#pragma unroll
+            for (int b = 0; b < MB; ++b) {
+                if (b < a.B) {
+                    const f32x4 x0 = *reinterpret_cast<const f32x4*>(xs + b * a.K + c * 8);
+                    const f32x4 x1 = *reinterpret_cast<const f32x4*>(xs + b * a.K + c * 8 + 4);
+                    float t = acc[b];
+                    t = fmaf(w[j][0], x0[0], t); t = fmaf(w[j][1], x0[1], t);
+                    t = fmaf(w[j][2], x0[2], t); t = fmaf(w[j][3], x0[3], t);
+                    t = fmaf(w[j][4], x1[0], t); t = fmaf(w[j][5], x1[1], t);
+                    t = fmaf(w[j][6], x1[2], t); t = fmaf(w[j][7], x1[3], t);
+                    acc[b] = t;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        const int o = 32 >> lv;
+        const int n = MB >> lv;
+        const bool upper = (lane & o) != 0;
+        if (n > 1) {
+            const int half = n >> 1;
+#pragma unroll
+            for (int i = 0; i < half; ++i) {
+                const float send = upper ? acc[i] : acc[i + half];
+                const float keep = upper ? acc[i + half] : acc[i];
+                acc[i] = keep + __shfl_xor(send, o);
+            }
+        } else {
+            acc[0] += __shfl_xor(acc[0], o);
+        }
+    }
+    constexpr int LB = (MB >= 16) ? 4 : 3;
+    const int b = lane >> (6 - LB);
+    const bool writer = (lane & ((1 << (6 - LB)) - 1)) == 0;
+    if (m < a.M && writer && b < a.B) {
+        const float pre = acc[0] + a.bias[m];
+        const size_t i = (size_t)b * a.M + m;
+        if (EPI == SE_BIAS) {
+            a.Y[i] = pre;
+        } else if (EPI == SE_BLOCK) {
+            a.Y[i] = xs[b * a.K + m] + silu(pre);
+        } else {
+            const bool noise = a.t > 0;
+            a.Y[i] = ddpm_update(a.xlat[i], pre, noise ? a.z[i] : 0.f, a.c1t[a.t], a.c2t[a.t],
+                                 a.sgt[a.t], noise);
+        }
+    }
+}
+
+template <typename TW, int EPI>
+void launch_small_v3(const SmallArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)a.B * a.K * sizeof(float);
+    const dim3 grid((a.M + 3) / 4);
+    if (a.B <= 8)
+        hipLaunchKernelGGL((small_linear_v3<TW, EPI, 8>), grid, dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL((small_linear_v3<TW, EPI, 16>), grid, dim3(256), lds, s, a);
+}
+
+int small_version() {
+    const char* e = getenv("LDM_SMALL_LINEAR");   // development A/B knob: 1, 2, 3 (default)
+    return (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 3;
+}
+
+template <typename TW, int EPI>
+void launch_small_v2(const SmallArgs& a, hipStream_t s) {
+    constexpr int R = 4;
+    const dim3 grid((a.M + R - 1) / R);
+    if (a.B <= 8)
+        hipLaunchKernelGGL((small_linear_v2<TW, EPI, R, 8>), grid, dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((small_linear_v2<TW, EPI, R, 16>), grid, dim3(64), 0, s, a);
+}
+
 template <int EPI>
 int launch_small(const SmallArgs& a, int w_dtype, hipStream_t s) {
+    const int ver = small_version();
+    if (ver == 2) {
+        if (w_dtype == LDM_BF16) launch_small_v2<unsigned short, EPI>(a, s);
+        else launch_small_v2<float, EPI>(a, s);
+        return launch_status("small_linear_v2");
+    }
+    if (ver == 3) {
+        if (w_dtype == LDM_BF16) launch_small_v3<unsigned short, EPI>(a, s);
+        else launch_small_v3<float, EPI>(a, s);
+        return launch_status("small_linear_v3");
+    }
     const size_t lds = (size_t)a.B * a.K * sizeof(float);
     const dim3 grid((a.M + 3) / 4);
     if (w_dtype == LDM_BF16)
