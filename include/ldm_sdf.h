@@ -42,6 +42,7 @@ extern "C" {
 /* workspace ops for ldm_workspace_bytes() */
 #define LDM_OP_DECODER_GRID 1
 #define LDM_OP_DECODER_POINTS 2
+/* workspace for the quarter layout is 64 KiB per shape; query with ldm_workspace_bytes_layout */
 
 typedef void* ldm_stream_t; /* hipStream_t; NULL = the null stream */
 
@@ -64,8 +65,12 @@ typedef struct ldm_decoder {
     const float* wxyz;    /* fp32 [2][H][3]  xyz columns of layer 0 and layer 4 */
     const float* w_last;  /* fp32 [H] final 512->1 weights (bf16/f16: MFMA-row permuted) */
     float b_last;         /* final bias */
-    int32_t reserved;
+    int32_t layout;       /* bf16/f16 stage-blob layout: LDM_LAYOUT_PASS8 or LDM_LAYOUT_QUARTER */
 } ldm_decoder_t;
+
+/* Stage-blob layouts of the MFMA decoder. */
+#define LDM_LAYOUT_PASS8 0   /* 8 m-chunks x 1 k-step per stage, 2 passes per layer */
+#define LDM_LAYOUT_QUARTER 1 /* 4 m-chunks x 2 k-steps per stage, 4 quarters per layer */
 
 /* DDPM tables, fp32 device arrays of length T. */
 typedef struct ldm_sched {
@@ -106,6 +111,7 @@ int ldm_abi_version(void);
 const char* ldm_last_error(void);
 /* Device bytes of workspace an op needs (B shapes, n = N (grid) or P (points)). */
 size_t ldm_workspace_bytes(int op, int B, int n, int dtype);
+size_t ldm_workspace_bytes_layout(int op, int B, int n, int dtype, int layout);
 
 /* ---- decoder: A1 grid coords, A2 latent fold, A3 fused MLP ----------------------------- */
 /* A1 standalone: xyz_out fp32 [(k1-k0)*N*N][3], z slowest, x fastest, x = fl32(fl32(i*vs)+origin). */

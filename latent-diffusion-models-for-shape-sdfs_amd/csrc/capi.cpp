@@ -6,7 +6,7 @@
 #include "ldm_internal.h"
 
 namespace ldm {
-size_t decoder_workspace_bytes(int B, int dtype);
+size_t decoder_workspace_bytes(int B, int dtype, int layout);
 
 static thread_local char g_last_error[512] = "";
 
@@ -28,7 +28,19 @@ extern "C" size_t ldm_workspace_bytes(int op, int B, int n, int dtype) {
     switch (op) {
         case LDM_OP_DECODER_GRID:
         case LDM_OP_DECODER_POINTS:
-            return ldm::decoder_workspace_bytes(B, dtype);
+            return ldm::decoder_workspace_bytes(B, dtype, LDM_LAYOUT_QUARTER);
+        default:
+            return 0;
+    }
+}
+
+extern "C" size_t ldm_workspace_bytes_layout(int op, int B, int n, int dtype, int layout) {
+    (void)n;
+    if (B < 1) return 0;
+    switch (op) {
+        case LDM_OP_DECODER_GRID:
+        case LDM_OP_DECODER_POINTS:
+            return ldm::decoder_workspace_bytes(B, dtype, layout);
         default:
             return 0;
     }

@@ -10,38 +10,14 @@
 //   grid_coords_kernel           A1 on its own (bit-exactness test surface).
 //   fold_kernel                  A2 per-shape biases.
 //   aux_pack_kernel<T>           per-shape "aux" weight stages (xyz + folded biases).
-#include "ldm_internal.h"
+#include "decoder_common.h"
 
 #include <math.h>
 #include <stdlib.h>
 
 namespace ldm {
 namespace {
-
-#define LDM_STR2(x) #x
-#define LDM_STR(x) LDM_STR2(x)
-
-// ------------------------------------------------------------------------------------------
-// A1: one grid axis value, x = fl32(fl32(i * vs) + origin).  Contraction is disabled so the
-// device rounds twice exactly like the CPU oracle (SURVEY.md §7 'Bit-exact coordinates').
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float grid_axis(int i, float vs, float origin) {
-#pragma clang fp contract(off)
-    float t = (float)i * vs;
-    return t + origin;
-}
-
-__device__ __forceinline__ void grid_point(int p, int N, int k0, float vs, float origin,
-                                           float& x, float& y, float& z) {
-    const int nn = N * N;
-    const int k = k0 + p / nn;
-    const int r = p - (p / nn) * nn;
-    const int j = r / N;
-    const int i = r - j * N;
-    x = grid_axis(i, vs, origin);
-    y = grid_axis(j, vs, origin);
-    z = grid_axis(k, vs, origin);
-}
+using namespace dec;
 
 __global__ void grid_coords_kernel(int N, int k0, int npts, float vs, float origin,
                                    float* __restrict__ out) {
@@ -71,39 +47,6 @@ __global__ void fold_kernel(const float* __restrict__ wz, const float* __restric
     for (int k = 0; k < L; ++k) acc = fmaf(w[k], zz[k], acc);
     beta[id] = acc + bz[l * H + f];
 }
-
-// ------------------------------------------------------------------------------------------
-// Element conversion + MFMA per 16-bit type.
-// ------------------------------------------------------------------------------------------
-template <typename T>
-struct Elem;
-template <>
-struct Elem<__bf16> {
-    static __device__ __forceinline__ unsigned pack(float a, float b) {
-        // one v_cvt_pk_bf16_f32 (RNE); the element-wise {(__bf16)a, (__bf16)b} form costs two
-        // single conversions + a v_perm
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        const f32x2 v = {a, b};
-        return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
-    }
-    static __device__ __forceinline__ float round(float x) { return (float)(__bf16)x; }
-    static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
-        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
-                                                       __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-    }
-};
-template <>
-struct Elem<_Float16> {
-    static __device__ __forceinline__ unsigned pack(float a, float b) {
-        f16x2 v = {(_Float16)a, (_Float16)b};
-        return __builtin_bit_cast(unsigned, v);
-    }
-    static __device__ __forceinline__ float round(float x) { return (float)(_Float16)x; }
-    static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
-        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
-                                                      __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
-    }
-};
 
 // ------------------------------------------------------------------------------------------
 // Per-shape aux stages: for layer 0 (stages 0,1) and layer 4 (stages 2,3), fragment i, lane
@@ -283,24 +226,6 @@ __device__ __forceinline__ void pipe_boundary(Pipe& p) {
             : (s == p.aux4b) ? p.aux4b + 1 : p.nst;
 }
 
-// Two consecutive 1 KiB LDS-DMA pieces with one M0 save/restore.  The second piece gets
-// its own address register (an instruction offset would also move the LDS destination).
-__device__ __forceinline__ void glds16x2(const uint8_t* gsrc, uint32_t lds_dst) {
-    unsigned keep;
-    const uint8_t* g2 = gsrc + 1024;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_add_u32 m0, %3, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "v"(g2), "s"(lds_dst)
-        : "memory");
-}
 
 __device__ __forceinline__ void pipe_issue_lean(Pipe& p, uint32_t ring_lds, int wave, int lane) {
     const uint8_t* src = (p.itile < p.n_tiles) ? p.isrc : p.blob;   // dummy past the end
@@ -408,25 +333,7 @@ __device__ __forceinline__ void kloop(Pipe& p, const char* smem, uint32_t ring_l
         step<T, false, SCHED>(p, smem, ring_lds, wave, lane, acur, hb[ks], acc);
 }
 
-// ReLU in the 16-bit domain: both bf16 and f16 order like sign-magnitude, so max with +0 as
-// signed int16 is ReLU (and rounding commutes with ReLU).
-__device__ __forceinline__ unsigned relu2(unsigned v) {
-    typedef short s16x2 __attribute__((ext_vector_type(2)));
-    s16x2 x = __builtin_bit_cast(s16x2, v);
-    const s16x2 z = {0, 0};
-    x = __builtin_elementwise_max(x, z);
-    return __builtin_bit_cast(unsigned, x);
-}
 
-// Accumulator m-chunk i (rows = features, cols = points) -> two B fragments (k-steps 2i, 2i+1).
-template <typename T>
-__device__ __forceinline__ void acc_to_frags(const f32x16& a, u32x4& f0, u32x4& f1) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        f0[q] = relu2(Elem<T>::pack(a[2 * q], a[2 * q + 1]));
-        f1[q] = relu2(Elem<T>::pack(a[8 + 2 * q], a[8 + 2 * q + 1]));
-    }
-}
 
 template <typename T, int S, bool POINTS, int SCHED>
 __global__ __launch_bounds__(256, 1) void dec_mfma_kernel(DecArgs a, int nst, int aux4a,
@@ -719,10 +626,13 @@ int check_decoder(const ldm_decoder_t* w) {
     LDM_REQUIRE(LDM_ALIGNED(w->weights, 16) && LDM_ALIGNED(w->w_last, 16), LDM_EALIGN,
                 "decoder weights must be 16-byte aligned");
     if (w->dtype != LDM_F32) {
+        LDM_REQUIRE(w->layout == LDM_LAYOUT_PASS8 || w->layout == LDM_LAYOUT_QUARTER, LDM_EINVAL,
+                    "bad decoder layout %d", w->layout);
         const int S = w->skip_width == 253 ? 256 : 512;
-        LDM_REQUIRE(w->n_stages == dec_n_stages(S), LDM_EINVAL,
-                    "n_stages %d != %d for skip width %d", w->n_stages, dec_n_stages(S),
-                    w->skip_width);
+        const int want = w->layout == LDM_LAYOUT_PASS8 ? dec_n_stages(S)
+                                                       : decoder_q_n_stages(w->skip_width);
+        LDM_REQUIRE(w->n_stages == want, LDM_EINVAL, "n_stages %d != %d for skip width %d",
+                    w->n_stages, want, w->skip_width);
     }
     return 0;
 }
@@ -787,6 +697,9 @@ int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int
                            points ? 1 : 0);
         return launch_status("ldm_decoder_fwd(f32)");
     }
+    if (w->layout == LDM_LAYOUT_QUARTER)
+        return decoder_q_fwd(w, beta, xyz, B, npts, N, k0, vs, origin, out, ws, ws_bytes, s,
+                             num_cus());
     LDM_REQUIRE(ws != nullptr && ws_bytes >= aux_bytes(B) && LDM_ALIGNED(ws, 16), LDM_ENOSPC,
                 "workspace too small: need %zu bytes, got %zu", aux_bytes(B), ws_bytes);
     // per-shape aux stages (folded biases + xyz columns) into the workspace
@@ -828,8 +741,9 @@ int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int
 
 }  // namespace
 
-size_t decoder_workspace_bytes(int B, int dtype) {
-    return dtype == LDM_F32 ? 0 : aux_bytes(B);
+size_t decoder_workspace_bytes(int B, int dtype, int layout) {
+    if (dtype == LDM_F32) return 0;
+    return layout == LDM_LAYOUT_PASS8 ? aux_bytes(B) : decoder_q_aux_bytes(B);
 }
 
 }  // namespace ldm

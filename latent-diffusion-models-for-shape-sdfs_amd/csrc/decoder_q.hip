@@ -1,0 +1,485 @@
+// Quarter-pipelined MFMA decoder (stage layout LDM_LAYOUT_QUARTER): SURVEY.md §8(a) A1+A3.
+//
+// Same math and operand maps as dec_mfma_kernel (decoder.hip), different work
+// order so that the per-chunk epilogue (AGPR read, cvt_pk, ReLU, store) overlaps matrix work:
+//   * a layer's output rows are split in quarters of 4 m-chunks (128 features);
+//   * one 8 KiB stage = 4 m-chunks x 2 k-steps (frag i = e*4 + c: chunk c, k-step 2j+e);
+//   * the accumulators alternate between two 4-chunk sets A/B (2 x 64 AGPRs);
+//   * quarter q's epilogue runs inside the first 4 steps of quarter q+1 (one chunk per step,
+//     between that step's MFMAs), on the other accumulator set;
+//   * quarters 0..nq-2 of a layer park their outputs in a per-wave LDS area (24 KiB/wave) that
+//     is reloaded into the B fragments hb[] at the next layer's start; the last quarter writes
+//     hb directly (the next layer only reads those k-steps 4+ steps later).
+// Layer 0 (aux only) and the final quarter of the tile (layer-7 dot + tanh + store) run
+// serialized.  DMA ring: 7 x 8 KiB, barrier every 2 steps, 6 stages ahead.
+#include "decoder_common.h"
+
+#include <stdlib.h>
+
+namespace ldm {
+namespace {
+using namespace dec;
+
+constexpr int QRING = 7;
+constexpr int QQ = 2;                         // barrier period (steps)
+constexpr int QD = 6;                         // stages issued ahead
+constexpr int QVM = 2 * (QD - 1 - QQ);        // vmcnt at a barrier
+static_assert(QRING >= QD + QQ - 1, "WAR distance");
+static_assert(QVM >= 0, "RAW distance");
+constexpr int QLDS_RING = QRING * kStageBytes;        // 56 KiB
+constexpr int QLDS_TMP = 4 * 24 * 1024;               // 96 KiB (3 quarters x 8 frags x 1 KiB x 4 waves)
+constexpr int QLDS_WL = 16 * 2 * 16 * 4;              // 2 KiB
+constexpr int QLDS_TOTAL = QLDS_RING + QLDS_TMP + QLDS_WL;
+static_assert(QLDS_TOTAL <= 160 * 1024, "LDS");
+
+__host__ __device__ constexpr int q_nq3(int S) { return S / 128; }     // quarters of layer 3
+__host__ __device__ constexpr int q_kp4(int S) { return S / 32; }      // pair-stages of layer 4
+__host__ __device__ constexpr int q_base4(int S) { return 4 + 68 + 68 + q_nq3(S) * 17; }
+__host__ __device__ constexpr int q_len4(int S) { return q_kp4(S) + 1; }
+__host__ __device__ constexpr int q_nstages(int S) { return q_base4(S) + 4 * q_len4(S) + 3 * 68; }
+__host__ __device__ constexpr int q_nquarters(int S) { return 4 + 4 + q_nq3(S) + 4 + 12; }
+static_assert(q_nstages(256) == 414 && q_nstages(512) == 480, "stage plan");
+
+// ------------------------------------------------------------------------------------------
+// per-shape aux stages (8 per shape): layer-0 quarters q = 0..3 -> stages 0..3, layer-4
+// quarters -> 4..7.  Frag c (0..3), lane l < 32: [wx, wy, wz, wx, wy, wz, beta_hi, beta_lo] of
+// feature (4q + c)*32 + l; frags 4..7 and lanes >= 32 are zero.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void qaux_pack_kernel(const float* __restrict__ beta, const float* __restrict__ wxyz,
+                                 int B, T* __restrict__ aux) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;   // (b, stage, frag, lane)
+    if (id >= B * 8 * 8 * 64) return;
+    const int lane = id & 63;
+    const int i = (id >> 6) & 7;
+    const int st = (id >> 9) & 7;
+    const int b = id >> 12;
+    const int layer = st >> 2;
+    const int q = st & 3;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (lane < 32 && i < 4) {
+        const int f = (4 * q + i) * 32 + lane;
+        const float* w = wxyz + ((size_t)layer * kHidden + f) * 3;
+        const float bb = beta[((size_t)b * 2 + layer) * kHidden + f];
+        const float hi = Elem<T>::round(bb);
+        v[0] = w[0]; v[1] = w[1]; v[2] = w[2];
+        v[3] = w[0]; v[4] = w[1]; v[5] = w[2];
+        v[6] = hi;   v[7] = bb - hi;
+    }
+    T* o = aux + (size_t)id * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (T)v[e];
+}
+
+// ------------------------------------------------------------------------------------------
+// DMA pipeline (lean issue path; source pattern changes only around the 8 per-shape stages)
+// ------------------------------------------------------------------------------------------
+struct QPipe {
+    const uint8_t* blob;
+    const uint8_t* aux;
+    const uint8_t* isrc;
+    int g, islot, cslot, is, inext, itile, ishape;
+    int n_tiles, tps, tstride, nst, base4, len4;
+};
+
+__device__ __forceinline__ void qpipe_boundary(QPipe& p) {
+    if (p.is == p.nst) {
+        p.is = 0;
+        p.itile += p.tstride;
+        p.ishape = p.itile / p.tps;
+    }
+    const int s = p.is;
+    int ai = -1;
+    if (s < 4) {
+        ai = s;
+    } else if (s >= p.base4 && s < p.base4 + 4 * p.len4) {
+        const int r = s - p.base4;
+        const int k = r / p.len4;
+        if (r - k * p.len4 == p.len4 - 1) ai = 4 + k;
+    }
+    if (ai >= 0) {
+        p.isrc = p.aux + ((size_t)p.ishape * 8 + ai) * kStageBytes;
+        p.inext = s + 1;
+    } else {
+        p.isrc = p.blob + (size_t)s * kStageBytes;
+        if (s < p.base4) p.inext = p.base4 + p.len4 - 1;
+        else if (s < p.base4 + 4 * p.len4) p.inext = p.base4 + p.len4 * ((s - p.base4) / p.len4 + 1) - 1;
+        else p.inext = p.nst;
+    }
+}
+
+__device__ __forceinline__ void qpipe_issue(QPipe& p, uint32_t ring_lds, int wave, int lane) {
+    const uint8_t* src = (p.itile < p.n_tiles) ? p.isrc : p.blob;   // dummy past the end
+    glds16x2(src + wave * 2048 + lane * 16,
+             ring_lds + (uint32_t)p.islot * kStageBytes + (uint32_t)wave * 2048u);
+    p.islot = (p.islot + 1 == QRING) ? 0 : p.islot + 1;
+    p.isrc += kStageBytes;
+    if (++p.is == p.inext) qpipe_boundary(p);
+}
+
+__device__ __forceinline__ void qread_stage(const char* smem, int slot, int lane, u32x4 (&a)[8]) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(smem + slot * kStageBytes);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = s[i * 64 + lane];
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-wave state
+// ------------------------------------------------------------------------------------------
+struct QCtx {
+    QPipe p;
+    const char* smem;
+    uint32_t ring_lds;
+    int wave, lane, h;
+    u32x4* tmp;          // this wave's parked quarter outputs: [24 frags][64 lanes]
+    const float* wl;     // permuted final weights [16 mc][2 h][16]
+    float part;          // final-layer partial dot product
+};
+
+// Pending epilogue kinds.  Every converted quarter is parked in the wave's LDS area (slot
+// 0..2); the last quarter of a layer reuses slot 0, whose previous contents the next layer
+// has already reloaded (see run_quarter), so no B fragment is ever written inside a step.
+enum QEpi { QE_NONE = 0, QE_TMP = 1, QE_FIN = 2 };
+
+// Convert chunk c of a finished accumulator set into its parking slot (CVT) or fold it into
+// the final-layer dot product (FIN).  Pure VALU/LDS work that fills MFMA issue gaps.
+template <typename T, int KIND>
+__device__ __forceinline__ void qepi_chunk(QCtx& c, const f32x16& a, int chunk, int slot,
+                                           int fin_q) {
+    if (KIND == QE_FIN) {
+        const f32x4* w = reinterpret_cast<const f32x4*>(c.wl + ((fin_q * 4 + chunk) * 2 + c.h) * 16);
+        float part = c.part;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 wv = w[q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) part = fmaf(fmaxf(a[4 * q + e], 0.f), wv[e], part);
+        }
+        c.part = part;
+    } else if (KIND == QE_TMP) {
+        u32x4 f0, f1;
+        acc_to_frags<T>(a, f0, f1);
+        c.tmp[(slot * 8 + 2 * chunk) * 64 + c.lane] = f0;
+        c.tmp[(slot * 8 + 2 * chunk + 1) * 64 + c.lane] = f1;
+    }
+}
+
+// One pipeline step on a pair-stage: 8 MFMAs (4 chunks x k-steps 2j, 2j+1) into accX, plus
+// (KIND != QE_NONE) chunk `ec` of the pending epilogue on accY, interleaved with the last 5.
+template <typename T, bool FIRST, int KIND>
+__device__ __forceinline__ void qstep(QCtx& c, u32x4 (&acur)[8], const u32x4 b0, const u32x4 b1,
+                                      f32x16 (&accX)[4], const f32x16 (&accY)[4], int ec,
+                                      int slot, int fin_q) {
+    const f32x16 zero = {};
+    accX[0] = Elem<T>::mfma(acur[0], b0, FIRST ? zero : accX[0]);
+    accX[1] = Elem<T>::mfma(acur[1], b0, FIRST ? zero : accX[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    if ((c.p.g & (QQ - 1)) == 0)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(QVM) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // rolling fragment buffer: fragment i of the next stage is read right after fragment i of
+    // this stage has been consumed (>= 6 MFMAs of latency cover, ~40 live fragment VGPRs)
+    c.p.cslot = (c.p.cslot + 1 == QRING) ? 0 : c.p.cslot + 1;
+    const u32x4* sl = reinterpret_cast<const u32x4*>(c.smem + c.p.cslot * kStageBytes);
+    acur[0] = sl[0 * 64 + c.lane];
+    acur[1] = sl[1 * 64 + c.lane];
+    const u32x4 f2 = acur[2];
+    accX[2] = Elem<T>::mfma(f2, b0, FIRST ? zero : accX[2]);
+    acur[2] = sl[2 * 64 + c.lane];
+    __builtin_amdgcn_sched_barrier(0);
+    qpipe_issue(c.p, c.ring_lds, c.wave, c.lane);
+    c.p.g++;
+    __builtin_amdgcn_sched_barrier(0);
+    const u32x4 f3 = acur[3];
+    accX[3] = Elem<T>::mfma(f3, b0, FIRST ? zero : accX[3]);
+    acur[3] = sl[3 * 64 + c.lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u32x4 f = acur[4 + i];
+        accX[i] = Elem<T>::mfma(f, b1, accX[i]);
+        acur[4 + i] = sl[(4 + i) * 64 + c.lane];
+    }
+    if (KIND != QE_NONE) qepi_chunk<T, KIND>(c, accY[ec], ec, slot, fin_q);
+}
+
+// The aux step of a quarter: frags 0..3 x bfrag (frags 4..7 of the stage are zero padding).
+template <typename T, bool FIRST>
+__device__ __forceinline__ void qstep_aux(QCtx& c, u32x4 (&acur)[8], const u32x4 bfrag,
+                                          f32x16 (&accX)[4]) {
+    const f32x16 zero = {};
+    accX[0] = Elem<T>::mfma(acur[0], bfrag, FIRST ? zero : accX[0]);
+    accX[1] = Elem<T>::mfma(acur[1], bfrag, FIRST ? zero : accX[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    if ((c.p.g & (QQ - 1)) == 0)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(QVM) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    c.p.cslot = (c.p.cslot + 1 == QRING) ? 0 : c.p.cslot + 1;
+    const u32x4* sl = reinterpret_cast<const u32x4*>(c.smem + c.p.cslot * kStageBytes);
+    acur[0] = sl[0 * 64 + c.lane];
+    acur[1] = sl[1 * 64 + c.lane];
+    const u32x4 f2 = acur[2];
+    accX[2] = Elem<T>::mfma(f2, bfrag, FIRST ? zero : accX[2]);
+    acur[2] = sl[2 * 64 + c.lane];
+    __builtin_amdgcn_sched_barrier(0);
+    qpipe_issue(c.p, c.ring_lds, c.wave, c.lane);
+    c.p.g++;
+    __builtin_amdgcn_sched_barrier(0);
+    const u32x4 f3 = acur[3];
+    accX[3] = Elem<T>::mfma(f3, bfrag, FIRST ? zero : accX[3]);
+#pragma unroll
+    for (int i = 3; i < 8; ++i) acur[i] = sl[i * 64 + c.lane];
+}
+
+// k-loop remainder j = 4 .. KP-1 (no epilogue work)
+// k-loop remainder j = 4 .. KP-1 (no epilogue work).  KP == 8 only occurs for layer 4 with a
+// 2-quarter layer 3 (K = 256), whose k-steps 8..15 were parked into hb[24..31].
+template <typename T, int KP>
+__device__ __forceinline__ void qkloop_rest(QCtx& c, u32x4 (&acur)[8], u32x4 (&hb)[32],
+                                            f32x16 (&accX)[4], const f32x16 (&accY)[4]) {
+    constexpr int OFF = (KP == 8) ? 16 : 0;
+#pragma unroll
+    for (int j = 4; j < KP; ++j)
+        qstep<T, false, QE_NONE>(c, acur, hb[OFF + 2 * j], hb[OFF + 2 * j + 1], accX, accY, 0,
+                                 0, 0);
+}
+
+struct QPend {
+    int kind, slot, fin_q;
+};
+
+// Quarter metadata (layers 1..7).  qi is the quarter index over the 26 (28) quarters.
+template <int S>
+__device__ __forceinline__ void quarter_info(int qi, int& layer, int& q, int& nq) {
+    constexpr int n3 = q_nq3(S);
+    if (qi < 4) { layer = 1; q = qi; nq = 4; }
+    else if (qi < 8) { layer = 2; q = qi - 4; nq = 4; }
+    else if (qi < 8 + n3) { layer = 3; q = qi - 8; nq = n3; }
+    else { const int r = qi - 8 - n3; layer = 4 + r / 4; q = r & 3; nq = 4; }
+}
+
+// One quarter: accumulate into accX (static set), run the pending epilogue of accY inside the
+// first 4 steps, then return this quarter's pending epilogue.
+template <typename T, int S>
+__device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u32x4 (&hb)[32],
+                                            const u32x4 bfrag, f32x16 (&accX)[4],
+                                            f32x16 (&accY)[4], QPend& pend) {
+    int layer, q, nq;
+    quarter_info<S>(qi, layer, q, nq);
+    // layer boundary: reload the parked quarters 0..2 of the previous layer into hb[0..23]
+    // (after a 2-quarter layer 3, slots 1-2 are stale and land in hb[8..23], which layer 4's
+    // K = 256 k-loop never reads: it takes k-steps 8..15 from hb[24..31])
+    if (q == 0 && layer >= 2) {   // layer 1's reload was done right after layer 0
+#pragma unroll
+        for (int i = 0; i < 24; ++i) hb[i] = c.tmp[i * 64 + c.lane];
+    }
+    const int KP = (layer == 4) ? q_kp4(S) : 16;
+    const int kind = pend.kind, slot = pend.slot, fq = pend.fin_q;
+    if (kind == QE_TMP) {
+        qstep<T, true, QE_TMP>(c, acur, hb[0], hb[1], accX, accY, 0, slot, 0);
+        qstep<T, false, QE_TMP>(c, acur, hb[2], hb[3], accX, accY, 1, slot, 0);
+        qstep<T, false, QE_TMP>(c, acur, hb[4], hb[5], accX, accY, 2, slot, 0);
+        qstep<T, false, QE_TMP>(c, acur, hb[6], hb[7], accX, accY, 3, slot, 0);
+    } else if (kind == QE_FIN) {
+        qstep<T, true, QE_FIN>(c, acur, hb[0], hb[1], accX, accY, 0, 0, fq);
+        qstep<T, false, QE_FIN>(c, acur, hb[2], hb[3], accX, accY, 1, 0, fq);
+        qstep<T, false, QE_FIN>(c, acur, hb[4], hb[5], accX, accY, 2, 0, fq);
+        qstep<T, false, QE_FIN>(c, acur, hb[6], hb[7], accX, accY, 3, 0, fq);
+    }
+    // first quarter of a layer: the previous layer's last quarter was just parked in slot 0
+    // by the 4 steps above; it always lands in hb[24..31] (k-steps 24..31; a K=256 layer 4
+    // reads its k-steps 8..15 from there, see qkloop_rest<8>), first read at pair j >= 4.
+    // A predicated select (not a branch) keeps hb's register assignment stable.
+    {
+        const bool rl = (q == 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const u32x4 v = c.tmp[i * 64 + c.lane];
+            hb[24 + i] = rl ? v : hb[24 + i];
+        }
+    }
+    if (KP == 16) qkloop_rest<T, 16>(c, acur, hb, accX, accY);
+    else qkloop_rest<T, 8>(c, acur, hb, accX, accY);
+    qstep_aux<T, false>(c, acur, bfrag, accX);
+    // this quarter's epilogue, deferred to the next quarter's first 4 steps
+    if (layer == 7) {
+        pend.kind = QE_FIN;
+        pend.fin_q = q;
+    } else {
+        pend.kind = QE_TMP;
+        pend.slot = (q < nq - 1) ? q : 0;
+    }
+}
+
+struct QArgs {
+    const uint8_t* blob;
+    const uint8_t* aux;
+    const float* w_last;
+    const float* xyz;
+    float* out;
+    float b_last;
+    int npts, tiles_per_shape, n_tiles;
+    int N, k0;
+    float vs, origin;
+};
+
+template <typename T, int S, bool POINTS>
+__global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[QLDS_TOTAL];
+    QCtx c;
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.h = c.lane >> 5;
+    c.smem = smem;
+    c.ring_lds = (uint32_t)(uintptr_t)smem;
+    c.tmp = reinterpret_cast<u32x4*>(smem + QLDS_RING + c.wave * 24576);
+    float* wl = reinterpret_cast<float*>(smem + QLDS_RING + QLDS_TMP);
+    c.wl = wl;
+    for (int i = threadIdx.x; i < 512; i += 256) wl[i] = a.w_last[i];
+    __syncthreads();
+    if ((int)blockIdx.x >= a.n_tiles) return;
+
+    QPipe& p = c.p;
+    p.blob = a.blob;
+    p.aux = a.aux;
+    p.g = 0;
+    p.islot = 0;
+    p.cslot = 0;
+    p.is = 0;
+    p.inext = 0;
+    p.itile = blockIdx.x;
+    p.ishape = p.itile / a.tiles_per_shape;
+    p.n_tiles = a.n_tiles;
+    p.tps = a.tiles_per_shape;
+    p.tstride = gridDim.x;
+    p.nst = q_nstages(S);
+    p.base4 = q_base4(S);
+    p.len4 = q_len4(S);
+    p.isrc = p.blob;
+    qpipe_boundary(p);
+#pragma unroll 1
+    for (int j = 0; j < QD; ++j) qpipe_issue(p, c.ring_lds, c.wave, c.lane);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * (QD - 1)) : "memory");
+    u32x4 acur[8];
+    qread_stage(smem, 0, c.lane, acur);
+
+#pragma unroll 1
+    for (int tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        const int shape = tile / a.tiles_per_shape;
+        const int local = tile - shape * a.tiles_per_shape;
+        int pt = local * kTilePoints + c.wave * 32 + (c.lane & 31);
+        const bool valid = pt < a.npts;
+        if (!valid) pt = a.npts - 1;
+        float x, y, z;
+        if (POINTS) {
+            const float* qq = a.xyz + ((size_t)shape * a.npts + pt) * 3;
+            x = qq[0];
+            y = qq[1];
+            z = qq[2];
+        } else {
+            grid_point(pt, a.N, a.k0, a.vs, a.origin, x, y, z);
+        }
+        u32x4 bfrag = {0u, 0u, 0u, 0u};
+        {
+            const float xh = Elem<T>::round(x), yh = Elem<T>::round(y), zh = Elem<T>::round(z);
+            const unsigned w0 = Elem<T>::pack(xh, yh);
+            const unsigned w1 = Elem<T>::pack(zh, x - xh);
+            const unsigned w2 = Elem<T>::pack(y - yh, z - zh);
+            const unsigned w3 = Elem<T>::pack(1.f, 1.f);
+            bfrag[0] = c.h ? 0u : w0;
+            bfrag[1] = c.h ? 0u : w1;
+            bfrag[2] = c.h ? 0u : w2;
+            bfrag[3] = c.h ? 0u : w3;
+        }
+        u32x4 hb[32];
+        f32x16 accA[4], accB[4];
+        c.part = 0.f;
+
+        // ---- layer 0: four aux-only quarters; 0..2 converted at once into parking slots
+        // 0..2, quarter 3 deferred like any layer's last quarter (slot 0, into hb[24..31]).
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            qstep_aux<T, true>(c, acur, bfrag, accA);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) qepi_chunk<T, QE_TMP>(c, accA[i], i, q, 0);
+        }
+        qstep_aux<T, true>(c, acur, bfrag, accB);
+#pragma unroll
+        for (int i = 0; i < 24; ++i) hb[i] = c.tmp[i * 64 + c.lane];
+
+        // ---- layers 1..7: quarters alternate A / B; epilogues deferred by one quarter
+        QPend pend = {QE_TMP, 0, 0};     // layer 0 quarter 3 (in accB) -> slot 0
+#pragma unroll 1
+        for (int qi = 0; qi < q_nquarters(S); qi += 2) {
+            run_quarter<T, S>(c, qi, acur, hb, bfrag, accA, accB, pend);
+            run_quarter<T, S>(c, qi + 1, acur, hb, bfrag, accB, accA, pend);
+        }
+        // ---- last quarter (layer 7, q = 3, set B): dot product, combine halves, tanh, store
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qepi_chunk<T, QE_FIN>(c, accB[i], i, 0, 3);
+        const float tot = c.part + __shfl_xor(c.part, 32);
+        const float sdf = tanhf(tot + a.b_last);
+        if (c.h == 0 && valid) a.out[(size_t)shape * a.npts + pt] = sdf;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <typename T, int S>
+void launch_q(const QArgs& a, bool points, hipStream_t s, int grid) {
+    if (points)
+        hipLaunchKernelGGL((dec_q_kernel<T, S, true>), dim3(grid), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((dec_q_kernel<T, S, false>), dim3(grid), dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+size_t decoder_q_aux_bytes(int B) { return (size_t)B * 8 * kStageBytes; }
+
+int decoder_q_n_stages(int skip_width) { return q_nstages(skip_width == 253 ? 256 : 512); }
+
+int decoder_q_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int B, int npts,
+                  int N, int k0, float vs, float origin, float* out, void* ws, size_t ws_bytes,
+                  hipStream_t s, int num_cus) {
+    const int S = w->skip_width == 253 ? 256 : 512;
+    LDM_REQUIRE(w->n_stages == q_nstages(S), LDM_EINVAL, "quarter layout: n_stages %d != %d",
+                w->n_stages, q_nstages(S));
+    LDM_REQUIRE(ws != nullptr && ws_bytes >= decoder_q_aux_bytes(B) && LDM_ALIGNED(ws, 16),
+                LDM_ENOSPC, "workspace too small: need %zu bytes, got %zu",
+                decoder_q_aux_bytes(B), ws_bytes);
+    {
+        const int n = B * 8 * 8 * 64;
+        if (w->dtype == LDM_BF16)
+            hipLaunchKernelGGL(qaux_pack_kernel<__bf16>, dim3((n + 255) / 256), dim3(256), 0, s,
+                               beta, w->wxyz, B, (__bf16*)ws);
+        else
+            hipLaunchKernelGGL(qaux_pack_kernel<_Float16>, dim3((n + 255) / 256), dim3(256), 0, s,
+                               beta, w->wxyz, B, (_Float16*)ws);
+        if (int e = launch_status("qaux_pack")) return e;
+    }
+    QArgs a;
+    a.blob = (const uint8_t*)w->weights;
+    a.aux = (const uint8_t*)ws;
+    a.w_last = w->w_last;
+    a.xyz = xyz;
+    a.out = out;
+    a.b_last = w->b_last;
+    a.npts = npts;
+    a.tiles_per_shape = (npts + kTilePoints - 1) / kTilePoints;
+    a.n_tiles = B * a.tiles_per_shape;
+    a.N = N;
+    a.k0 = k0;
+    a.vs = vs;
+    a.origin = origin;
+    const int grid = a.n_tiles < num_cus ? a.n_tiles : num_cus;
+    const bool points = xyz != nullptr;
+    if (w->dtype == LDM_BF16) {
+        if (S == 256) launch_q<__bf16, 256>(a, points, s, grid);
+        else launch_q<__bf16, 512>(a, points, s, grid);
+    } else {
+        if (S == 256) launch_q<_Float16, 256>(a, points, s, grid);
+        else launch_q<_Float16, 512>(a, points, s, grid);
+    }
+    return launch_status("ldm_decoder_fwd(quarter)");
+}
+
+}  // namespace ldm

@@ -52,4 +52,11 @@ __host__ __device__ constexpr int dec_n_stages(int S) {
 }
 __host__ __device__ constexpr int dec_base4(int S) { return 2 + 66 + 66 + (S / 256) * 33; }
 
+// quarter-pipelined decoder (decoder_q.hip)
+size_t decoder_q_aux_bytes(int B);
+int decoder_q_n_stages(int skip_width);
+int decoder_q_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int B, int npts,
+                  int N, int k0, float vs, float origin, float* out, void* ws, size_t ws_bytes,
+                  hipStream_t s, int num_cus);
+
 }  // namespace ldm

@@ -20,6 +20,8 @@ HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__fi
 ABI_VERSION = 1
 LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
+LAYOUT_PASS8, LAYOUT_QUARTER = 0, 1
+LAYOUT_CODES = {"pass8": LAYOUT_PASS8, "quarter": LAYOUT_QUARTER}
 EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R = 0, 1, 2, 3, 4
 MAX_BLOCKS = 8
 
@@ -33,7 +35,7 @@ class Decoder(C.Structure):
     _fields_ = [("abi_version", C.c_int32), ("dtype", C.c_int32), ("hidden", C.c_int32),
                 ("skip_width", C.c_int32), ("latent_dim", C.c_int32), ("n_stages", C.c_int32),
                 ("weights", _vp), ("wz", _vp), ("bz", _vp), ("wxyz", _vp), ("w_last", _vp),
-                ("b_last", C.c_float), ("reserved", C.c_int32)]
+                ("b_last", C.c_float), ("layout", C.c_int32)]
 
 
 class Sched(C.Structure):
@@ -69,6 +71,7 @@ SIGNATURES = [
     ("ldm_abi_version", _i, []),
     ("ldm_last_error", C.c_char_p, []),
     ("ldm_workspace_bytes", _sz, [_i, _i, _i, _i]),
+    ("ldm_workspace_bytes_layout", _sz, [_i, _i, _i, _i, _i]),
     ("ldm_grid_coords", _i, [_i, _i, _i, _f, _f, _fp, _vp]),
     ("ldm_decoder_fold", _i, [C.POINTER(Decoder), _fp, _i, _fp, _vp]),
     ("ldm_decoder_grid_fwd", _i, [C.POINTER(Decoder), _fp, _i, _i, _i, _i, _f, _f, _fp, _vp,

@@ -70,7 +70,7 @@ class SDFDecoder:
                 raise ValueError(f"layer {l}: expected W[{o},{i}], b[{o}]")
         self.weights = [w.detach().to("cpu", torch.float32).contiguous() for w in weights]
         self.biases = [b.detach().to("cpu", torch.float32).contiguous() for b in biases]
-        self._dev: Dict[Tuple[str, torch.device], Dict[str, object]] = {}
+        self._dev: Dict[Tuple[str, torch.device, str], Dict[str, object]] = {}
 
     @property
     def skip_width(self) -> int:
@@ -80,14 +80,18 @@ class SDFDecoder:
         return (self.hidden == 512 and self.n_hidden == 8 and self.skip == 4
                 and self.skip_width in (253, 512))
 
-    def device_pack(self, dtype: str, device: torch.device) -> Dict[str, object]:
-        """Packed device arrays + ``ldm_decoder_t`` (cached per dtype/device)."""
+    DEFAULT_LAYOUT = "pass8"
+
+    def device_pack(self, dtype: str, device: torch.device,
+                    layout: Optional[str] = None) -> Dict[str, object]:
+        """Packed device arrays + ``ldm_decoder_t`` (cached per dtype/device/layout)."""
         device = torch.device(device)
-        key = (dtype, device)
+        layout = layout or self.DEFAULT_LAYOUT
+        key = (dtype, device, layout)
         if key not in self._dev:
             if not self.gpu_supported():
                 raise capi.LdmError("GPU decoder kernels support DeepSDF 8x512 with skip at 4")
-            host = pack_decoder(self.weights, self.biases, self.latent_dim, dtype)
+            host = pack_decoder(self.weights, self.biases, self.latent_dim, dtype, layout)
             dev = {k: (v.to(device) if isinstance(v, torch.Tensor) else v)
                    for k, v in host.items()}
             desc = capi.Decoder()
@@ -103,6 +107,7 @@ class SDFDecoder:
             desc.wxyz = dev["wxyz"].data_ptr()
             desc.w_last = dev["w_last"].data_ptr()
             desc.b_last = host["b_last"]
+            desc.layout = capi.LAYOUT_CODES[layout]
             dev["desc"] = desc
             self._dev[key] = dev
         return self._dev[key]

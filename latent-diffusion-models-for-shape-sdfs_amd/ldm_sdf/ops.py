@@ -69,7 +69,7 @@ def decoder_grid_fwd(desc: capi.Decoder, beta: torch.Tensor, N: int, k0: int, k1
     if out.numel() != B * npts or not out.is_contiguous():
         raise capi.LdmError("decoder_grid_fwd: out must be a contiguous [B, k1-k0, N, N]")
     lib = capi.load()
-    wsb = lib.ldm_workspace_bytes(capi.LDM_OP_DECODER_GRID, B, N, desc.dtype)
+    wsb = lib.ldm_workspace_bytes_layout(capi.LDM_OP_DECODER_GRID, B, N, desc.dtype, desc.layout)
     if ws is None or ws.numel() < wsb:
         ws = torch.empty(max(wsb, 16), device=beta.device, dtype=torch.uint8)
     capi.check(lib.ldm_decoder_grid_fwd(C.byref(desc), beta.data_ptr(), B, N, k0, k1,
@@ -91,7 +91,8 @@ def decoder_points_fwd(desc: capi.Decoder, beta: torch.Tensor, xyz: torch.Tensor
     if out is None:
         out = torch.empty(B, P, device=xyz.device, dtype=torch.float32)
     lib = capi.load()
-    wsb = lib.ldm_workspace_bytes(capi.LDM_OP_DECODER_POINTS, B, P, desc.dtype)
+    wsb = lib.ldm_workspace_bytes_layout(capi.LDM_OP_DECODER_POINTS, B, P, desc.dtype,
+                                         desc.layout)
     if ws is None or ws.numel() < wsb:
         ws = torch.empty(max(wsb, 16), device=xyz.device, dtype=torch.uint8)
     capi.check(lib.ldm_decoder_points_fwd(C.byref(desc), beta.data_ptr(), xyz.data_ptr(), B, P,

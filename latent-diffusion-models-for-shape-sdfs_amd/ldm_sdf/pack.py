@@ -70,8 +70,24 @@ def stage_plan(skip_width: int) -> List[StageRef]:
     return plan
 
 
-def n_stages(skip_width: int) -> int:
-    return len(stage_plan(skip_width))
+def n_stages(skip_width: int, layout: str = "pass8") -> int:
+    return len(stage_plan_quarter(skip_width) if layout == "quarter" else stage_plan(skip_width))
+
+
+def stage_plan_quarter(skip_width: int) -> List[StageRef]:
+    """Stage sequence of the quarter-pipelined kernel (csrc/decoder_q.hip): per layer, quarters
+    of 4 m-chunks; per quarter, K/32 pair-stages (4 chunks x k-steps 2j, 2j+1) then one aux
+    stage.  ``pass_`` holds the quarter index and ``ks`` the pair index j (-1 = aux)."""
+    S = skip_pad(skip_width)
+    layers = [(0, 4, 0), (1, 4, 16), (2, 4, 16), (3, S // 128, 16), (4, 4, S // 32),
+              (5, 4, 16), (6, 4, 16), (7, 4, 16)]
+    plan = []
+    for (l, nq, kp) in layers:
+        for q in range(nq):
+            for j in range(kp):
+                plan.append(StageRef(l, q, j, False))
+            plan.append(StageRef(l, q, -1, l in (0, 4)))
+    return plan
 
 
 def _round(x: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
@@ -146,6 +162,50 @@ def pack_stage_blob(pieces: Dict[str, torch.Tensor], dt: torch.dtype) -> torch.T
     return out
 
 
+def pack_stage_blob_quarter(pieces: Dict[str, torch.Tensor], dt: torch.dtype) -> torch.Tensor:
+    """Quarter-layout blob ``[n_stages, 8, 64, 8]``: main stage (layer, quarter q, pair j) frag
+    ``i = e*4 + c`` is the A fragment of m-chunk ``4q + c`` at k-step ``2j + e``; the aux stage
+    has ``[0,0,0,0,0,0,b_hi,b_lo]`` in frags 0..3 (lanes < 32) and zero frags 4..7."""
+    sw = pieces["skip_width"]
+    S = skip_pad(sw)
+    plan = stage_plan_quarter(sw)
+    lanes = np.arange(64)
+    rows_l = lanes & 31
+    kcols = np.array([[PERM[8 * (l >> 5) + j] for j in range(8)] for l in lanes])  # [64, 8]
+    padded = {}
+    for l in range(1, 8):
+        w = pieces["main"][l]
+        M = S if l == 3 else H
+        K = S if l == 4 else H
+        wp = torch.zeros(M, K, dtype=torch.float64)
+        wp[:w.shape[0], :w.shape[1]] = w
+        padded[l] = _round(wp, dt)
+    out = torch.zeros(len(plan), 8, 64, 8, dtype=dt)
+    fr = np.arange(8)
+    chunk_of = fr % 4            # frag i = e*4 + c
+    e_of = fr // 4
+    for si, st in enumerate(plan):
+        if st.per_shape:
+            continue
+        q = st.pass_
+        if st.ks >= 0:
+            wp = padded[st.layer]
+            rows = (4 * q + chunk_of)[:, None] * 32 + rows_l[None, :]              # [8, 64]
+            ks = 2 * st.ks + e_of                                                   # [8]
+            cols = ks[:, None, None] * 16 + kcols[None, :, :]                       # [8, 64, 8]
+            out[si] = wp[torch.from_numpy(rows)[:, :, None], torch.from_numpy(cols)]
+        else:
+            b = pieces["bias"][st.layer]
+            bp = torch.zeros(S if st.layer == 3 else H, dtype=torch.float64)
+            bp[:b.shape[0]] = b
+            hi, lo = _hi_lo(bp, dt)
+            f = (4 * q + np.arange(4))[:, None] * 32 + np.arange(32)[None, :]      # [4, 32]
+            ft = torch.from_numpy(f)
+            out[si, :4, :32, 6] = hi[ft]
+            out[si, :4, :32, 7] = lo[ft]
+    return out
+
+
 def permute_w_last(w_last: torch.Tensor) -> torch.Tensor:
     """``wl[(mc*2 + h)*16 + r] = w8[32 mc + (r&3) + 8 (r>>2) + 4 h]`` (accumulator row order)."""
     idx = [32 * mc + (r & 3) + 8 * (r >> 2) + 4 * h
@@ -164,8 +224,10 @@ def pack_f32_blob(pieces: Dict[str, torch.Tensor]) -> torch.Tensor:
     return torch.cat(parts).to(torch.float32)
 
 
-def pack_decoder(weights, biases, latent_dim: int, dtype: str) -> Dict[str, object]:
-    """All host-side arrays of an ``ldm_decoder_t`` for ``dtype`` in {fp32, bf16, fp16}."""
+def pack_decoder(weights, biases, latent_dim: int, dtype: str,
+                 layout: str = "quarter") -> Dict[str, object]:
+    """All host-side arrays of an ``ldm_decoder_t`` for ``dtype`` in {fp32, bf16, fp16}; the
+    16-bit stage blob in ``layout`` ("quarter": csrc/decoder_q.hip, "pass8": decoder.hip)."""
     pieces = canonical_pieces(weights, biases, latent_dim)
     out = {
         "skip_width": pieces["skip_width"],
@@ -175,15 +237,18 @@ def pack_decoder(weights, biases, latent_dim: int, dtype: str) -> Dict[str, obje
         "wxyz": pieces["wxyz"].to(torch.float32).contiguous(),
         "b_last": float(pieces["b_last"]),
     }
+    out["layout"] = layout
     if dtype == "fp32":
         out["weights"] = pack_f32_blob(pieces)
         out["w_last"] = pieces["w_last"].to(torch.float32).contiguous()
         out["n_stages"] = 0
     elif dtype in ("bf16", "fp16"):
         dt = torch.bfloat16 if dtype == "bf16" else torch.float16
-        out["weights"] = pack_stage_blob(pieces, dt).contiguous()
+        blob = (pack_stage_blob_quarter(pieces, dt) if layout == "quarter"
+                else pack_stage_blob(pieces, dt))
+        out["weights"] = blob.contiguous()
         out["w_last"] = permute_w_last(pieces["w_last"]).contiguous()
-        out["n_stages"] = n_stages(pieces["skip_width"])
+        out["n_stages"] = n_stages(pieces["skip_width"], layout)
     else:
         raise ValueError(f"unknown decoder dtype {dtype!r}")
     return out

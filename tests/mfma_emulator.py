@@ -142,3 +142,86 @@ def emulate(packed: dict, beta: np.ndarray, xyz: np.ndarray, dtype: str) -> np.n
             tot = part[:32] + part[32:]
             out[b, g0:g0 + 32] = np.tanh(tot + packed["b_last"])
     return out
+
+
+def aux_stage_quarter(beta_l: np.ndarray, wxyz_l: np.ndarray, q: int, dt) -> np.ndarray:
+    """Per-shape aux stage of the quarter layout (csrc/decoder_q.hip qaux_pack_kernel)."""
+    st = np.zeros((8, 64, 8))
+    for c in range(4):
+        f = (4 * q + c) * 32 + np.arange(32)
+        hi = round_dt(beta_l[f], dt)
+        lo = round_dt(beta_l[f] - hi, dt)
+        w = wxyz_l[f]
+        st[c, :32, 0:3] = round_dt(w, dt)
+        st[c, :32, 3:6] = round_dt(w, dt)
+        st[c, :32, 6] = hi
+        st[c, :32, 7] = lo
+    return st
+
+
+def emulate_quarter(packed: dict, beta: np.ndarray, xyz: np.ndarray, dtype: str) -> np.ndarray:
+    """Fragment-level replay of the quarter layout: per quarter, acc[c] += A(frag e*4+c) @
+    B(hb[2j+e]) over its pair-stages plus the aux stage (frags 0..3 x the xyz/one fragment);
+    the layer's new k-step 8q+2c+s is chunk c of quarter q converted (16-bit, ReLU)."""
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float16
+    blob = packed["weights"].to(torch.float64).numpy()
+    wl = packed["w_last"].numpy().astype(np.float64)
+    wxyz = packed["wxyz"].numpy().astype(np.float64)
+    plan = pack.stage_plan_quarter(packed["skip_width"])
+    B, P, _ = xyz.shape
+    out = np.zeros((B, P))
+    for b in range(B):
+        auxs = [aux_stage_quarter(beta[b, 0], wxyz[0], q, dt) for q in range(4)] + \
+               [aux_stage_quarter(beta[b, 1], wxyz[1], q, dt) for q in range(4)]
+        for g0 in range(0, P, 32):
+            x = xyz[b, g0:g0 + 32].astype(np.float32)
+            hi = round_dt(x, dt)
+            lo = round_dt(x.astype(np.float64) - hi, dt)
+            Baux = np.zeros((16, 32))
+            Baux[0:3] = hi.T
+            Baux[3:6] = lo.T
+            Baux[6:8] = 1.0
+            hb = [np.zeros((16, 32)) for _ in range(32)]
+            new = {}
+            part = np.zeros(64)
+            si, aux_seen = 0, 0
+            while si < len(plan):
+                st0 = plan[si]
+                layer, q = st0.layer, st0.pass_
+                C = [np.zeros((32, 32)) for _ in range(4)]
+                while True:
+                    st = plan[si]
+                    data = auxs[aux_seen] if st.per_shape else blob[si]
+                    if st.per_shape:
+                        aux_seen += 1
+                    if st.ks < 0:
+                        for c in range(4):
+                            C[c] += frag_to_A(data[c]) @ Baux
+                    else:
+                        for e in range(2):
+                            for c in range(4):
+                                C[c] += frag_to_A(data[e * 4 + c]) @ hb[2 * st.ks + e]
+                    si += 1
+                    if st.ks < 0:
+                        break
+                if layer == 7:
+                    for c in range(4):
+                        mc = 4 * q + c
+                        for h in range(2):
+                            rows = acc_rows(h)
+                            w = wl[(mc * 2 + h) * 16:(mc * 2 + h) * 16 + 16]
+                            part[h * 32:(h + 1) * 32] += (np.maximum(C[c][rows, :], 0) *
+                                                          w[:, None]).sum(0)
+                else:
+                    for c in range(4):
+                        f0, f1 = acc_to_Bmats(C[c], dt)
+                        new[8 * q + 2 * c] = f0
+                        new[8 * q + 2 * c + 1] = f1
+                    last_q = (si >= len(plan)) or plan[si].layer != layer
+                    if last_q:
+                        for k, v in new.items():
+                            hb[k] = v
+                        new = {}
+            tot = part[:32] + part[32:]
+            out[b, g0:g0 + 32] = np.tanh(tot + packed["b_last"])
+    return out

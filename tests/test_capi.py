@@ -36,7 +36,8 @@ def test_abi_version_and_error_path_without_gpu():
     assert lib.ldm_grid_coords(0, 0, 0, 0.0, 0.0, None, None) == -22
     assert b"bad grid slab" in lib.ldm_last_error()
     assert lib.ldm_decoder_grid_fwd(None, None, 1, 8, 0, 8, 0.1, -1.0, None, None, 0, None) != 0
-    assert lib.ldm_workspace_bytes(1, 4, 256, 1) == 4 * 4 * 8192
+    assert lib.ldm_workspace_bytes(1, 4, 256, 1) == 4 * 8 * 8192            # quarter layout
+    assert lib.ldm_workspace_bytes_layout(1, 4, 256, 1, 0) == 4 * 4 * 8192   # pass8 layout
 
 
 def test_struct_layouts_match_c():

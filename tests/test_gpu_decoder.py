@@ -67,23 +67,33 @@ def test_fold_matches_oracle(dev, decoder, small):
     assert (beta - want).abs().max() < 1e-5
 
 
+@pytest.mark.parametrize("layout", ["quarter", "pass8"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
-def test_decode_grid_32_vs_golden(dev, decoder, small, dtype):
+def test_decode_grid_32_vs_golden(dev, decoder, small, dtype, layout):
     import ldm_sdf
     z = torch.from_numpy(small["z"]).to(dev)
-    sdf = ldm_sdf.decode(decoder, z, 32, dtype=dtype).cpu().double().numpy()
+    decoder.DEFAULT_LAYOUT = layout
+    try:
+        sdf = ldm_sdf.decode(decoder, z, 32, dtype=dtype).cpu().double().numpy()
+    finally:
+        del decoder.DEFAULT_LAYOUT          # back to the class default
     want = small["sdf_grid"].reshape(2, 32, 32, 32)
     err = np.abs(sdf - want).max()
     assert err <= TOL[dtype], (dtype, err)
     assert np.isfinite(sdf).all()
 
 
+@pytest.mark.parametrize("layout", ["quarter", "pass8"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
-def test_decode_points_ragged_vs_golden(dev, decoder, small, dtype):
+def test_decode_points_ragged_vs_golden(dev, decoder, small, dtype, layout):
     import ldm_sdf
     z = torch.from_numpy(small["z"]).to(dev)
     pts = torch.from_numpy(small["pts"]).to(dev)          # [2, 1000, 3], 1000 % 128 != 0
-    got = ldm_sdf.decode_points(decoder, z, pts, dtype=dtype).cpu().double().numpy()
+    decoder.DEFAULT_LAYOUT = layout
+    try:
+        got = ldm_sdf.decode_points(decoder, z, pts, dtype=dtype).cpu().double().numpy()
+    finally:
+        del decoder.DEFAULT_LAYOUT          # back to the class default
     err = np.abs(got - small["sdf_pts"]).max()
     assert err <= TOL[dtype], (dtype, err)
 
@@ -110,17 +120,19 @@ def test_widen_skip_fp16(dev):
     assert dec.widen_skip and dec.skip_width == 512
     z = torch.from_numpy(g["z"]).to(dev)
     pts = torch.from_numpy(g["pts"]).to(dev)
-    for dt in ("fp16", "fp32"):
+    for dt, lay in (("fp16", "quarter"), ("fp16", "pass8"), ("fp32", "quarter")):
+        dec.DEFAULT_LAYOUT = lay
         got = ldm_sdf.decode_points(dec, z, pts, dtype=dt).cpu().double().numpy()
-        assert np.abs(got - g["sdf_pts"]).max() <= TOL[dt], dt
+        assert np.abs(got - g["sdf_pts"]).max() <= TOL[dt], (dt, lay)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_slab_equals_slice_bitwise(dev, decoder, small, dtype):
+@pytest.mark.parametrize("dtype,layout", [("fp32", "quarter"), ("bf16", "quarter"),
+                                          ("bf16", "pass8")])
+def test_slab_equals_slice_bitwise(dev, decoder, small, dtype, layout):
     """Each point's value is independent of its tile/slab: slabs are bitwise slices."""
     from ldm_sdf import ops
     z = torch.from_numpy(small["z"]).to(dev)
-    pk = decoder.device_pack(dtype, dev)
+    pk = decoder.device_pack(dtype, dev, layout=layout)
     beta = ops.decoder_fold(pk["desc"], z)
     N = 40
     full = ops.decoder_grid_fwd(pk["desc"], beta, N, 0, N)
@@ -132,14 +144,19 @@ def test_slab_equals_slice_bitwise(dev, decoder, small, dtype):
     assert torch.equal(one[0], full[1])
 
 
-def test_many_tiles_persistent_loop_subset(dev, decoder):
+@pytest.mark.parametrize("layout", ["quarter", "pass8"])
+def test_many_tiles_persistent_loop_subset(dev, decoder, layout):
     """64^3 x 3 shapes = 6144 tiles (> 1 per CU): spot-check vs the oracle on a subset."""
     import ldm_sdf
     from oracle import ref_cpu as R
     g = torch.Generator().manual_seed(3)
     z = torch.randn(3, 256, generator=g) * 0.1
     N = 64
-    sdf = ldm_sdf.decode(decoder, z.to(dev), N, dtype="bf16").cpu()
+    decoder.DEFAULT_LAYOUT = layout
+    try:
+        sdf = ldm_sdf.decode(decoder, z.to(dev), N, dtype="bf16").cpu()
+    finally:
+        del decoder.DEFAULT_LAYOUT          # back to the class default
     idx = torch.randint(0, N ** 3, (3, 600), generator=g)
     grid = torch.from_numpy(R.grid_coords_np(N))
     p = R.make_decoder_params(seed=1234)

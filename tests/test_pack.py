@@ -6,7 +6,7 @@ import torch
 
 from ldm_sdf import pack
 from oracle import ref_cpu as R
-from tests.mfma_emulator import emulate
+from tests.mfma_emulator import emulate, emulate_quarter
 
 
 def test_perm_is_accumulator_row_order():
@@ -15,6 +15,17 @@ def test_perm_is_accumulator_row_order():
         for j in range(8):
             assert pack.PERM[8 * h + j] == 8 * (j >> 2) + 4 * h + (j & 3)
     assert sorted(pack.PERM.tolist()) == list(range(16))
+
+
+@pytest.mark.parametrize("sw", [253, 512])
+def test_quarter_plan_matches_kernel_constants(sw):
+    S = pack.skip_pad(sw)
+    plan = pack.stage_plan_quarter(sw)
+    base4 = 4 + 68 + 68 + (S // 128) * 17
+    len4 = S // 32 + 1
+    assert len(plan) == base4 + 4 * len4 + 3 * 68                 # csrc q_nstages
+    per = [i for i, s in enumerate(plan) if s.per_shape]
+    assert per == [0, 1, 2, 3] + [base4 + len4 * (k + 1) - 1 for k in range(4)]
 
 
 @pytest.mark.parametrize("sw", [253, 512])
@@ -48,11 +59,13 @@ def test_emulated_kernel_matches_oracle(dtype, tol):
     z = torch.randn(2, 256, generator=g, dtype=torch.float64) * 0.1
     xyz = (torch.rand(2, 64, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
     want = R.decoder_forward(p, z, xyz.double()).numpy()
-    packed = pack.pack_decoder(p.weights, p.biases, 256, dtype)
     beta = R.latent_fold(p, z).float().numpy()
-    got = emulate(packed, beta, xyz.numpy(), dtype)
-    err = np.abs(got - want).max()
+    packed = pack.pack_decoder(p.weights, p.biases, 256, dtype, layout="pass8")
+    err = np.abs(emulate(packed, beta, xyz.numpy(), dtype) - want).max()
     assert err < tol, err
+    packed_q = pack.pack_decoder(p.weights, p.biases, 256, dtype, layout="quarter")
+    err_q = np.abs(emulate_quarter(packed_q, beta, xyz.numpy(), dtype) - want).max()
+    assert err_q < tol, err_q
     # and it is not trivially close: outputs vary
     assert want.std() > 0.005
 
@@ -63,6 +76,8 @@ def test_emulated_widen_skip_fp16():
     z = torch.randn(1, 1024, generator=g, dtype=torch.float64) * 0.1
     xyz = (torch.rand(1, 32, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
     want = R.decoder_forward(p, z, xyz.double()).numpy()
-    packed = pack.pack_decoder(p.weights, p.biases, 1024, "fp16")
-    got = emulate(packed, R.latent_fold(p, z).float().numpy(), xyz.numpy(), "fp16")
-    assert np.abs(got - want).max() < 3e-3
+    beta = R.latent_fold(p, z).float().numpy()
+    packed = pack.pack_decoder(p.weights, p.biases, 1024, "fp16", layout="pass8")
+    assert np.abs(emulate(packed, beta, xyz.numpy(), "fp16") - want).max() < 3e-3
+    packed_q = pack.pack_decoder(p.weights, p.biases, 1024, "fp16", layout="quarter")
+    assert np.abs(emulate_quarter(packed_q, beta, xyz.numpy(), "fp16") - want).max() < 3e-3
