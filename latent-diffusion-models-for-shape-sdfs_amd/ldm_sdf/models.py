@@ -80,7 +80,7 @@ class SDFDecoder:
         return (self.hidden == 512 and self.n_hidden == 8 and self.skip == 4
                 and self.skip_width in (253, 512))
 
-    DEFAULT_LAYOUT = "pass8"
+    DEFAULT_LAYOUT = "quarter"
 
     def device_pack(self, dtype: str, device: torch.device,
                     layout: Optional[str] = None) -> Dict[str, object]:
