@@ -20,6 +20,14 @@ namespace ldm {
 namespace {
 using namespace dec;
 
+// Timing ablations for diagnostic builds only (scripts/ablate_decoder.sh; results are wrong):
+// 1 = no s_barrier/vmcnt wait, 2 = no DMA issue either, 4 = no epilogue, 8 = no A reads.
+#ifndef QABL
+#define QABL 0
+#endif
+
+#define QRD(sl, i) ((QABL & 8) ? acur[i] : (sl)[(i) * 64 + c.lane])
+
 constexpr int QRING = 7;
 constexpr int QQ = 2;                         // barrier period (steps)
 constexpr int QD = 6;                         // stages issued ahead
@@ -77,11 +85,15 @@ __global__ void qaux_pack_kernel(const float* __restrict__ beta, const float* __
 struct QPipe {
     const uint8_t* blob;
     const uint8_t* aux;
-    const uint8_t* isrc;
-    int g, islot, cslot, is, inext, itile, ishape;
+    const uint8_t* isrc;        // source of the next stage to issue (wave-uniform)
+    uint32_t islot, ring_beg, ring_end;   // LDS byte address of this wave's piece of that slot
+    int is, inext, itile, ishape;
     int n_tiles, tps, tstride, nst, base4, len4;
 };
 
+// Slow path, at the 8 per-tile points where the source switches between the blob and the
+// shape's aux stages (and at the tile seam).  Past the last tile every stage comes from the
+// blob (dummy copies keep every wave's vmcnt arithmetic exact).
 __device__ __forceinline__ void qpipe_boundary(QPipe& p) {
     if (p.is == p.nst) {
         p.is = 0;
@@ -97,22 +109,23 @@ __device__ __forceinline__ void qpipe_boundary(QPipe& p) {
         const int k = r / p.len4;
         if (r - k * p.len4 == p.len4 - 1) ai = 4 + k;
     }
-    if (ai >= 0) {
+    if (ai >= 0 && p.itile < p.n_tiles) {
         p.isrc = p.aux + ((size_t)p.ishape * 8 + ai) * kStageBytes;
         p.inext = s + 1;
     } else {
         p.isrc = p.blob + (size_t)s * kStageBytes;
-        if (s < p.base4) p.inext = p.base4 + p.len4 - 1;
+        if (p.itile >= p.n_tiles) p.inext = p.nst;
+        else if (s < 4) p.inext = 4;
+        else if (s < p.base4) p.inext = p.base4 + p.len4 - 1;
         else if (s < p.base4 + 4 * p.len4) p.inext = p.base4 + p.len4 * ((s - p.base4) / p.len4 + 1) - 1;
         else p.inext = p.nst;
     }
 }
 
-__device__ __forceinline__ void qpipe_issue(QPipe& p, uint32_t ring_lds, int wave, int lane) {
-    const uint8_t* src = (p.itile < p.n_tiles) ? p.isrc : p.blob;   // dummy past the end
-    glds16x2(src + wave * 2048 + lane * 16,
-             ring_lds + (uint32_t)p.islot * kStageBytes + (uint32_t)wave * 2048u);
-    p.islot = (p.islot + 1 == QRING) ? 0 : p.islot + 1;
+// Fast path: ~12 instructions (2 LDS-DMA pieces, one M0 write, scalar pointer bumps).
+__device__ __forceinline__ void qpipe_issue(QPipe& p, uint32_t voff) {
+    glds2_saddr(p.isrc, voff, p.islot);
+    p.islot = (p.islot + kStageBytes == p.ring_end) ? p.ring_beg : p.islot + kStageBytes;
     p.isrc += kStageBytes;
     if (++p.is == p.inext) qpipe_boundary(p);
 }
@@ -129,7 +142,8 @@ __device__ __forceinline__ void qread_stage(const char* smem, int slot, int lane
 struct QCtx {
     QPipe p;
     const char* smem;
-    uint32_t ring_lds;
+    uint32_t coff;       // LDS byte offset of the stage being consumed
+    uint32_t voff;       // wave * 2 KiB + lane * 16: this lane's bytes of a stage
     int wave, lane, h;
     u32x4* tmp;          // this wave's parked quarter outputs: [24 frags][64 lanes]
     const float* wl;     // permuted final weights [16 mc][2 h][16]
@@ -164,83 +178,90 @@ __device__ __forceinline__ void qepi_chunk(QCtx& c, const f32x16& a, int chunk, 
     }
 }
 
+// Consumer side of a step: advance to the next ring slot (byte offset, wraps at QRING).
+__device__ __forceinline__ const u32x4* qnext_slot(QCtx& c) {
+    c.coff = (c.coff + kStageBytes == QRING * kStageBytes) ? 0u : c.coff + kStageBytes;
+    return reinterpret_cast<const u32x4*>(c.smem + c.coff);
+}
+
+// Barrier + RAW wait, every QQ = 2 steps.  `bar` is a compile-time constant after inlining:
+// every quarter has an odd number of steps, so quarter A of a pair starts on an even step and
+// quarter B on an odd one (run_quarter's PAR).
+__device__ __forceinline__ void qbarrier(bool bar) {
+    if (!(QABL & 3) && bar)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(QVM) : "memory");
+}
+
 // One pipeline step on a pair-stage: 8 MFMAs (4 chunks x k-steps 2j, 2j+1) into accX, plus
 // (KIND != QE_NONE) chunk `ec` of the pending epilogue on accY, interleaved with the last 5.
 template <typename T, bool FIRST, int KIND>
 __device__ __forceinline__ void qstep(QCtx& c, u32x4 (&acur)[8], const u32x4 b0, const u32x4 b1,
                                       f32x16 (&accX)[4], const f32x16 (&accY)[4], int ec,
-                                      int slot, int fin_q) {
+                                      int slot, int fin_q, bool bar) {
     const f32x16 zero = {};
     accX[0] = Elem<T>::mfma(acur[0], b0, FIRST ? zero : accX[0]);
     accX[1] = Elem<T>::mfma(acur[1], b0, FIRST ? zero : accX[1]);
     __builtin_amdgcn_sched_barrier(0);
-    if ((c.p.g & (QQ - 1)) == 0)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(QVM) : "memory");
+    qbarrier(bar);
     __builtin_amdgcn_sched_barrier(0);
     // rolling fragment buffer: fragment i of the next stage is read right after fragment i of
     // this stage has been consumed (>= 6 MFMAs of latency cover, ~40 live fragment VGPRs)
-    c.p.cslot = (c.p.cslot + 1 == QRING) ? 0 : c.p.cslot + 1;
-    const u32x4* sl = reinterpret_cast<const u32x4*>(c.smem + c.p.cslot * kStageBytes);
-    acur[0] = sl[0 * 64 + c.lane];
-    acur[1] = sl[1 * 64 + c.lane];
+    const u32x4* sl = qnext_slot(c);
+    acur[0] = QRD(sl, 0);
+    acur[1] = QRD(sl, 1);
     const u32x4 f2 = acur[2];
     accX[2] = Elem<T>::mfma(f2, b0, FIRST ? zero : accX[2]);
-    acur[2] = sl[2 * 64 + c.lane];
+    acur[2] = QRD(sl, 2);
     __builtin_amdgcn_sched_barrier(0);
-    qpipe_issue(c.p, c.ring_lds, c.wave, c.lane);
-    c.p.g++;
+    if (!(QABL & 2)) qpipe_issue(c.p, c.voff);
     __builtin_amdgcn_sched_barrier(0);
     const u32x4 f3 = acur[3];
     accX[3] = Elem<T>::mfma(f3, b0, FIRST ? zero : accX[3]);
-    acur[3] = sl[3 * 64 + c.lane];
+    acur[3] = QRD(sl, 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const u32x4 f = acur[4 + i];
         accX[i] = Elem<T>::mfma(f, b1, accX[i]);
-        acur[4 + i] = sl[(4 + i) * 64 + c.lane];
+        acur[4 + i] = QRD(sl, 4 + i);
     }
-    if (KIND != QE_NONE) qepi_chunk<T, KIND>(c, accY[ec], ec, slot, fin_q);
+    if (KIND != QE_NONE && !(QABL & 4)) qepi_chunk<T, KIND>(c, accY[ec], ec, slot, fin_q);
 }
 
 // The aux step of a quarter: frags 0..3 x bfrag (frags 4..7 of the stage are zero padding).
 template <typename T, bool FIRST>
 __device__ __forceinline__ void qstep_aux(QCtx& c, u32x4 (&acur)[8], const u32x4 bfrag,
-                                          f32x16 (&accX)[4]) {
+                                          f32x16 (&accX)[4], bool bar) {
     const f32x16 zero = {};
     accX[0] = Elem<T>::mfma(acur[0], bfrag, FIRST ? zero : accX[0]);
     accX[1] = Elem<T>::mfma(acur[1], bfrag, FIRST ? zero : accX[1]);
     __builtin_amdgcn_sched_barrier(0);
-    if ((c.p.g & (QQ - 1)) == 0)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(QVM) : "memory");
+    qbarrier(bar);
     __builtin_amdgcn_sched_barrier(0);
-    c.p.cslot = (c.p.cslot + 1 == QRING) ? 0 : c.p.cslot + 1;
-    const u32x4* sl = reinterpret_cast<const u32x4*>(c.smem + c.p.cslot * kStageBytes);
-    acur[0] = sl[0 * 64 + c.lane];
-    acur[1] = sl[1 * 64 + c.lane];
+    const u32x4* sl = qnext_slot(c);
+    acur[0] = QRD(sl, 0);
+    acur[1] = QRD(sl, 1);
     const u32x4 f2 = acur[2];
     accX[2] = Elem<T>::mfma(f2, bfrag, FIRST ? zero : accX[2]);
-    acur[2] = sl[2 * 64 + c.lane];
+    acur[2] = QRD(sl, 2);
     __builtin_amdgcn_sched_barrier(0);
-    qpipe_issue(c.p, c.ring_lds, c.wave, c.lane);
-    c.p.g++;
+    if (!(QABL & 2)) qpipe_issue(c.p, c.voff);
     __builtin_amdgcn_sched_barrier(0);
     const u32x4 f3 = acur[3];
     accX[3] = Elem<T>::mfma(f3, bfrag, FIRST ? zero : accX[3]);
 #pragma unroll
-    for (int i = 3; i < 8; ++i) acur[i] = sl[i * 64 + c.lane];
+    for (int i = 3; i < 8; ++i) acur[i] = QRD(sl, i);
 }
 
-// k-loop remainder j = 4 .. KP-1 (no epilogue work)
 // k-loop remainder j = 4 .. KP-1 (no epilogue work).  KP == 8 only occurs for layer 4 with a
 // 2-quarter layer 3 (K = 256), whose k-steps 8..15 were parked into hb[24..31].
-template <typename T, int KP>
+template <typename T, int KP, int PAR>
 __device__ __forceinline__ void qkloop_rest(QCtx& c, u32x4 (&acur)[8], u32x4 (&hb)[32],
                                             f32x16 (&accX)[4], const f32x16 (&accY)[4]) {
     constexpr int OFF = (KP == 8) ? 16 : 0;
 #pragma unroll
     for (int j = 4; j < KP; ++j)
         qstep<T, false, QE_NONE>(c, acur, hb[OFF + 2 * j], hb[OFF + 2 * j + 1], accX, accY, 0,
-                                 0, 0);
+                                 0, 0, ((j + PAR) & 1) == 0);
 }
 
 struct QPend {
@@ -259,7 +280,7 @@ __device__ __forceinline__ void quarter_info(int qi, int& layer, int& q, int& nq
 
 // One quarter: accumulate into accX (static set), run the pending epilogue of accY inside the
 // first 4 steps, then return this quarter's pending epilogue.
-template <typename T, int S>
+template <typename T, int S, int PAR>
 __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u32x4 (&hb)[32],
                                             const u32x4 bfrag, f32x16 (&accX)[4],
                                             f32x16 (&accY)[4], QPend& pend) {
@@ -275,15 +296,15 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
     const int KP = (layer == 4) ? q_kp4(S) : 16;
     const int kind = pend.kind, slot = pend.slot, fq = pend.fin_q;
     if (kind == QE_TMP) {
-        qstep<T, true, QE_TMP>(c, acur, hb[0], hb[1], accX, accY, 0, slot, 0);
-        qstep<T, false, QE_TMP>(c, acur, hb[2], hb[3], accX, accY, 1, slot, 0);
-        qstep<T, false, QE_TMP>(c, acur, hb[4], hb[5], accX, accY, 2, slot, 0);
-        qstep<T, false, QE_TMP>(c, acur, hb[6], hb[7], accX, accY, 3, slot, 0);
+        qstep<T, true, QE_TMP>(c, acur, hb[0], hb[1], accX, accY, 0, slot, 0, ((0 + PAR) & 1) == 0);
+        qstep<T, false, QE_TMP>(c, acur, hb[2], hb[3], accX, accY, 1, slot, 0, ((1 + PAR) & 1) == 0);
+        qstep<T, false, QE_TMP>(c, acur, hb[4], hb[5], accX, accY, 2, slot, 0, ((2 + PAR) & 1) == 0);
+        qstep<T, false, QE_TMP>(c, acur, hb[6], hb[7], accX, accY, 3, slot, 0, ((3 + PAR) & 1) == 0);
     } else if (kind == QE_FIN) {
-        qstep<T, true, QE_FIN>(c, acur, hb[0], hb[1], accX, accY, 0, 0, fq);
-        qstep<T, false, QE_FIN>(c, acur, hb[2], hb[3], accX, accY, 1, 0, fq);
-        qstep<T, false, QE_FIN>(c, acur, hb[4], hb[5], accX, accY, 2, 0, fq);
-        qstep<T, false, QE_FIN>(c, acur, hb[6], hb[7], accX, accY, 3, 0, fq);
+        qstep<T, true, QE_FIN>(c, acur, hb[0], hb[1], accX, accY, 0, 0, fq, ((0 + PAR) & 1) == 0);
+        qstep<T, false, QE_FIN>(c, acur, hb[2], hb[3], accX, accY, 1, 0, fq, ((1 + PAR) & 1) == 0);
+        qstep<T, false, QE_FIN>(c, acur, hb[4], hb[5], accX, accY, 2, 0, fq, ((2 + PAR) & 1) == 0);
+        qstep<T, false, QE_FIN>(c, acur, hb[6], hb[7], accX, accY, 3, 0, fq, ((3 + PAR) & 1) == 0);
     }
     // first quarter of a layer: the previous layer's last quarter was just parked in slot 0
     // by the 4 steps above; it always lands in hb[24..31] (k-steps 24..31; a K=256 layer 4
@@ -297,9 +318,9 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
             hb[24 + i] = rl ? v : hb[24 + i];
         }
     }
-    if (KP == 16) qkloop_rest<T, 16>(c, acur, hb, accX, accY);
-    else qkloop_rest<T, 8>(c, acur, hb, accX, accY);
-    qstep_aux<T, false>(c, acur, bfrag, accX);
+    if (KP == 16) qkloop_rest<T, 16, PAR>(c, acur, hb, accX, accY);
+    else qkloop_rest<T, 8, PAR>(c, acur, hb, accX, accY);
+    qstep_aux<T, false>(c, acur, bfrag, accX, PAR == 0);     // step KP (even)
     // this quarter's epilogue, deferred to the next quarter's first 4 steps
     if (layer == 7) {
         pend.kind = QE_FIN;
@@ -328,9 +349,10 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
     QCtx c;
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c.voff = (uint32_t)c.wave * 2048u + (uint32_t)c.lane * 16u;
     c.h = c.lane >> 5;
     c.smem = smem;
-    c.ring_lds = (uint32_t)(uintptr_t)smem;
+    c.coff = 0;
     c.tmp = reinterpret_cast<u32x4*>(smem + QLDS_RING + c.wave * 24576);
     float* wl = reinterpret_cast<float*>(smem + QLDS_RING + QLDS_TMP);
     c.wl = wl;
@@ -341,9 +363,9 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
     QPipe& p = c.p;
     p.blob = a.blob;
     p.aux = a.aux;
-    p.g = 0;
-    p.islot = 0;
-    p.cslot = 0;
+    p.ring_beg = (uint32_t)(uintptr_t)smem + (uint32_t)c.wave * 2048u;
+    p.ring_end = p.ring_beg + QRING * kStageBytes;
+    p.islot = p.ring_beg;
     p.is = 0;
     p.inext = 0;
     p.itile = blockIdx.x;
@@ -357,7 +379,7 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
     p.isrc = p.blob;
     qpipe_boundary(p);
 #pragma unroll 1
-    for (int j = 0; j < QD; ++j) qpipe_issue(p, c.ring_lds, c.wave, c.lane);
+    for (int j = 0; j < QD; ++j) qpipe_issue(p, c.voff);
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * (QD - 1)) : "memory");
     u32x4 acur[8];
     qread_stage(smem, 0, c.lane, acur);
@@ -398,11 +420,11 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
         // 0..2, quarter 3 deferred like any layer's last quarter (slot 0, into hb[24..31]).
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            qstep_aux<T, true>(c, acur, bfrag, accA);
+            qstep_aux<T, true>(c, acur, bfrag, accA, (q & 1) == 0);
 #pragma unroll
             for (int i = 0; i < 4; ++i) qepi_chunk<T, QE_TMP>(c, accA[i], i, q, 0);
         }
-        qstep_aux<T, true>(c, acur, bfrag, accB);
+        qstep_aux<T, true>(c, acur, bfrag, accB, false);      // step 3
 #pragma unroll
         for (int i = 0; i < 24; ++i) hb[i] = c.tmp[i * 64 + c.lane];
 
@@ -410,8 +432,8 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
         QPend pend = {QE_TMP, 0, 0};     // layer 0 quarter 3 (in accB) -> slot 0
 #pragma unroll 1
         for (int qi = 0; qi < q_nquarters(S); qi += 2) {
-            run_quarter<T, S>(c, qi, acur, hb, bfrag, accA, accB, pend);
-            run_quarter<T, S>(c, qi + 1, acur, hb, bfrag, accB, accA, pend);
+            run_quarter<T, S, 0>(c, qi, acur, hb, bfrag, accA, accB, pend);
+            run_quarter<T, S, 1>(c, qi + 1, acur, hb, bfrag, accB, accA, pend);
         }
         // ---- last quarter (layer 7, q = 3, set B): dot product, combine halves, tanh, store
 #pragma unroll

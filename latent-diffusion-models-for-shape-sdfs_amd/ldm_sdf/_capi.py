@@ -14,6 +14,8 @@ from typing import Optional
 import torch  # noqa: F401  (must precede the CDLL load)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldm_sdf.so")
+# diagnostic builds only (scripts/ablate_decoder.sh): an alternative in-tree library file
+LIB_PATH = os.environ.get("LDM_SDF_LIB", LIB_PATH)
 HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                             "..", "..", "include", "ldm_sdf.h"))
 
