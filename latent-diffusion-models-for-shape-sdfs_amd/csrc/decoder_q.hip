@@ -21,9 +21,16 @@ namespace {
 using namespace dec;
 
 // Timing ablations for diagnostic builds only (scripts/ablate_decoder.sh; results are wrong):
-// 1 = no s_barrier/vmcnt wait, 2 = no DMA issue either, 4 = no epilogue, 8 = no A reads.
+// 1 = no s_barrier/vmcnt wait, 2 = no DMA issue either, 4 = no epilogue (MFMAs then dead-code
+// eliminated: invalid), 8 = no A reads, 16 = epilogue reduced to one live element per chunk.
 #ifndef QABL
 #define QABL 0
+#endif
+
+// Diagnostic build only: wave 0 stamps s_memtime around the quarters of its second tile into
+// LDS and dumps them over the output at the end (scripts/stamp_decoder.py; results are wrong).
+#ifndef QSTAMP
+#define QSTAMP 0
 #endif
 
 #define QRD(sl, i) ((QABL & 8) ? acur[i] : (sl)[(i) * 64 + c.lane])
@@ -37,7 +44,8 @@ static_assert(QVM >= 0, "RAW distance");
 constexpr int QLDS_RING = QRING * kStageBytes;        // 56 KiB
 constexpr int QLDS_TMP = 4 * 24 * 1024;               // 96 KiB (3 quarters x 8 frags x 1 KiB x 4 waves)
 constexpr int QLDS_WL = 16 * 2 * 16 * 4;              // 2 KiB
-constexpr int QLDS_TOTAL = QLDS_RING + QLDS_TMP + QLDS_WL;
+constexpr int QLDS_STAMP = QSTAMP ? 1024 : 0;
+constexpr int QLDS_TOTAL = QLDS_RING + QLDS_TMP + QLDS_WL + QLDS_STAMP;
 static_assert(QLDS_TOTAL <= 160 * 1024, "LDS");
 
 __host__ __device__ constexpr int q_nq3(int S) { return S / 128; }     // quarters of layer 3
@@ -84,41 +92,34 @@ __global__ void qaux_pack_kernel(const float* __restrict__ beta, const float* __
 // ------------------------------------------------------------------------------------------
 struct QPipe {
     const uint8_t* blob;
-    const uint8_t* aux;
     const uint8_t* isrc;        // source of the next stage to issue (wave-uniform)
+    const uint8_t* aux_sh;      // per-shape aux stages of the tile being issued (null: past the end)
+    const uint8_t* next_aux_sh; // ... of the following tile (set by the consumer at tile start)
     uint32_t islot, ring_beg, ring_end;   // LDS byte address of this wave's piece of that slot
-    int is, inext, itile, ishape;
-    int n_tiles, tps, tstride, nst, base4, len4;
+    int is, inext, k4;          // stage being issued, next switch point, layer-4 aux stages done
+    int nst, base4, len4;
 };
 
-// Slow path, at the 8 per-tile points where the source switches between the blob and the
-// shape's aux stages (and at the tile seam).  Past the last tile every stage comes from the
-// blob (dummy copies keep every wave's vmcnt arithmetic exact).
+// Slow path, at the 17 per-tile points where the source switches between the blob and the
+// shape's aux stages (stages 0..3 and the last stage of each layer-4 quarter) and at the tile
+// seam.  Compact on purpose: it is inlined into every step.  Past the last tile every stage
+// comes from the blob (dummy copies keep every wave's vmcnt arithmetic exact).
 __device__ __forceinline__ void qpipe_boundary(QPipe& p) {
     if (p.is == p.nst) {
         p.is = 0;
-        p.itile += p.tstride;
-        p.ishape = p.itile / p.tps;
+        p.k4 = 0;
+        p.aux_sh = p.next_aux_sh;
     }
     const int s = p.is;
-    int ai = -1;
-    if (s < 4) {
-        ai = s;
-    } else if (s >= p.base4 && s < p.base4 + 4 * p.len4) {
-        const int r = s - p.base4;
-        const int k = r / p.len4;
-        if (r - k * p.len4 == p.len4 - 1) ai = 4 + k;
-    }
-    if (ai >= 0 && p.itile < p.n_tiles) {
-        p.isrc = p.aux + ((size_t)p.ishape * 8 + ai) * kStageBytes;
+    const int apos = (p.k4 < 4) ? p.base4 + p.k4 * p.len4 + p.len4 - 1 : p.nst;
+    if (p.aux_sh != nullptr && (s < 4 || s == apos)) {
+        const int ai = (s < 4) ? s : 4 + p.k4;
+        p.k4 += (s < 4) ? 0 : 1;
+        p.isrc = p.aux_sh + ai * kStageBytes;
         p.inext = s + 1;
     } else {
-        p.isrc = p.blob + (size_t)s * kStageBytes;
-        if (p.itile >= p.n_tiles) p.inext = p.nst;
-        else if (s < 4) p.inext = 4;
-        else if (s < p.base4) p.inext = p.base4 + p.len4 - 1;
-        else if (s < p.base4 + 4 * p.len4) p.inext = p.base4 + p.len4 * ((s - p.base4) / p.len4 + 1) - 1;
-        else p.inext = p.nst;
+        p.isrc = p.blob + s * kStageBytes;
+        p.inext = (p.aux_sh != nullptr) ? apos : p.nst;
     }
 }
 
@@ -148,7 +149,26 @@ struct QCtx {
     u32x4* tmp;          // this wave's parked quarter outputs: [24 frags][64 lanes]
     const float* wl;     // permuted final weights [16 mc][2 h][16]
     float part;          // final-layer partial dot product
+    unsigned long long* st;   // QSTAMP: stamp area (LDS)
+    bool stamp_on;
 };
+
+#define QST(k)                                                                   \
+    do {                                                                         \
+        if (QSTAMP && c.stamp_on && c.lane == 0) c.st[(k)] = __builtin_readcyclecounter(); \
+    } while (0)
+// stamp after the MFMAs issued so far have retired (reads the last-written accumulator)
+#define QSTS(k, accv)                                                            \
+    do {                                                                         \
+        if (QSTAMP) {                                                            \
+            __builtin_amdgcn_sched_barrier(0);                                   \
+            const float _d = (accv)[3][0];                                       \
+            asm volatile("; stamp sync %0" ::"v"(_d));                           \
+            __builtin_amdgcn_sched_barrier(0);                                   \
+            QST(k);                                                              \
+            __builtin_amdgcn_sched_barrier(0);                                   \
+        }                                                                        \
+    } while (0)
 
 // Pending epilogue kinds.  Every converted quarter is parked in the wave's LDS area (slot
 // 0..2); the last quarter of a layer reuses slot 0, whose previous contents the next layer
@@ -160,6 +180,11 @@ enum QEpi { QE_NONE = 0, QE_TMP = 1, QE_FIN = 2 };
 template <typename T, int KIND>
 __device__ __forceinline__ void qepi_chunk(QCtx& c, const f32x16& a, int chunk, int slot,
                                            int fin_q) {
+    if (QABL & 16) {            // timing ablation: keep the MFMA chains live, no epilogue work
+        if (KIND == QE_FIN) c.part += a[0];
+        else reinterpret_cast<float*>(c.tmp)[(slot * 8 + 2 * chunk) * 256 + c.lane] = a[0];
+        return;
+    }
     if (KIND == QE_FIN) {
         const f32x4* w = reinterpret_cast<const f32x4*>(c.wl + ((fin_q * 4 + chunk) * 2 + c.h) * 16);
         float part = c.part;
@@ -212,9 +237,6 @@ __device__ __forceinline__ void qstep(QCtx& c, u32x4 (&acur)[8], const u32x4 b0,
     const u32x4 f2 = acur[2];
     accX[2] = Elem<T>::mfma(f2, b0, FIRST ? zero : accX[2]);
     acur[2] = QRD(sl, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!(QABL & 2)) qpipe_issue(c.p, c.voff);
-    __builtin_amdgcn_sched_barrier(0);
     const u32x4 f3 = acur[3];
     accX[3] = Elem<T>::mfma(f3, b0, FIRST ? zero : accX[3]);
     acur[3] = QRD(sl, 3);
@@ -224,6 +246,12 @@ __device__ __forceinline__ void qstep(QCtx& c, u32x4 (&acur)[8], const u32x4 b0,
         accX[i] = Elem<T>::mfma(f, b1, accX[i]);
         acur[4 + i] = QRD(sl, 4 + i);
     }
+    // LDS-DMA issue after the step's fragment reads: measured in the qstep skeleton
+    // (scripts/microbench/qstep_skeleton.hip) 333 vs 363 cycles/step against issuing it
+    // between MFMAs 2 and 3.  The barrier still precedes it, so the ring distances hold.
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(QABL & 2)) qpipe_issue(c.p, c.voff);
+    __builtin_amdgcn_sched_barrier(0);
     if (KIND != QE_NONE && !(QABL & 4)) qepi_chunk<T, KIND>(c, accY[ec], ec, slot, fin_q);
 }
 
@@ -243,13 +271,13 @@ __device__ __forceinline__ void qstep_aux(QCtx& c, u32x4 (&acur)[8], const u32x4
     const u32x4 f2 = acur[2];
     accX[2] = Elem<T>::mfma(f2, bfrag, FIRST ? zero : accX[2]);
     acur[2] = QRD(sl, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!(QABL & 2)) qpipe_issue(c.p, c.voff);
-    __builtin_amdgcn_sched_barrier(0);
     const u32x4 f3 = acur[3];
     accX[3] = Elem<T>::mfma(f3, bfrag, FIRST ? zero : accX[3]);
 #pragma unroll
     for (int i = 3; i < 8; ++i) acur[i] = QRD(sl, i);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(QABL & 2)) qpipe_issue(c.p, c.voff);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // k-loop remainder j = 4 .. KP-1 (no epilogue work).  KP == 8 only occurs for layer 4 with a
@@ -280,7 +308,7 @@ __device__ __forceinline__ void quarter_info(int qi, int& layer, int& q, int& nq
 
 // One quarter: accumulate into accX (static set), run the pending epilogue of accY inside the
 // first 4 steps, then return this quarter's pending epilogue.
-template <typename T, int S, int PAR>
+template <typename T, int S, int PAR, int KP>
 __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u32x4 (&hb)[32],
                                             const u32x4 bfrag, f32x16 (&accX)[4],
                                             f32x16 (&accY)[4], QPend& pend) {
@@ -293,7 +321,7 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
 #pragma unroll
         for (int i = 0; i < 24; ++i) hb[i] = c.tmp[i * 64 + c.lane];
     }
-    const int KP = (layer == 4) ? q_kp4(S) : 16;
+    QSTS(2 + 3 * qi, accY);
     const int kind = pend.kind, slot = pend.slot, fq = pend.fin_q;
     if (kind == QE_TMP) {
         qstep<T, true, QE_TMP>(c, acur, hb[0], hb[1], accX, accY, 0, slot, 0, ((0 + PAR) & 1) == 0);
@@ -306,6 +334,7 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
         qstep<T, false, QE_FIN>(c, acur, hb[4], hb[5], accX, accY, 2, 0, fq, ((2 + PAR) & 1) == 0);
         qstep<T, false, QE_FIN>(c, acur, hb[6], hb[7], accX, accY, 3, 0, fq, ((3 + PAR) & 1) == 0);
     }
+    QSTS(3 + 3 * qi, accX);
     // first quarter of a layer: the previous layer's last quarter was just parked in slot 0
     // by the 4 steps above; it always lands in hb[24..31] (k-steps 24..31; a K=256 layer 4
     // reads its k-steps 8..15 from there, see qkloop_rest<8>), first read at pair j >= 4.
@@ -318,8 +347,8 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
             hb[24 + i] = rl ? v : hb[24 + i];
         }
     }
-    if (KP == 16) qkloop_rest<T, 16, PAR>(c, acur, hb, accX, accY);
-    else qkloop_rest<T, 8, PAR>(c, acur, hb, accX, accY);
+    qkloop_rest<T, KP, PAR>(c, acur, hb, accX, accY);
+    QSTS(4 + 3 * qi, accX);
     qstep_aux<T, false>(c, acur, bfrag, accX, PAR == 0);     // step KP (even)
     // this quarter's epilogue, deferred to the next quarter's first 4 steps
     if (layer == 7) {
@@ -356,27 +385,24 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
     c.tmp = reinterpret_cast<u32x4*>(smem + QLDS_RING + c.wave * 24576);
     float* wl = reinterpret_cast<float*>(smem + QLDS_RING + QLDS_TMP);
     c.wl = wl;
+    c.st = reinterpret_cast<unsigned long long*>(smem + QLDS_RING + QLDS_TMP + QLDS_WL);
+    c.stamp_on = false;
     for (int i = threadIdx.x; i < 512; i += 256) wl[i] = a.w_last[i];
     __syncthreads();
     if ((int)blockIdx.x >= a.n_tiles) return;
 
     QPipe& p = c.p;
     p.blob = a.blob;
-    p.aux = a.aux;
     p.ring_beg = (uint32_t)(uintptr_t)smem + (uint32_t)c.wave * 2048u;
     p.ring_end = p.ring_beg + QRING * kStageBytes;
     p.islot = p.ring_beg;
-    p.is = 0;
-    p.inext = 0;
-    p.itile = blockIdx.x;
-    p.ishape = p.itile / a.tiles_per_shape;
-    p.n_tiles = a.n_tiles;
-    p.tps = a.tiles_per_shape;
-    p.tstride = gridDim.x;
     p.nst = q_nstages(S);
     p.base4 = q_base4(S);
     p.len4 = q_len4(S);
-    p.isrc = p.blob;
+    p.aux_sh = a.aux + (size_t)(blockIdx.x / a.tiles_per_shape) * 8 * kStageBytes;
+    p.next_aux_sh = nullptr;
+    p.is = 0;
+    p.k4 = 0;
     qpipe_boundary(p);
 #pragma unroll 1
     for (int j = 0; j < QD; ++j) qpipe_issue(p, c.voff);
@@ -388,6 +414,11 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
     for (int tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         const int shape = tile / a.tiles_per_shape;
         const int local = tile - shape * a.tiles_per_shape;
+        {   // the DMA stream crosses into the next tile QD stages before this tile ends
+            const int nt = tile + (int)gridDim.x;
+            p.next_aux_sh = (nt < a.n_tiles)
+                ? a.aux + (size_t)(nt / a.tiles_per_shape) * 8 * kStageBytes : nullptr;
+        }
         int pt = local * kTilePoints + c.wave * 32 + (c.lane & 31);
         const bool valid = pt < a.npts;
         if (!valid) pt = a.npts - 1;
@@ -415,6 +446,8 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
         u32x4 hb[32];
         f32x16 accA[4], accB[4];
         c.part = 0.f;
+        c.stamp_on = QSTAMP && c.wave == 0 && tile == (int)blockIdx.x + (int)gridDim.x;
+        QST(0);
 
         // ---- layer 0: four aux-only quarters; 0..2 converted at once into parking slots
         // 0..2, quarter 3 deferred like any layer's last quarter (slot 0, into hb[24..31]).
@@ -429,11 +462,30 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
         for (int i = 0; i < 24; ++i) hb[i] = c.tmp[i * 64 + c.lane];
 
         // ---- layers 1..7: quarters alternate A / B; epilogues deferred by one quarter
+        QSTS(1, accB);
         QPend pend = {QE_TMP, 0, 0};     // layer 0 quarter 3 (in accB) -> slot 0
+        // Pairs of quarters.  K is a compile-time property of each run_quarter instance (a
+        // runtime K made the compiler re-home all 64 accumulator AGPRs at the k-loop join).
+        // Pairs of quarters.  K is a compile-time property of each run_quarter instance (a
+        // runtime K made the compiler re-home all 64 accumulator AGPRs at the k-loop join),
+        // and each pair body exists once in the code (the kernel must stay well inside the
+        // instruction cache: a 75 KB variant with three pair loops ran 30 % slower).
+        constexpr int L4B = 8 + q_nq3(S);              // first layer-4 quarter
+        int qi = 0;
 #pragma unroll 1
-        for (int qi = 0; qi < q_nquarters(S); qi += 2) {
-            run_quarter<T, S, 0>(c, qi, acur, hb, bfrag, accA, accB, pend);
-            run_quarter<T, S, 1>(c, qi + 1, acur, hb, bfrag, accB, accA, pend);
+        for (int phase = 0; phase < 2; ++phase) {
+            const int qend = (phase == 0 && q_kp4(S) != 16) ? L4B : q_nquarters(S);
+#pragma unroll 1
+            for (; qi < qend; qi += 2) {               // layers 1..3, then 5..7 (all K = 512)
+                run_quarter<T, S, 0, 16>(c, qi, acur, hb, bfrag, accA, accB, pend);
+                run_quarter<T, S, 1, 16>(c, qi + 1, acur, hb, bfrag, accB, accA, pend);
+            }
+            if (q_kp4(S) == 16) break;
+#pragma unroll 1
+            for (; phase == 0 && qi < L4B + 4; qi += 2) {   // layer 4 (K = 256)
+                run_quarter<T, S, 0, q_kp4(S)>(c, qi, acur, hb, bfrag, accA, accB, pend);
+                run_quarter<T, S, 1, q_kp4(S)>(c, qi + 1, acur, hb, bfrag, accB, accA, pend);
+            }
         }
         // ---- last quarter (layer 7, q = 3, set B): dot product, combine halves, tanh, store
 #pragma unroll
@@ -441,8 +493,14 @@ __global__ __launch_bounds__(256, 1) void dec_q_kernel(QArgs a) {
         const float tot = c.part + __shfl_xor(c.part, 32);
         const float sdf = tanhf(tot + a.b_last);
         if (c.h == 0 && valid) a.out[(size_t)shape * a.npts + pt] = sdf;
+        QST(2 + 3 * q_nquarters(S));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (QSTAMP && c.wave == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        for (int k = c.lane; k < 96; k += 64)
+            reinterpret_cast<unsigned long long*>(a.out)[(size_t)blockIdx.x * 96 + k] = c.st[k];
+    }
 }
 
 template <typename T, int S>
