@@ -197,7 +197,7 @@ def main():
                        "parallelism": f"zslab{world}"},
             "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
                          "frac": ach / peak, "traffic": prof_traffic,
-                         "kernel": "dec_mfma_kernel (+aux_pack, <0.1%)",
+                         "kernel": "dec_q_kernel (+qaux_pack, <0.1%)",
                          "flops_per_query": FLOPS_PER_QUERY,
                          "queries_per_launch": B * npts_local, "avg_launch_ms": kms},
         }
