@@ -189,6 +189,41 @@ int ldm_colsum(const float* G, int Bn, int M, float* out, int accumulate, ldm_st
 int ldm_gather_rows(const float* table, const int32_t* idx, int Bn, int C, float* out,
                     ldm_stream_t s);
 
+/* ---- C17 1D-UNet denoiser: fused conv1d (implicit GEMM) ------------------ */
+/* Y[b][co][l] = epi( sum_s sum_{ci<C_s} sum_{k<ksize_s} W_s(co,ci,k) * act_s(Xsrc_s(b,ci,l,k))
+ *                    + bias[co] + bias2[co] + cbias[b*scb + co]  (+ R[b][co][l]) )
+ * act_s = SiLU if silu_in else identity (applied to the input before the taps).
+ * Xsrc for LDM_CONV_DIRECT: X[b][ci][l*stride + k - pad];  LDM_CONV_UP2 (nearest 2x upsample,
+ * then the conv, stride 1): p = l + k - pad, X[b][ci][p >> 1] for 0 <= p < 2 L_in.
+ * Out-of-range positions read 0 (zero padding).  W_s(co,ci,k) = W_s[co*ldw + ci*ksize + k]
+ * (a column block of a [Cout][.][ksize] weight, so a channel concat [u || s] is two segments
+ * of one weight).  Segments share B, Cout and L_out; up to LDM_CONV_MAX_SEGS of them.
+ * Epilogues: LDM_CONV_EPI_STORE  Y = pre
+ *            LDM_CONV_EPI_DDPM   Y = c1[t] (xlat - c2[t] pre) + sigma[t] z   (A8 with
+ *                                eps = pre; z ignored at t = 0; the UNet's output conv)   */
+#define LDM_CONV_DIRECT 0
+#define LDM_CONV_UP2 1
+#define LDM_CONV_MAX_SEGS 4
+#define LDM_CONV_EPI_STORE 0
+#define LDM_CONV_EPI_DDPM 1
+typedef struct ldm_conv1d_seg {
+    const float* X;  /* fp32 [B][C][L_in] */
+    const void* W;   /* w_dtype, see above */
+    int32_t C, L_in, ksize, stride, pad, mode, silu_in, ldw;
+} ldm_conv1d_seg_t;
+typedef struct ldm_conv1d_args {
+    int32_t B, Cout, L_out, n_seg, w_dtype, epi;
+    ldm_conv1d_seg_t seg[LDM_CONV_MAX_SEGS];
+    const float* bias;                /* [Cout] or NULL */
+    const float* bias2;               /* [Cout] or NULL (shortcut bias) */
+    const float* cbias; int64_t scb;  /* per-(b, co) bias or NULL; scb = 0: batch-uniform */
+    const float* R;                   /* residual [B][Cout][L_out] or NULL */
+    float* Y;                         /* [B][Cout][L_out] */
+    const float* xlat; const float* z;           /* LDM_CONV_EPI_DDPM: x_t and noise [B][L] */
+    const float* c1; const float* c2; const float* sigma; int32_t t;   /* A4 device tables */
+} ldm_conv1d_args_t;
+int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,26 @@ class LinearArgs(C.Structure):
                 ("A_out", _vp), ("sab", C.c_int64)]
 
 
+CONV_DIRECT, CONV_UP2 = 0, 1
+CONV_MAX_SEGS = 4
+CONV_EPI_STORE, CONV_EPI_DDPM = 0, 1
+
+
+class ConvSeg(C.Structure):
+    _fields_ = [("X", _vp), ("W", _vp), ("C", C.c_int32), ("L_in", C.c_int32),
+                ("ksize", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
+                ("mode", C.c_int32), ("silu_in", C.c_int32), ("ldw", C.c_int32)]
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("B", C.c_int32), ("Cout", C.c_int32), ("L_out", C.c_int32),
+                ("n_seg", C.c_int32), ("w_dtype", C.c_int32), ("epi", C.c_int32),
+                ("seg", ConvSeg * CONV_MAX_SEGS),
+                ("bias", _vp), ("bias2", _vp), ("cbias", _vp), ("scb", C.c_int64),
+                ("R", _vp), ("Y", _vp), ("xlat", _vp), ("z", _vp),
+                ("c1", _vp), ("c2", _vp), ("sigma", _vp), ("t", C.c_int32)]
+
+
 # (name, restype, argtypes) -- every symbol include/ldm_sdf.h declares.
 _i, _sz, _f = C.c_int, C.c_size_t, C.c_float
 SIGNATURES = [
@@ -89,6 +109,7 @@ SIGNATURES = [
     ("ldm_silu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),
     ("ldm_colsum", _i, [_fp, _i, _i, _fp, _i, _vp]),
     ("ldm_gather_rows", _i, [_fp, _vp, _i, _i, _fp, _vp]),
+    ("ldm_conv1d", _i, [C.POINTER(ConvArgs), _vp]),
 ]
 
 _lib: Optional[C.CDLL] = None

@@ -75,10 +75,11 @@ def decode_points(decoder: SDFDecoder, latents: torch.Tensor, xyz: torch.Tensor,
 class Sampler:
     """A10: the T-step reverse loop for a fixed (n, steps, dtype), captured once as a HIP
     graph (``torch.cuda.CUDAGraph`` = hipGraph on ROCm) and replayed.  Each step is the
-    fused ``ldm_sample_step`` (in-projection, n_blocks residual blocks, out-projection with
-    the DDPM update in its epilogue)."""
+    denoiser's fused reverse step (``make_stepper``): for the MLP, ``ldm_sample_step``
+    (in-projection, n_blocks residual blocks, out-projection with the DDPM update in its
+    epilogue); for the 1D-UNet, 18 ``ldm_conv1d`` launches ending in the same update."""
 
-    def __init__(self, denoiser: MLPDenoiser, schedule: DDPMSchedule, n: int, *,
+    def __init__(self, denoiser, schedule: DDPMSchedule, n: int, *,
                  steps: Optional[int] = None, dtype: str = "bf16", device=None,
                  use_graph: bool = True):
         self.device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
@@ -87,20 +88,18 @@ class Sampler:
         self.steps = self.T if steps is None else int(steps)
         if not (1 <= self.steps <= self.T):
             raise ValueError("steps must be in [1, T]")
-        self.dev = denoiser.device_pack(dtype, self.device)
         self.sd = schedule.device(self.device)
-        D, H = denoiser.D, denoiser.H
+        D = denoiser.D
         self.x = [torch.empty(n, D, device=self.device) for _ in range(2)]
         self.noise = torch.empty(self.T, n, D, device=self.device)
-        self.ws = torch.empty(2 * n * H, device=self.device)
+        self.step = denoiser.make_stepper(n, dtype, self.device, self.sd["desc"])
         self.graph = None
         self.use_graph = use_graph
 
     def _loop(self) -> None:
         cur = 0
         for t in range(self.T - 1, self.T - 1 - self.steps, -1):
-            ops.sample_step(self.dev["desc"], self.sd["desc"], self.x[cur], self.noise[t], t,
-                            self.x[cur ^ 1], self.ws)
+            self.step(self.x[cur], self.noise[t], t, self.x[cur ^ 1])
             cur ^= 1
 
     @property
@@ -128,7 +127,7 @@ class Sampler:
         return self.result
 
 
-def sample(denoiser: MLPDenoiser, schedule: DDPMSchedule, n: int, *,
+def sample(denoiser, schedule: DDPMSchedule, n: int, *,
            steps: Optional[int] = None, dtype: str = "bf16", x_T: Optional[torch.Tensor] = None,
            noise: Optional[torch.Tensor] = None, generator: Optional[torch.Generator] = None,
            device=None, use_graph: bool = True, group=None) -> torch.Tensor:

@@ -238,6 +238,16 @@ class MLPDenoiser:
         """Call after the fp32 masters changed (training): drops packed copies / E tables."""
         self._dev.clear()
 
+    def make_stepper(self, n: int, dtype: str, device, sched_desc):
+        """Callable ``step(x, z, t, x_out)``: one fused reverse step (``ldm_sample_step``)."""
+        from . import ops
+        desc = self.device_pack(dtype, device)["desc"]
+        ws = torch.empty(2 * n * self.H, device=device)
+
+        def step(x, z, t, x_out):
+            ops.sample_step(desc, sched_desc, x, z, t, x_out, ws)
+        return step
+
     def device_pack(self, dtype: str, device, with_tables: bool = True) -> Dict[str, object]:
         """Weights in ``dtype`` on ``device`` + the per-block E tables (A5):
         ``E_k[t] = U_k temb(t) + b_k`` for all t, computed with the device GEMM kernel."""

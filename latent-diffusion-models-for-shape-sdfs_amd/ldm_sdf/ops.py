@@ -239,6 +239,78 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# ---------------------------------------------------------------------------------------- C17
+class ConvSegment:
+    """One operand segment of ``ldm_conv1d``: input ``X [B, C, L_in]`` (fp32, contiguous),
+    weight ``W [Cout, Cw, ksize]`` (fp32/bf16, contiguous; the segment uses the column block
+    ``[c_off, c_off + C)``), tap geometry and the SiLU-on-input flag."""
+
+    __slots__ = ("X", "W", "c_off", "ksize", "stride", "pad", "mode", "silu")
+
+    def __init__(self, X, W, *, c_off=0, stride=1, pad=None, mode=capi.CONV_DIRECT, silu=False):
+        self.X, self.W, self.c_off = X, W, c_off
+        self.ksize = W.shape[2]
+        self.stride, self.mode, self.silu = stride, mode, silu
+        self.pad = (self.ksize - 1) // 2 if pad is None else pad
+
+
+def conv1d_args(segs, Y: torch.Tensor, *, bias=None, bias2=None, cbias=None, scb: int = 0,
+                R=None, epi: int = capi.CONV_EPI_STORE, xlat=None, z=None, sched=None,
+                t: int = 0) -> capi.ConvArgs:
+    """Validated ``ldm_conv1d_args_t`` (kept alive by the caller for graph capture)."""
+    B, Cout, L_out = Y.shape
+    if not 1 <= len(segs) <= capi.CONV_MAX_SEGS:
+        raise capi.LdmError("conv1d: 1..4 segments")
+    _f32(Y, bias, bias2, cbias, R, xlat, z)
+    _contig(Y, bias, bias2, cbias, R, xlat, z)
+    a = capi.ConvArgs()
+    a.B, a.Cout, a.L_out, a.n_seg, a.epi = B, Cout, L_out, len(segs), epi
+    wdt = segs[0].W.dtype
+    a.w_dtype = {torch.float32: capi.LDM_F32, torch.bfloat16: capi.LDM_BF16}.get(wdt, -1)
+    if a.w_dtype < 0:
+        raise capi.LdmError(f"conv1d: weight dtype {wdt}")
+    for i, s in enumerate(segs):
+        X, W = s.X, s.W
+        _f32(X)
+        _contig(X, W)
+        if W.dtype != wdt or W.shape[0] != Cout or X.shape[0] != B:
+            raise capi.LdmError(f"conv1d seg {i}: weight/batch mismatch")
+        Cs = X.shape[1]
+        if s.c_off + Cs > W.shape[1]:
+            raise capi.LdmError(f"conv1d seg {i}: channels {s.c_off}+{Cs} > {W.shape[1]}")
+        Lsrc = 2 * X.shape[2] if s.mode == capi.CONV_UP2 else X.shape[2]
+        if (Lsrc + 2 * s.pad - s.ksize) // s.stride + 1 != L_out:
+            raise capi.LdmError(f"conv1d seg {i}: L_in {X.shape[2]} does not give L_out {L_out}")
+        g = a.seg[i]
+        g.X = X.data_ptr()
+        g.W = W.data_ptr() + s.c_off * s.ksize * W.element_size()
+        g.C, g.L_in, g.ksize, g.stride, g.pad = Cs, X.shape[2], s.ksize, s.stride, s.pad
+        g.mode, g.silu_in, g.ldw = s.mode, int(bool(s.silu)), W.shape[1] * s.ksize
+    for name, v in (("bias", bias), ("bias2", bias2), ("R", R), ("xlat", xlat), ("z", z)):
+        setattr(a, name, capi.ptr(v))
+    if R is not None and R.shape != Y.shape:
+        raise capi.LdmError("conv1d: R must match Y")
+    if cbias is not None:
+        a.cbias, a.scb = cbias.data_ptr(), int(scb)
+    a.Y = Y.data_ptr()
+    if epi == capi.CONV_EPI_DDPM:
+        if sched is None or xlat is None or xlat.shape != (B, Cout * L_out):
+            raise capi.LdmError("conv1d DDPM epilogue: needs sched and xlat [B, L]")
+        a.c1, a.c2, a.sigma, a.t = sched.c1, sched.c2, sched.sigma, int(t)
+    return a
+
+
+def conv1d_launch(a: capi.ConvArgs, device) -> None:
+    capi.check(capi.load().ldm_conv1d(C.byref(a), capi.stream_handle(device)), "ldm_conv1d")
+
+
+def conv1d(segs, Y: torch.Tensor, **kw) -> torch.Tensor:
+    """``Y = epi(sum_seg conv(act(X_seg); W_seg) + biases (+ R))`` -- see include/ldm_sdf.h."""
+    capi.require_device(Y, *[s.X for s in segs])
+    conv1d_launch(conv1d_args(segs, Y, **kw), Y.device)
+    return Y
+
+
 # ---------------------------------------------------------------------------------------- A5
 def temb_forward(dev: Dict[str, object], e: torch.Tensor, H: int,
                  save: Optional[dict] = None) -> torch.Tensor:

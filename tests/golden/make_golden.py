@@ -20,9 +20,11 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from oracle import ref_cpu as R  # noqa: E402
+from oracle import ref_unet as U  # noqa: E402
 
 DEC_SEED, LAT_SEED, PTS_SEED = 1234, 0, 7
 DEN_SEED, SAMPLE_SEED = 4321, 11
+UNET_SEED = 2468
 
 
 def decoder_case():
@@ -81,12 +83,37 @@ def train_case(B=64):
     return out
 
 
+def unet_case(steps=10, B=2):
+    """C17: 1D-UNet (D=1024, C=(32,64,128)) eps at mixed t and a 10-step trajectory (fp64)."""
+    up = U.make_unet_params(seed=UNET_SEED)
+    tab = R.ddpm_tables(1000)
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    g = torch.Generator().manual_seed(SAMPLE_SEED + 2)
+    x_T = torch.randn(B, 1024, generator=g, dtype=torch.float32)
+    noise = torch.zeros(1000, B, 1024, dtype=torch.float32)
+    noise[1000 - steps:] = torch.randn(steps, B, 1024, generator=g, dtype=torch.float32)
+    t_mixed = torch.tensor([999, 5][:B])
+    eps_mixed = U.unet_forward(up, x_T.double(), t_mixed, emb)
+    x = x_T.double()
+    traj = [x]
+    for t in range(999, 999 - steps, -1):
+        eps = U.unet_forward(up, x, torch.full((B,), t), emb)
+        x = R.ddpm_step(tab, x, eps, noise[t].double(), t)
+        traj.append(x)
+    return dict(x_T=x_T.numpy(), noise_tail=noise[1000 - steps:].numpy(),
+                traj=torch.stack(traj).numpy(), t_mixed=t_mixed.numpy().astype(np.int32),
+                eps_mixed=eps_mixed.numpy(), steps=np.int32(steps))
+
+
 CASES = {"decoder_small": decoder_case, "decoder_widen": widen_case,
-         "sampling_20": sampling_case, "train_step": train_case}
+         "sampling_20": sampling_case, "train_step": train_case, "unet_10": unet_case}
 
 
 def main():
+    only = sys.argv[1:]
     for name, fn in CASES.items():
+        if only and name not in only:
+            continue
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **fn())
         print(f"wrote {path} ({os.path.getsize(path)} bytes)")
