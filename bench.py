@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--ddpm-batch", type=int, default=8)
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--train-steps", type=int, default=20)
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip config 5 (1D-UNet sampling on 1024-d latents -> fp16 decode "
+                         "of a 512^3 grid with the widen-skip decoder)")
+    ap.add_argument("--c5-batch", type=int, default=1)
     ap.add_argument("--config3", action="store_true",
                     help="also time sample(8) -> decode 128^3 end to end (adds a decoder "
                          "launch of another size to the profile)")
@@ -104,6 +108,91 @@ def cpu_baseline_sampling(budget_s: float, B: int):
     dt = time.perf_counter() - t0
     return {"value": steps / dt, "unit": "steps/s", "cores": torch.get_num_threads(),
             "kind": "port", "sample": f"{steps} reverse steps, B={B}, fp32 torch-CPU oracle"}
+
+
+FLOPS_PER_QUERY_WIDEN = 2 * (3 * 512 + 2 * 512 * 512 + 512 * 512 + 515 * 512 + 3 * 512 * 512
+                             + 512)
+
+
+def config5(args, rank, world, dev, group, gen):
+    """Config 5: 1000-step DDPM sampling of ``--c5-batch`` 1024-d latents with the 1D-UNet
+    (bf16 weights, hipGraph) -> fp16 MFMA decode (widen-skip decoder, L=1024) of a 512^3
+    grid, z-slab sharded over the ranks + all-gather.  Decode time = max over ranks."""
+    import ldm_sdf
+    from ldm_sdf import ops
+    from ldm_sdf.dist import slab_bounds
+    nb, N = args.c5_batch, 512
+    unet = ldm_sdf.UNet1DDenoiser(D=1024, seed=2468)
+    sch = ldm_sdf.DDPMSchedule()
+    lo, hi = ldm_sdf.dist.batch_shard(nb, rank, world)
+    nl = max(1, hi - lo)
+    sampler = ldm_sdf.Sampler(unet, sch, nl, dtype="bf16", device=dev)
+    xT = torch.randn(nl, 1024, device=dev, generator=gen)
+    noise = torch.randn(1000, nl, 1024, device=dev, generator=gen)
+    sampler.run(xT, noise)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        lat = sampler.run(xT, noise)
+    torch.cuda.synchronize()
+    sps = 1000 * reps / (time.perf_counter() - t0)
+    latents = ldm_sdf.dist.all_gather_rows(lat[:hi - lo].clone(), nb, group=group) \
+        if world > 1 else lat[:nb].clone()
+    dec = ldm_sdf.SDFDecoder(1024, seed=1235)            # widen-skip (L + 3 >= H)
+    pack = dec.device_pack("fp16", dev)
+    desc = pack["desc"]
+    k0, k1, _ = slab_bounds(rank, world, N)
+    out = torch.empty(nb, N, N, N, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = []
+
+    def step(timed):
+        beta = ops.decoder_fold(desc, latents.float().contiguous())
+
+        def slab(a, b, dst):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            ops.decoder_grid_fwd(desc, beta, N, a, b, out=dst)
+            e1.record(stream)
+            if timed:
+                ev.append((e0, e1))
+        if world == 1:
+            slab(0, N, out)
+        else:
+            ldm_sdf.dist.decode_sharded(slab, nb, N, dev, group=group, out=out)
+
+    step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    if world > 1:
+        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt)
+    kms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    ach = FLOPS_PER_QUERY_WIDEN * nb * (k1 - k0) * N * N / (kms * 1e-3) / 1e12
+    H = unet.HT
+    wbytes = 2 * sum(v.numel() for k, v in unet.params.items()
+                     if not (k.startswith("b") or k.endswith((".b", ".b1", ".b2", ".bs"))
+                             or k.startswith("Wt") or k.endswith(".p")))
+    return {"workload": f"config5: {nb} x 1000-step 1D-UNet sampling (D=1024, C=(32,64,128), "
+                        f"bf16) -> fp16 decode of a {N}^3 grid (widen-skip, L=1024), "
+                        f"z-slab over {world} rank(s)",
+            "decode_queries_per_s": nb * N ** 3 / el, "decode_s": el,
+            "decode_roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_TFLOPS["fp16"],
+                                "unit": "TFLOP/s", "frac": ach / PEAK_TFLOPS["fp16"],
+                                "flops_per_query": FLOPS_PER_QUERY_WIDEN,
+                                "avg_launch_ms": kms},
+            "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
+            "unet_graph": "hipGraph of 1000 steps x 18 ldm_conv1d launches",
+            "unet_conv_weight_bytes_per_step": wbytes}
 
 
 def main():
@@ -232,6 +321,10 @@ def main():
                                     "frac": sps * wbytes / 8e12,
                                     "bytes_per_step": wbytes},
                        "config3_sample_plus_decode128_s": e2e}
+    if not args.no_config5:
+        res_c5 = config5(args, rank, world, dev, group, gen)
+        if rank == 0:
+            res["config5"] = res_c5
     if rank == 0 and not args.no_train:
         # config 2: DDPM training on 1k synthetic 256-d latents, MLP denoiser, bf16, batch 1000
         den_t = ldm_sdf.MLPDenoiser(seed=4321)

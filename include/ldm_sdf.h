@@ -195,9 +195,13 @@ int ldm_gather_rows(const float* table, const int32_t* idx, int Bn, int C, float
  * act_s = SiLU if silu_in else identity (applied to the input before the taps).
  * Xsrc for LDM_CONV_DIRECT: X[b][ci][l*stride + k - pad];  LDM_CONV_UP2 (nearest 2x upsample,
  * then the conv, stride 1): p = l + k - pad, X[b][ci][p >> 1] for 0 <= p < 2 L_in.
- * Out-of-range positions read 0 (zero padding).  W_s(co,ci,k) = W_s[co*ldw + ci*ksize + k]
- * (a column block of a [Cout][.][ksize] weight, so a channel concat [u || s] is two segments
- * of one weight).  Segments share B, Cout and L_out; up to LDM_CONV_MAX_SEGS of them.
+ * Out-of-range positions read 0 (zero padding).  Weights are packed for the matrix cores
+ * (ldm_sdf/ops.py pack_conv_weight): a torch [Cout][Cw][K] weight becomes
+ * Wp[Cout16][K][Cw16] (Cout16, Cw16 = sizes rounded up to 16, zero-filled) with the input
+ * channel stored at perm16(ci) = (ci & ~15) | ((ci & 3) << 2) | ((ci >> 2) & 3), so
+ * W_s(co,ci,k) = W_s[co*ldw + k*kstride + perm16(ci)] with ldw = K*Cw16, kstride = Cw16.
+ * A channel concat [u || s] is two segments whose W_s point at channel offsets (multiples
+ * of 16) of one packed weight.
  * Epilogues: LDM_CONV_EPI_STORE  Y = pre
  *            LDM_CONV_EPI_DDPM   Y = c1[t] (xlat - c2[t] pre) + sigma[t] z   (A8 with
  *                                eps = pre; z ignored at t = 0; the UNet's output conv)   */
@@ -208,8 +212,8 @@ int ldm_gather_rows(const float* table, const int32_t* idx, int Bn, int C, float
 #define LDM_CONV_EPI_DDPM 1
 typedef struct ldm_conv1d_seg {
     const float* X;  /* fp32 [B][C][L_in] */
-    const void* W;   /* w_dtype, see above */
-    int32_t C, L_in, ksize, stride, pad, mode, silu_in, ldw;
+    const void* W;   /* w_dtype, packed (see above) */
+    int32_t C, L_in, ksize, stride, pad, mode, silu_in, ldw, kstride;
 } ldm_conv1d_seg_t;
 typedef struct ldm_conv1d_args {
     int32_t B, Cout, L_out, n_seg, w_dtype, epi;

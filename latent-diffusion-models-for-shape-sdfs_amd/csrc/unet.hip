@@ -1,7 +1,7 @@
 // C17: the 1D-UNet denoiser's fused conv1d on MI355X (gfx950), DESIGN.md §9.
 //
-// One kernel, ldm_conv1d, runs every conv of the UNet as an implicit GEMM
-//   Y[b][co][l] = sum_seg sum_{ci,k} W(co,ci,k) act(X[b][ci][src(l,k)]) + biases (+ R)
+// One kernel, ldm_conv1d, runs every conv of the UNet as an implicit GEMM on the matrix cores
+//   Y[b][co][l] = sum_seg sum_{k,ci} W(co,ci,k) act(X[b][ci][src(l,k)]) + biases (+ R)
 // with the block structure fused into its operands and epilogue:
 //   * SiLU of the input is applied while staging the input window (no separate pass);
 //   * a channel concat [u || s] is two segments of one weight (no concat copy);
@@ -12,126 +12,238 @@
 //   * nearest-2x upsampling is an index map of the staging loads (LDM_CONV_UP2);
 //   * the output conv carries the DDPM reverse step (A8) in its epilogue.
 //
-// Tiling: a workgroup (256 threads = 4 waves) owns 32 output channels x 64 positions of one
-// shape.  The input window (16 channels x (63*stride + ksize) positions) and the weight slice
-// (16 channels x ksize taps x 32 outputs) are staged in LDS per 16-channel chunk; each thread
-// accumulates 2 channels x 4 consecutive positions in fp32 (VALU FMA: the UNet is a small,
-// latency-bound GEMV-like op at the sampling batch, MFMA is reserved for the decoder as the
-// north star asks).  Stores are 4 consecutive positions per thread.
+// Arithmetic: v_mfma_f32_16x16x4_f32 -- fp32 activations and fp32 (or bf16-stored) weights,
+// fp32 products and accumulation, so the bf16 path differs from fp32 only by its weights.
+// The UNet at the sampling batch is a chain of small, latency-bound launches, so the design
+// minimises per-launch latency rather than maximising MFMA occupancy:
+//   * a workgroup (4 waves) owns 16 output channels x TP positions of one shape (TP = 16 for
+//     small grids, 32/64 for large ones); the 4 waves split the contraction (tap x channel
+//     chunks of 16) and their partial tiles are summed in a fixed order through LDS, so the
+//     result is deterministic;
+//   * every input window and weight slice of the launch is staged in LDS in ONE round trip
+//     (loads of a segment issued back to back before their LDS stores), then one barrier,
+//     then the MFMA loop runs from LDS only;
+//   * LDS layouts put each lane's operands for 4 consecutive MFMAs in one ds_read_b128:
+//     channels are permuted inside every group of 16 (perm16) on staging, and the weights
+//     arrive already permuted from the host packing (ldm_sdf/ops.py pack_conv_weight).
 #include "ldm_internal.h"
 #include "ddpm_common.h"
 
 namespace ldm {
 namespace {
 
-constexpr int kCoT = 32;          // output channels per workgroup
-constexpr int kLT = 64;           // output positions per workgroup
-constexpr int kCiT = 16;          // input channels per LDS chunk
-constexpr int kMaxWin = 63 * 2 + 4;
-constexpr int kXsLd = kMaxWin + 2;   // 132
-constexpr int kWsLd = kCoT + 1;      // 33
-constexpr int kMaxKs = 4;
-
-template <typename TW>
-__device__ __forceinline__ float ldw(const void* W, int64_t i) {
-    if (sizeof(TW) == 2) return bf16_to_f32(reinterpret_cast<const unsigned short*>(W)[i]);
-    return reinterpret_cast<const float*>(W)[i];
+__host__ __device__ constexpr int round16(int c) { return (c + 15) & ~15; }
+// Position of channel ci inside its 16-group so that lane group g reads channels
+// 16c + 4m + g (m = 0..3: four consecutive MFMAs) as one 16-byte vector.
+__host__ __device__ constexpr int perm16(int ci) {
+    return (ci & ~15) | ((ci & 3) << 2) | ((ci >> 2) & 3);
 }
 
-template <typename TW, int KS, int ST>
-__device__ __forceinline__ void conv_segment(float (&acc)[2][4], float* __restrict__ xs,
-                                             float* __restrict__ ws, const ldm_conv1d_seg_t& s,
-                                             int b, int co0, int l0, int Cout) {
-    constexpr int WIN = (kLT - 1) * ST + KS;
+struct SegPlan {
+    int cinp;   // channels rounded up to 16
+    int win;    // input window (positions) of one tile
+    int xoff;   // LDS float offset of the window  [win][cinp + 4]
+    int woff;   // LDS float offset of the weights [16][ksize * cinp + 4]
+    int ch0;    // first contraction chunk (16 channels x one tap) of this segment
+};
+struct ConvPlan {
+    SegPlan s[LDM_CONV_MAX_SEGS];
+    int nchunks;
+};
+
+template <int TP>
+__device__ __forceinline__ void stage_x(float* __restrict__ xs, const ldm_conv1d_seg_t& s,
+                                        const SegPlan& p, int b, int pos0) {
+    constexpr int CW = TP <= 16 ? 32 : 64;            // window columns per pass row
+    constexpr int RPP = 256 / CW;                     // channel rows per pass
+    constexpr int NB = 32;
     const int tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;
+    const int col = tid % CW, row = tid / CW;
     const bool up2 = s.mode == LDM_CONV_UP2;
     const int Lsrc = up2 ? 2 * s.L_in : s.L_in;
-    const int p0 = l0 * ST - s.pad;
-    for (int ci0 = 0; ci0 < s.C; ci0 += kCiT) {
-        for (int i = tid; i < kCiT * WIN; i += 256) {
-            const int ci = i / WIN, j = i - ci * WIN;
-            const int c = ci0 + ci, p = p0 + j;
-            float v = 0.f;
-            if (c < s.C && p >= 0 && p < Lsrc) {
-                v = s.X[((int64_t)b * s.C + c) * s.L_in + (up2 ? (p >> 1) : p)];
-                if (s.silu_in) v = silu(v);
-            }
-            xs[ci * kXsLd + j] = v;
-        }
-        for (int i = tid; i < kCoT * kCiT * KS; i += 256) {
-            const int co = i / (kCiT * KS), r = i - co * (kCiT * KS);
-            const int ci = r / KS;
-            float v = 0.f;
-            if (co0 + co < Cout && ci0 + ci < s.C)
-                v = ldw<TW>(s.W, (int64_t)(co0 + co) * s.ldw + (int64_t)ci0 * KS + r);
-            ws[r * kWsLd + co] = v;
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int ci = 0; ci < kCiT; ++ci) {
+    const int pstart = pos0 * s.stride - s.pad;
+    const float* X = s.X + (int64_t)b * s.C * s.L_in;
+    const int ncolp = (p.win + CW - 1) / CW;
+    const int nrowp = (p.cinp + RPP - 1) / RPP;
+    const int nitem = ncolp * nrowp;
+    const int ld = p.cinp + 4;
+    for (int base = 0; base < nitem; base += NB) {
+        float v[NB];
 #pragma unroll
-            for (int k = 0; k < KS; ++k) {
-                const float w0 = ws[(ci * KS + k) * kWsLd + ty * 2];
-                const float w1 = ws[(ci * KS + k) * kWsLd + ty * 2 + 1];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float x = xs[ci * kXsLd + (tx * 4 + i) * ST + k];
-                    acc[0][i] = fmaf(w0, x, acc[0][i]);
-                    acc[1][i] = fmaf(w1, x, acc[1][i]);
-                }
-            }
+        for (int u = 0; u < NB; ++u) {
+            const int it = base + u;
+            const int ci = (it / ncolp) * RPP + row, j = (it % ncolp) * CW + col;
+            const int pp = pstart + j;
+            v[u] = 0.f;
+            if (it < nitem && ci < s.C && j < p.win && pp >= 0 && pp < Lsrc)
+                v[u] = X[(int64_t)ci * s.L_in + (up2 ? (pp >> 1) : pp)];
         }
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int it = base + u;
+            const int ci = (it / ncolp) * RPP + row, j = (it % ncolp) * CW + col;
+            if (it < nitem && ci < p.cinp && j < p.win)
+                xs[j * ld + perm16(ci)] = s.silu_in ? silu(v[u]) : v[u];
+        }
     }
 }
 
 template <typename TW>
-__global__ __launch_bounds__(256) void conv1d_kernel(ldm_conv1d_args_t a) {
-    __shared__ __attribute__((aligned(16))) float xs[kCiT * kXsLd];
-    __shared__ __attribute__((aligned(16))) float ws[kCiT * kMaxKs * kWsLd];
-    const int l0 = blockIdx.x * kLT, co0 = blockIdx.y * kCoT, b = blockIdx.z;
-    float acc[2][4];
+__device__ __forceinline__ void stage_w(float* __restrict__ ws, const ldm_conv1d_seg_t& s,
+                                        const SegPlan& p, int co0) {
+    constexpr int NB = 32;
+    const int tid = threadIdx.x;
+    const int col = tid & 63, row = tid >> 6;         // 4 rows per pass
+    const int ncolp = (p.cinp + 63) / 64;
+    const int nitem = 4 * s.ksize * ncolp;            // (row pass, tap, column pass)
+    const int ld = s.ksize * p.cinp + 4;
+    const TW* W = reinterpret_cast<const TW*>(s.W);
+    for (int base = 0; base < nitem; base += NB) {
+        float v[NB];
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+        for (int u = 0; u < NB; ++u) {
+            const int it = base + u;
+            const int rp = it / (s.ksize * ncolp), rem = it % (s.ksize * ncolp);
+            const int k = rem / ncolp, e = (rem % ncolp) * 64 + col;
+            const int co = rp * 4 + row;
+            v[u] = 0.f;
+            if (it < nitem && e < p.cinp) {
+                const int64_t gi = (int64_t)(co0 + co) * s.ldw + (int64_t)k * s.kstride + e;
+                if constexpr (sizeof(TW) == 2) v[u] = bf16_to_f32(W[gi]);
+                else v[u] = W[gi];
+            }
+        }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[r][i] = 0.f;
-    for (int si = 0; si < a.n_seg; ++si) {
-        const ldm_conv1d_seg_t& s = a.seg[si];
-        if (s.ksize == 3 && s.stride == 1)
-            conv_segment<TW, 3, 1>(acc, xs, ws, s, b, co0, l0, a.Cout);
-        else if (s.ksize == 3 && s.stride == 2)
-            conv_segment<TW, 3, 2>(acc, xs, ws, s, b, co0, l0, a.Cout);
-        else if (s.ksize == 1)
-            conv_segment<TW, 1, 1>(acc, xs, ws, s, b, co0, l0, a.Cout);
-        else if (s.ksize == 4 && s.stride == 2)
-            conv_segment<TW, 4, 2>(acc, xs, ws, s, b, co0, l0, a.Cout);
+        for (int u = 0; u < NB; ++u) {
+            const int it = base + u;
+            const int rp = it / (s.ksize * ncolp), rem = it % (s.ksize * ncolp);
+            const int k = rem / ncolp, e = (rem % ncolp) * 64 + col;
+            const int co = rp * 4 + row;
+            if (it < nitem && e < p.cinp) ws[co * ld + k * p.cinp + e] = v[u];
+        }
     }
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+}
+
+template <typename TW, int TP>
+__global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, ConvPlan pl) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    constexpr int NT = TP / 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c16 = lane & 15;
+    const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
+
+    for (int si = 0; si < a.n_seg; ++si) {
+        stage_x<TP>(sm + pl.s[si].xoff, a.seg[si], pl.s[si], b, pos0);
+        stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
+    }
+    __syncthreads();
+
+    f32x4 acc[NT];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int co = co0 + ty * 2 + r;
-        if (co >= a.Cout) continue;
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c_beg = pl.nchunks * wave / 4, c_end = pl.nchunks * (wave + 1) / 4;
+    int si = 0;
+    for (int ch = c_beg; ch < c_end; ++ch) {
+        while (si + 1 < a.n_seg && ch >= pl.s[si + 1].ch0) ++si;
+        const SegPlan& p = pl.s[si];
+        const int ks = a.seg[si].ksize, st = a.seg[si].stride;
+        const int ng = p.cinp >> 4;
+        const int q = ch - p.ch0, k = q / ng, cg = q - k * ng;
+        const f32x4 av = *reinterpret_cast<const f32x4*>(
+            sm + p.woff + c16 * (ks * p.cinp + 4) + k * p.cinp + cg * 16 + 4 * g);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int j = (t * 16 + c16) * st + k;
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(
+                sm + p.xoff + j * (p.cinp + 4) + cg * 16 + 4 * g);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc[t], 0, 0, 0);
+        }
+    }
+    __syncthreads();                    // every wave is done reading the staged operands
+    float* red = sm;                    // [wave][t][reg][lane]
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[((wave * NT + t) * 4 + i) * 64 + lane] = acc[t][i];
+    __syncthreads();
+
+    for (int o = tid; o < 16 * TP; o += 256) {
+        const int r = o / TP, pc = o % TP;
+        const int co = co0 + r, l = pos0 + pc;
+        if (co >= a.Cout || l >= a.L_out) continue;
+        const int t = pc >> 4, ln = 16 * (r >> 2) + (pc & 15), i = r & 3;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[((w * NT + t) * 4 + i) * 64 + ln];
         float bb = 0.f;
         if (a.bias) bb += a.bias[co];
         if (a.bias2) bb += a.bias2[co];
         if (a.cbias) bb += a.cbias[(int64_t)b * a.scb + co];
-        const int64_t row = ((int64_t)b * a.Cout + co) * a.L_out;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int l = l0 + tx * 4 + i;
-            if (l >= a.L_out) continue;
-            float pre = acc[r][i] + bb;
-            if (a.R) pre += a.R[row + l];
-            if (a.epi == LDM_CONV_EPI_DDPM) {
-                const bool noise = a.t > 0;
-                a.Y[row + l] = ddpm_update(a.xlat[row + l], pre, noise ? a.z[row + l] : 0.f,
-                                           a.c1[a.t], a.c2[a.t], a.sigma[a.t], noise);
-            } else {
-                a.Y[row + l] = pre;
-            }
+        const int64_t idx = ((int64_t)b * a.Cout + co) * a.L_out + l;
+        float pre = v + bb;
+        if (a.R) pre += a.R[idx];
+        if (a.epi == LDM_CONV_EPI_DDPM) {
+            const bool noise = a.t > 0;
+            a.Y[idx] = ddpm_update(a.xlat[idx], pre, noise ? a.z[idx] : 0.f, a.c1[a.t],
+                                   a.c2[a.t], a.sigma[a.t], noise);
+        } else {
+            a.Y[idx] = pre;
         }
     }
+}
+
+constexpr int kMaxLdsBytes = 160 * 1024;
+
+int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) {
+    int off = 0, ch = 0;
+    for (int i = 0; i < a.n_seg; ++i) {
+        const ldm_conv1d_seg_t& g = a.seg[i];
+        SegPlan& p = pl->s[i];
+        p.cinp = round16(g.C);
+        p.win = (TP - 1) * g.stride + g.ksize;
+        p.xoff = off;
+        off += p.win * (p.cinp + 4);
+        p.woff = off;
+        off += 16 * (g.ksize * p.cinp + 4);
+        p.ch0 = ch;
+        ch += g.ksize * (p.cinp / 16);
+    }
+    pl->nchunks = ch;
+    const int red = 4 * (TP / 16) * 4 * 64;
+    *lds_bytes = 4 * (off > red ? off : red);
+    return *lds_bytes <= kMaxLdsBytes ? 0 : LDM_ENOSPC;
+}
+
+template <typename TW, int TP>
+int launch_tp(const ldm_conv1d_args_t& a, hipStream_t s) {
+    ConvPlan pl = {};
+    int lds = 0;
+    LDM_REQUIRE(make_plan(a, TP, &pl, &lds) == 0, LDM_ENOSPC,
+                "conv1d: staged operands need %d B of LDS (> %d); split the channels", lds,
+                kMaxLdsBytes);
+    static bool attr_set = false;     // one per instantiation; idempotent if raced
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&conv1d_mfma_kernel<TW, TP>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
+        LDM_REQUIRE(e == hipSuccess, (int)e, "conv1d: hipFuncSetAttribute: %s",
+                    hipGetErrorString(e));
+        attr_set = true;
+    }
+    const dim3 grid((a.L_out + TP - 1) / TP, (a.Cout + 15) / 16, a.B);
+    hipLaunchKernelGGL((conv1d_mfma_kernel<TW, TP>), grid, dim3(256), lds, s, a, pl);
+    return launch_status("ldm_conv1d");
+}
+
+template <typename TW>
+int launch_conv(const ldm_conv1d_args_t& a, hipStream_t s) {
+    // Widest tile that still leaves >= 512 workgroups (latency: small grids get TP = 16).
+    const long tiles16 = (long)((a.L_out + 15) / 16) * ((a.Cout + 15) / 16) * a.B;
+    if (tiles16 >= 4 * 512) return launch_tp<TW, 64>(a, s);
+    if (tiles16 >= 2 * 512) return launch_tp<TW, 32>(a, s);
+    return launch_tp<TW, 16>(a, s);
 }
 
 }  // namespace
@@ -160,14 +272,11 @@ extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
                     g.ksize, g.stride);
         LDM_REQUIRE(g.mode == LDM_CONV_DIRECT || (g.mode == LDM_CONV_UP2 && g.stride == 1),
                     LDM_EINVAL, "conv1d seg %d: bad mode %d", i, g.mode);
-        LDM_REQUIRE(g.ldw >= g.C * g.ksize, LDM_EINVAL, "conv1d seg %d: ldw %d < C*ksize", i,
-                    g.ldw);
+        LDM_REQUIRE(g.kstride >= ((g.C + 15) & ~15) && g.ldw >= g.ksize * g.kstride,
+                    LDM_EINVAL, "conv1d seg %d: packed weight pitches (ldw %d, kstride %d)",
+                    i, g.ldw, g.kstride);
         LDM_REQUIRE(g.pad < g.ksize, LDM_EINVAL, "conv1d seg %d: pad %d >= ksize", i, g.pad);
     }
-    const dim3 grid((a->L_out + kLT - 1) / kLT, (a->Cout + kCoT - 1) / kCoT, a->B);
-    if (a->w_dtype == LDM_BF16)
-        hipLaunchKernelGGL(conv1d_kernel<unsigned short>, grid, dim3(256), 0, (hipStream_t)s, *a);
-    else
-        hipLaunchKernelGGL(conv1d_kernel<float>, grid, dim3(256), 0, (hipStream_t)s, *a);
-    return launch_status("ldm_conv1d");
+    if (a->w_dtype == LDM_BF16) return launch_conv<unsigned short>(*a, (hipStream_t)s);
+    return launch_conv<float>(*a, (hipStream_t)s);
 }

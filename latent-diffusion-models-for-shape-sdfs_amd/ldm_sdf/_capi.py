@@ -75,7 +75,8 @@ CONV_EPI_STORE, CONV_EPI_DDPM = 0, 1
 class ConvSeg(C.Structure):
     _fields_ = [("X", _vp), ("W", _vp), ("C", C.c_int32), ("L_in", C.c_int32),
                 ("ksize", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
-                ("mode", C.c_int32), ("silu_in", C.c_int32), ("ldw", C.c_int32)]
+                ("mode", C.c_int32), ("silu_in", C.c_int32), ("ldw", C.c_int32),
+                ("kstride", C.c_int32)]
 
 
 class ConvArgs(C.Structure):

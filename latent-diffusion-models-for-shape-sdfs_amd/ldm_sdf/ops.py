@@ -240,16 +240,36 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------------------- C17
+def _r16(n: int) -> int:
+    return (n + 15) // 16 * 16
+
+
+def perm16_index(C: int) -> torch.Tensor:
+    """``perm16``: position of channel ci inside its group of 16 (include/ldm_sdf.h)."""
+    ci = torch.arange(C)
+    return (ci & ~15) | ((ci & 3) << 2) | ((ci >> 2) & 3)
+
+
+def pack_conv_weight(W: torch.Tensor) -> torch.Tensor:
+    """torch conv weight ``[Cout, Cw, K]`` -> the matrix-core packing ldm_conv1d reads:
+    ``[Cout16, K, Cw16]`` (zero-padded to multiples of 16) with channel ci at perm16(ci)."""
+    Cout, Cw, K = W.shape
+    out = torch.zeros(_r16(Cout), K, _r16(Cw), dtype=W.dtype, device=W.device)
+    out[:Cout, :, perm16_index(_r16(Cw))[:Cw].to(W.device)] = W.permute(0, 2, 1)
+    return out
+
+
 class ConvSegment:
     """One operand segment of ``ldm_conv1d``: input ``X [B, C, L_in]`` (fp32, contiguous),
-    weight ``W [Cout, Cw, ksize]`` (fp32/bf16, contiguous; the segment uses the column block
-    ``[c_off, c_off + C)``), tap geometry and the SiLU-on-input flag."""
+    packed weight ``Wp [Cout16, ksize, Cw16]`` (``pack_conv_weight``; fp32/bf16; the segment
+    uses input channels ``[c_off, c_off + C)``, c_off a multiple of 16), tap geometry and the
+    SiLU-on-input flag."""
 
     __slots__ = ("X", "W", "c_off", "ksize", "stride", "pad", "mode", "silu")
 
-    def __init__(self, X, W, *, c_off=0, stride=1, pad=None, mode=capi.CONV_DIRECT, silu=False):
-        self.X, self.W, self.c_off = X, W, c_off
-        self.ksize = W.shape[2]
+    def __init__(self, X, Wp, *, c_off=0, stride=1, pad=None, mode=capi.CONV_DIRECT, silu=False):
+        self.X, self.W, self.c_off = X, Wp, c_off
+        self.ksize = Wp.shape[1]
         self.stride, self.mode, self.silu = stride, mode, silu
         self.pad = (self.ksize - 1) // 2 if pad is None else pad
 
@@ -273,19 +293,22 @@ def conv1d_args(segs, Y: torch.Tensor, *, bias=None, bias2=None, cbias=None, scb
         X, W = s.X, s.W
         _f32(X)
         _contig(X, W)
-        if W.dtype != wdt or W.shape[0] != Cout or X.shape[0] != B:
-            raise capi.LdmError(f"conv1d seg {i}: weight/batch mismatch")
+        if W.dtype != wdt or W.dim() != 3 or W.shape[0] != _r16(Cout) or X.shape[0] != B \
+                or W.shape[2] % 16:
+            raise capi.LdmError(f"conv1d seg {i}: packed weight [{_r16(Cout)}, K, Cw16] / "
+                                f"batch mismatch (got {tuple(W.shape)})")
         Cs = X.shape[1]
-        if s.c_off + Cs > W.shape[1]:
-            raise capi.LdmError(f"conv1d seg {i}: channels {s.c_off}+{Cs} > {W.shape[1]}")
+        if s.c_off % 16 or s.c_off + Cs > W.shape[2]:
+            raise capi.LdmError(f"conv1d seg {i}: channels {s.c_off}+{Cs} vs {W.shape[2]}")
         Lsrc = 2 * X.shape[2] if s.mode == capi.CONV_UP2 else X.shape[2]
         if (Lsrc + 2 * s.pad - s.ksize) // s.stride + 1 != L_out:
             raise capi.LdmError(f"conv1d seg {i}: L_in {X.shape[2]} does not give L_out {L_out}")
         g = a.seg[i]
         g.X = X.data_ptr()
-        g.W = W.data_ptr() + s.c_off * s.ksize * W.element_size()
+        g.W = W.data_ptr() + s.c_off * W.element_size()
         g.C, g.L_in, g.ksize, g.stride, g.pad = Cs, X.shape[2], s.ksize, s.stride, s.pad
-        g.mode, g.silu_in, g.ldw = s.mode, int(bool(s.silu)), W.shape[1] * s.ksize
+        g.mode, g.silu_in = s.mode, int(bool(s.silu))
+        g.ldw, g.kstride = s.ksize * W.shape[2], W.shape[2]
     for name, v in (("bias", bias), ("bias2", bias2), ("R", R), ("xlat", xlat), ("z", z)):
         setattr(a, name, capi.ptr(v))
     if R is not None and R.shape != Y.shape:

@@ -94,8 +94,13 @@ class UNet1DDenoiser:
         wdt = {"fp32": torch.float32, "bf16": torch.bfloat16}[dtype]
         dev: Dict[str, object] = {}
         for n, v in self.params.items():
-            is_w = n.startswith("W") or n.endswith((".w", ".w1", ".w2", ".ws", ".p"))
-            dev[n] = v.to(device).to(wdt if is_w else torch.float32).contiguous()
+            v = v.to(device)
+            if n.endswith((".w", ".w1", ".w2", ".ws")):        # conv: matrix-core packing
+                dev[n] = ops.pack_conv_weight(v.to(wdt))
+            elif n.startswith("W") or n.endswith(".p"):       # linear [out][in]
+                dev[n] = v.to(wdt).contiguous()
+            else:
+                dev[n] = v.to(torch.float32).contiguous()
         emb = self.emb_table.to(device).contiguous()
         temb = ops.temb_forward(dev, emb, self.HT)                      # [T, HT]
         for i, (_, co) in enumerate(unet_res_specs(self.C)):

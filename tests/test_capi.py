@@ -51,6 +51,8 @@ def test_struct_layouts_match_c():
              sizeof(ldm_denoiser_t), sizeof(ldm_linear_args_t));
       printf("%zu %zu %zu %zu\n", offsetof(ldm_decoder_t, weights), offsetof(ldm_decoder_t, b_last),
              offsetof(ldm_denoiser_t, e_tab), offsetof(ldm_linear_args_t, A_out));
+      printf("%zu %zu %zu %zu\n", sizeof(ldm_conv1d_seg_t), sizeof(ldm_conv1d_args_t),
+             offsetof(ldm_conv1d_args_t, bias), offsetof(ldm_conv1d_args_t, t));
       return 0; }
     '''
     tmp = "/tmp/ldm_layout_check"
@@ -64,5 +66,7 @@ def test_struct_layouts_match_c():
     sizes = [int(x) for x in out]
     assert sizes[:4] == [ctypes.sizeof(capi.Decoder), ctypes.sizeof(capi.Sched),
                          ctypes.sizeof(capi.Denoiser), ctypes.sizeof(capi.LinearArgs)]
-    assert sizes[4:] == [capi.Decoder.weights.offset, capi.Decoder.b_last.offset,
-                         capi.Denoiser.e_tab.offset, capi.LinearArgs.A_out.offset]
+    assert sizes[4:8] == [capi.Decoder.weights.offset, capi.Decoder.b_last.offset,
+                          capi.Denoiser.e_tab.offset, capi.LinearArgs.A_out.offset]
+    assert sizes[8:] == [ctypes.sizeof(capi.ConvSeg), ctypes.sizeof(capi.ConvArgs),
+                         capi.ConvArgs.bias.offset, capi.ConvArgs.t.offset]

@@ -45,7 +45,8 @@ CASES = [
     ("k3s1_silu_cb_res", 2, [(40, 130, 3, 1, 0, True)], 40, True, True),
     ("k3s2", 2, [(33, 257, 3, 2, 0, False)], 70, False, False),
     ("up2", 2, [(64, 37, 3, 1, 1, False)], 20, False, False),
-    ("concat", 2, [(24, 64, 3, 1, 0, True), (24, 64, 3, 1, 0, True)], 24, True, False),
+    ("concat", 2, [(32, 64, 3, 1, 0, True), (20, 64, 3, 1, 0, True)], 24, True, False),
+    ("big_b_tile64", 40, [(64, 256, 3, 1, 0, True)], 64, True, True),
     ("k3_plus_1x1", 2, [(32, 64, 3, 1, 0, True), (16, 64, 1, 1, 0, False),
                         (16, 64, 1, 1, 0, False)], 32, False, False),
     ("k4s2", 2, [(8, 130, 4, 2, 0, False)], 5, False, False),
@@ -86,7 +87,7 @@ def test_conv1d_vs_torch(dev, case, wdt):
     if R is not None:
         ref = ref + R.double()
     Y = torch.empty(B, Cout, L_out, device=dev)
-    segs_dev = [ops.ConvSegment(X.to(dev), W.to(dev), c_off=co, stride=st, mode=mode, silu=silu,
+    segs_dev = [ops.ConvSegment(X.to(dev), ops.pack_conv_weight(W.to(dev)), c_off=co, stride=st, mode=mode, silu=silu,
                                 pad=1)
                 for (X, W, co, st, mode, silu) in specs]
     for s in segs_dev:
@@ -113,7 +114,8 @@ def test_conv1d_ddpm_epilogue(dev):
     z = torch.randn(B, L, generator=g)
     for t in (0, 1, 640, 999):
         out = torch.empty(B, L, device=dev)
-        ops.conv1d([ops.ConvSegment(X.to(dev), W.to(dev), silu=True)], out.view(B, 1, L),
+        ops.conv1d([ops.ConvSegment(X.to(dev), ops.pack_conv_weight(W.to(dev)), silu=True)],
+                   out.view(B, 1, L),
                    bias=b.to(dev), epi=1, xlat=x.to(dev), z=z.to(dev), sched=sd, t=t)
         eps = _ref_seg(X, W, 0, 1, 0, True)[:, 0] + b.double()
         want = R.ddpm_step(tab, x.double(), eps, z.double(), t)
@@ -123,12 +125,15 @@ def test_conv1d_ddpm_epilogue(dev):
 def test_conv1d_rejects_bad_args(dev):
     from ldm_sdf import LdmError, ops
     X = torch.randn(1, 4, 10, device=dev)
-    W = torch.randn(2, 4, 5, device=dev)          # ksize 5 unsupported
+    W = ops.pack_conv_weight(torch.randn(2, 4, 5, device=dev))      # ksize 5 unsupported
     with pytest.raises(LdmError):
         ops.conv1d([ops.ConvSegment(X, W)], torch.empty(1, 2, 10, device=dev))
-    W3 = torch.randn(2, 4, 3, device=dev)
+    W3 = ops.pack_conv_weight(torch.randn(2, 4, 3, device=dev))
     with pytest.raises(LdmError):                 # wrong output length
         ops.conv1d([ops.ConvSegment(X, W3)], torch.empty(1, 2, 9, device=dev))
+    with pytest.raises(LdmError):                 # unpacked [Cout, Cin, K] weight
+        ops.conv1d([ops.ConvSegment(X, torch.randn(2, 4, 3, device=dev))],
+                   torch.empty(1, 2, 10, device=dev))
 
 
 def _unet(dtype=torch.float64, rounded=False):

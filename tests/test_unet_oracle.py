@@ -143,3 +143,40 @@ def test_unet_rejects_bad_length(D):
             UNet1DDenoiser(D=D)
     else:
         UNet1DDenoiser(D=D, C=(2, 2, 2), HT=8, TE=8)
+
+
+def test_pack_conv_weight_layout():
+    """ldm_conv1d's packed weight: [Cout16][K][Cw16], channel ci at perm16(ci), zero pad."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(0)
+    W = torch.randn(5, 20, 3, generator=g)
+    P = ops.pack_conv_weight(W)
+    assert P.shape == (16, 3, 32)
+    perm = ops.perm16_index(32).tolist()
+    assert sorted(perm) == list(range(32))
+    for m in range(4):                 # lane group g reads channels 4m+g at 4g+m
+        for gg in range(4):
+            assert perm[4 * m + gg] == 4 * gg + m
+    for co in range(5):
+        for ci in range(20):
+            for k in range(3):
+                assert P[co, k, perm[ci]] == W[co, ci, k]
+    assert int((P != 0).sum()) == W.numel()                   # everything else is zero
+
+
+def test_conv_args_validation_on_host():
+    """conv1d_args builds/validates the C struct without touching a GPU."""
+    from ldm_sdf import LdmError, ops
+    X = torch.randn(2, 20, 64)
+    Wp = ops.pack_conv_weight(torch.randn(8, 40, 3))
+    Y = torch.empty(2, 8, 64)
+    a = ops.conv1d_args([ops.ConvSegment(X, Wp, silu=True), ops.ConvSegment(X, Wp, c_off=16)],
+                        Y)
+    assert a.n_seg == 2 and a.seg[1].W - a.seg[0].W == 16 * 4
+    assert a.seg[0].ldw == 3 * 48 and a.seg[0].kstride == 48
+    with pytest.raises(LdmError):      # channel offset not a multiple of 16
+        ops.conv1d_args([ops.ConvSegment(X, Wp, c_off=8)], Y)
+    with pytest.raises(LdmError):      # output length mismatch
+        ops.conv1d_args([ops.ConvSegment(X, Wp)], torch.empty(2, 8, 63))
+    with pytest.raises(LdmError):      # unpacked weight
+        ops.conv1d_args([ops.ConvSegment(X, torch.randn(8, 20, 3))], Y)
