@@ -49,14 +49,19 @@ struct SegPlan {
 struct ConvPlan {
     SegPlan s[LDM_CONV_MAX_SEGS];
     int nchunks;
+    int lds_floats;   // including 4 scratch floats at the end (stores of out-of-range slots)
 };
 
-template <int TP>
-__device__ __forceinline__ void stage_x(float* __restrict__ xs, const ldm_conv1d_seg_t& s,
-                                        const SegPlan& p, int b, int pos0) {
-    constexpr int CW = TP <= 16 ? 32 : 64;            // window columns per pass row
+// Staging issues every load of a segment before the first LDS store (one global round trip),
+// branch-free: out-of-range slots load a clamped in-bounds address and select 0, and store
+// to a scratch word past the operands.  The slot count NB is picked per segment from the
+// real item count (4 / 8 / 16 / 32), so a small segment does not pay a 32-slot unroll.
+template <int TP, int NB>
+__device__ __forceinline__ void stage_x_nb(float* __restrict__ xs, float* __restrict__ trash,
+                                           const ldm_conv1d_seg_t& s, const SegPlan& p, int b,
+                                           int pos0) {
+    constexpr int CW = TP <= 16 ? 32 : 64;            // window columns per pass
     constexpr int RPP = 256 / CW;                     // channel rows per pass
-    constexpr int NB = 32;
     const int tid = threadIdx.x;
     const int col = tid % CW, row = tid / CW;
     const bool up2 = s.mode == LDM_CONV_UP2;
@@ -64,64 +69,94 @@ __device__ __forceinline__ void stage_x(float* __restrict__ xs, const ldm_conv1d
     const int pstart = pos0 * s.stride - s.pad;
     const float* X = s.X + (int64_t)b * s.C * s.L_in;
     const int ncolp = (p.win + CW - 1) / CW;
-    const int nrowp = (p.cinp + RPP - 1) / RPP;
-    const int nitem = ncolp * nrowp;
+    const int nitem = ncolp * ((p.cinp + RPP - 1) / RPP);
     const int ld = p.cinp + 4;
     for (int base = 0; base < nitem; base += NB) {
         float v[NB];
+        int dst[NB];
+        int rp = base / ncolp, cp = base - rp * ncolp;
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
-            const int it = base + u;
-            const int ci = (it / ncolp) * RPP + row, j = (it % ncolp) * CW + col;
-            const int pp = pstart + j;
-            v[u] = 0.f;
-            if (it < nitem && ci < s.C && j < p.win && pp >= 0 && pp < Lsrc)
-                v[u] = X[(int64_t)ci * s.L_in + (up2 ? (pp >> 1) : pp)];
+            const int ci = rp * RPP + row, j = cp * CW + col, pp = pstart + j;
+            const bool in = base + u < nitem && ci < p.cinp && j < p.win;
+            const bool ok = in && ci < s.C && pp >= 0 && pp < Lsrc;
+            const int src = ok ? ci * s.L_in + (up2 ? (pp >> 1) : pp) : 0;
+            v[u] = X[src];
+            v[u] = ok ? v[u] : 0.f;
+            dst[u] = in ? j * ld + perm16(ci) : -1;
+            if (++cp == ncolp) { cp = 0; ++rp; }
         }
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
-            const int it = base + u;
-            const int ci = (it / ncolp) * RPP + row, j = (it % ncolp) * CW + col;
-            if (it < nitem && ci < p.cinp && j < p.win)
-                xs[j * ld + perm16(ci)] = s.silu_in ? silu(v[u]) : v[u];
+            float* d = dst[u] >= 0 ? xs + dst[u] : trash;
+            *d = s.silu_in ? silu(v[u]) : v[u];
+        }
+    }
+}
+
+template <int TP>
+__device__ __forceinline__ void stage_x(float* xs, float* trash, const ldm_conv1d_seg_t& s,
+                                        const SegPlan& p, int b, int pos0) {
+    constexpr int CW = TP <= 16 ? 32 : 64;
+    const int n = ((p.win + CW - 1) / CW) * ((p.cinp + 256 / CW - 1) / (256 / CW));
+    if (n <= 4) stage_x_nb<TP, 4>(xs, trash, s, p, b, pos0);
+    else if (n <= 8) stage_x_nb<TP, 8>(xs, trash, s, p, b, pos0);
+    else if (n <= 16) stage_x_nb<TP, 16>(xs, trash, s, p, b, pos0);
+    else stage_x_nb<TP, 32>(xs, trash, s, p, b, pos0);
+}
+
+// Weights: 16-byte vector loads along a packed row (4 fp32 or 8 bf16 channels per load).
+template <typename TW, int NB>
+__device__ __forceinline__ void stage_w_nb(float* __restrict__ ws, const ldm_conv1d_seg_t& s,
+                                           const SegPlan& p, int co0) {
+    constexpr int EPV = 16 / sizeof(TW);              // elements per 16-byte vector
+    const int tid = threadIdx.x;
+    const int nvec = p.cinp / EPV;                    // vectors per (row, tap)
+    const int per_row = s.ksize * nvec;
+    const int nitem = 16 * per_row;
+    const int ld = s.ksize * p.cinp + 4;
+    const char* W = reinterpret_cast<const char*>(s.W);
+    for (int base = 0; base < nitem; base += 256 * NB) {
+        u32x4 v[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int it = base + u * 256 + tid;
+            const int itc = it < nitem ? it : 0;
+            const int co = itc / per_row, r = itc - co * per_row;
+            const int k = r / nvec, e = (r - k * nvec) * EPV;
+            const int64_t gi = (int64_t)(co0 + co) * s.ldw + (int64_t)k * s.kstride + e;
+            v[u] = *reinterpret_cast<const u32x4*>(W + gi * (int64_t)sizeof(TW));
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int it = base + u * 256 + tid;
+            if (it >= nitem) continue;
+            const int co = it / per_row, r = it - co * per_row;
+            const int k = r / nvec, e = (r - k * nvec) * EPV;
+            float* d = ws + co * ld + k * p.cinp + e;
+            if constexpr (sizeof(TW) == 2) {
+                const u32x4 w = v[u];
+                *reinterpret_cast<f32x4*>(d) = f32x4{
+                    __builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
+                    __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
+                *reinterpret_cast<f32x4*>(d + 4) = f32x4{
+                    __builtin_bit_cast(float, w[2] << 16), __builtin_bit_cast(float, w[2] & 0xffff0000u),
+                    __builtin_bit_cast(float, w[3] << 16), __builtin_bit_cast(float, w[3] & 0xffff0000u)};
+            } else {
+                *reinterpret_cast<u32x4*>(d) = v[u];
+            }
         }
     }
 }
 
 template <typename TW>
-__device__ __forceinline__ void stage_w(float* __restrict__ ws, const ldm_conv1d_seg_t& s,
-                                        const SegPlan& p, int co0) {
-    constexpr int NB = 32;
-    const int tid = threadIdx.x;
-    const int col = tid & 63, row = tid >> 6;         // 4 rows per pass
-    const int ncolp = (p.cinp + 63) / 64;
-    const int nitem = 4 * s.ksize * ncolp;            // (row pass, tap, column pass)
-    const int ld = s.ksize * p.cinp + 4;
-    const TW* W = reinterpret_cast<const TW*>(s.W);
-    for (int base = 0; base < nitem; base += NB) {
-        float v[NB];
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int it = base + u;
-            const int rp = it / (s.ksize * ncolp), rem = it % (s.ksize * ncolp);
-            const int k = rem / ncolp, e = (rem % ncolp) * 64 + col;
-            const int co = rp * 4 + row;
-            v[u] = 0.f;
-            if (it < nitem && e < p.cinp) {
-                const int64_t gi = (int64_t)(co0 + co) * s.ldw + (int64_t)k * s.kstride + e;
-                if constexpr (sizeof(TW) == 2) v[u] = bf16_to_f32(W[gi]);
-                else v[u] = W[gi];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int it = base + u;
-            const int rp = it / (s.ksize * ncolp), rem = it % (s.ksize * ncolp);
-            const int k = rem / ncolp, e = (rem % ncolp) * 64 + col;
-            const int co = rp * 4 + row;
-            if (it < nitem && e < p.cinp) ws[co * ld + k * p.cinp + e] = v[u];
-        }
-    }
+__device__ __forceinline__ void stage_w(float* ws, const ldm_conv1d_seg_t& s, const SegPlan& p,
+                                        int co0) {
+    const int n = (16 * s.ksize * (p.cinp / (16 / (int)sizeof(TW))) + 255) / 256;
+    if (n <= 1) stage_w_nb<TW, 1>(ws, s, p, co0);
+    else if (n <= 2) stage_w_nb<TW, 2>(ws, s, p, co0);
+    else if (n <= 4) stage_w_nb<TW, 4>(ws, s, p, co0);
+    else stage_w_nb<TW, 8>(ws, s, p, co0);
 }
 
 template <typename TW, int TP>
@@ -132,9 +167,10 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, C
     const int g = lane >> 4, c16 = lane & 15;
     const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
 
+    float* trash = sm + pl.lds_floats - 4;
     for (int si = 0; si < a.n_seg; ++si) {
-        stage_x<TP>(sm + pl.s[si].xoff, a.seg[si], pl.s[si], b, pos0);
         stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
+        stage_x<TP>(sm + pl.s[si].xoff, trash, a.seg[si], pl.s[si], b, pos0);
     }
     __syncthreads();
 
@@ -142,13 +178,17 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, C
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int c_beg = pl.nchunks * wave / 4, c_end = pl.nchunks * (wave + 1) / 4;
+    // walk this wave's chunks with carried (segment, tap, channel group) counters
     int si = 0;
+    while (si + 1 < a.n_seg && c_beg >= pl.s[si + 1].ch0) ++si;
+    int ng = pl.s[si].cinp >> 4;
+    int q = c_beg - pl.s[si].ch0;
+    int k = 0;
+    while (q >= ng) { q -= ng; ++k; }
+    int cg = q;
     for (int ch = c_beg; ch < c_end; ++ch) {
-        while (si + 1 < a.n_seg && ch >= pl.s[si + 1].ch0) ++si;
         const SegPlan& p = pl.s[si];
         const int ks = a.seg[si].ksize, st = a.seg[si].stride;
-        const int ng = p.cinp >> 4;
-        const int q = ch - p.ch0, k = q / ng, cg = q - k * ng;
         const f32x4 av = *reinterpret_cast<const f32x4*>(
             sm + p.woff + c16 * (ks * p.cinp + 4) + k * p.cinp + cg * 16 + 4 * g);
 #pragma unroll
@@ -159,6 +199,10 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, C
 #pragma unroll
             for (int m = 0; m < 4; ++m)
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc[t], 0, 0, 0);
+        }
+        if (++cg == ng) {
+            cg = 0;
+            if (++k == ks && si + 1 < a.n_seg) { k = 0; ++si; ng = pl.s[si].cinp >> 4; }
         }
     }
     __syncthreads();                    // every wave is done reading the staged operands
@@ -212,7 +256,8 @@ int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) 
     }
     pl->nchunks = ch;
     const int red = 4 * (TP / 16) * 4 * 64;
-    *lds_bytes = 4 * (off > red ? off : red);
+    pl->lds_floats = (off > red ? off : red) + 4;
+    *lds_bytes = 4 * pl->lds_floats;
     return *lds_bytes <= kMaxLdsBytes ? 0 : LDM_ENOSPC;
 }
 
