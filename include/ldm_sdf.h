@@ -228,6 +228,24 @@ typedef struct ldm_conv1d_args {
 } ldm_conv1d_args_t;
 int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s);
 
+/* ---- C18 marching cubes on a decoded volume ---------------------------- */
+/* vol: fp32 [N][N][N] (z slowest, as decode writes it); a corner is inside when v < level.
+ * Vertices are one per crossing grid edge, ordered by (owner point, axis), positions by the A1
+ * grid rule and p0 + t (p1 - p0), t = (level - v0) / (v1 - v0), each op rounded to fp32;
+ * faces are int32 vertex triples ordered by (cube, case-table order), wound so that
+ * (b - a) x (c - a) points toward larger values.  Two passes, because the caller allocates
+ * the outputs: ldm_mc_count writes device int32 counts_out[2] = {n_vertices, n_faces};
+ * ldm_mc_emit (same vol / level / ws) then fills verts fp32 [V][3] and faces int32 [F][3]. */
+size_t ldm_mc_workspace_bytes(int N);
+int ldm_mc_count(const float* vol, int N, float level, void* ws, size_t ws_bytes,
+                 int32_t* counts_out, ldm_stream_t s);
+int ldm_mc_emit(const float* vol, int N, float level, float vs, float origin, void* ws,
+                size_t ws_bytes, float* verts, int32_t* faces, ldm_stream_t s);
+/* Host: the compile-time generated case table: tri [256][16] cube-edge ids (-1 padded),
+ * ntri [256].  Edge e = 4a + m runs along axis a (x, y, z) from the corner whose other two
+ * coordinate bits (lower axis first) are m; corner c sits at (c & 1, c >> 1 & 1, c >> 2 & 1). */
+int ldm_mc_table(int8_t* tri, uint8_t* ntri);
+
 #ifdef __cplusplus
 }
 #endif

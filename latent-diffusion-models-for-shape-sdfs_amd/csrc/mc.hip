@@ -1,0 +1,443 @@
+// C18: marching cubes on a decoded SDF volume, MI355X (gfx950).  DESIGN.md §10.
+//
+// The consumer of decode's output.  Conventions -- corner / edge
+// numbering, the face-local ambiguity rule, vertex and face order, fp32 interpolation -- are
+// those of oracle/ref_mc.py, which the GPU output matches bit for bit.
+//
+// The case table is GENERATED at compile time (constexpr) from the rule, independently of the
+// oracle's Python generator; tests compare the two tables (ldm_mc_table exports this one).
+//
+// Passes (HBM-bound integer/byte work; no MFMA):
+//   1. classify   one thread per grid point: 3-bit mask of its owned crossing edges (+x, +y,
+//                 +z), and for the cube it anchors the 8-corner case and its triangle count,
+//                 packed in one u16 (mask | ntri << 3 | case << 8) -> 2 B/point written
+//   2. block sums per 4096-point chunk: (#vertices, #triangles)
+//   3. chunk scan  one workgroup: exclusive offsets of the chunks + the totals
+//   4. vertices   per chunk: in-chunk exclusive scan, vertex positions, per-point first
+//                 vertex index (vofs)
+//   5. faces      per chunk: in-chunk scan of triangle counts, 3 vertex ids per triangle
+//                 through vofs + the owner's mask
+// Vertex order = (owner point, axis); face order = (cube, table order): a pure function of
+// the volume, so the output is deterministic and equal to the oracle's.
+#include "ldm_internal.h"
+
+#include <string.h>
+
+namespace ldm {
+namespace {
+
+// ------------------------------------------------------------------------------ case table
+struct McTables {
+    signed char tri[256][16];
+    unsigned char ntri[256];
+};
+
+// corner c: offset (c & 1, c >> 1 & 1, c >> 2 & 1); edge e = 4a + m along axis a from the
+// corner whose other two bits (lower axis first) are m.
+constexpr int mc_edge_id(int c0, int c1) {
+    const int d = c0 ^ c1;
+    const int a = d == 1 ? 0 : (d == 2 ? 1 : 2);
+    const int o0 = a == 0 ? 1 : 0, o1 = a == 2 ? 1 : 2;
+    const int lo = c0 & c1;
+    return 4 * a + (((lo >> o0) & 1) | (((lo >> o1) & 1) << 1));
+}
+constexpr int mc_edge_start(int e) {
+    const int a = e / 4, m = e % 4;
+    const int o0 = a == 0 ? 1 : 0, o1 = a == 2 ? 1 : 2;
+    return ((m & 1) << o0) | (((m >> 1) & 1) << o1);
+}
+
+struct McFaces {
+    int c[6][4];
+};
+// faces as corner rings, counter-clockwise seen from outside the cube
+constexpr McFaces mc_faces() {
+    McFaces f{};
+    int n = 0;
+    for (int a = 0; a < 3; ++a) {
+        const int u = (a + 1) % 3, w = (a + 2) % 3;
+        for (int s = 0; s < 2; ++s) {
+            const int ub[4] = {0, 1, 1, 0}, wb[4] = {0, 0, 1, 1};
+            for (int q = 0; q < 4; ++q) {
+                const int r = s ? q : 3 - q;          // outward normal -e_a: reversed ring
+                f.c[n][q] = (s << a) | (ub[r] << u) | (wb[r] << w);
+            }
+            ++n;
+        }
+    }
+    return f;
+}
+
+// bitmask of the (two) faces containing edge e
+constexpr int mc_edge_face_mask(int e, const McFaces& F) {
+    const int c0 = mc_edge_start(e), c1 = c0 | (1 << (e / 4));
+    int m = 0;
+    for (int f = 0; f < 6; ++f) {
+        bool h0 = false, h1 = false;
+        for (int q = 0; q < 4; ++q) {
+            h0 = h0 || F.c[f][q] == c0;
+            h1 = h1 || F.c[f][q] == c1;
+        }
+        if (h0 && h1) m |= 1 << f;
+    }
+    return m;
+}
+
+constexpr McTables make_mc_tables() {
+    McTables T{};
+    const McFaces F = mc_faces();
+    int efm[12] = {};
+    for (int e = 0; e < 12; ++e) efm[e] = mc_edge_face_mask(e, F);
+    for (int cfg = 0; cfg < 256; ++cfg) {
+        for (int i = 0; i < 16; ++i) T.tri[cfg][i] = -1;
+        int nxt[12] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+        for (int f = 0; f < 6; ++f) {
+            int ce[4] = {}, ck[4] = {}, nc = 0;      // crossings: edge, kind (1 = leaves inside)
+            for (int q = 0; q < 4; ++q) {
+                const int A = F.c[f][q], B = F.c[f][(q + 1) % 4];
+                const int ia = (cfg >> A) & 1, ib = (cfg >> B) & 1;
+                if (ia != ib) {
+                    ce[nc] = mc_edge_id(A, B);
+                    ck[nc] = ia;
+                    ++nc;
+                }
+            }
+            for (int q = 0; q < nc; ++q) {
+                if (!ck[q]) continue;
+                int r = (q + nc - 1) % nc;
+                while (ck[r]) r = (r + nc - 1) % nc;  // closest earlier "enters inside"
+                nxt[ce[q]] = ce[r];
+            }
+        }
+        bool seen[12] = {};
+        int nt = 0;
+        for (int s0 = 0; s0 < 12; ++s0) {
+            if (nxt[s0] < 0 || seen[s0]) continue;
+            int cyc[12] = {}, n = 0;
+            int e = s0;
+            do {
+                cyc[n++] = e;
+                seen[e] = true;
+                e = nxt[e];
+            } while (e != s0);
+            // first rotation whose fan diagonals avoid the cube faces
+            int r0 = -1;
+            for (int r = 0; r < n && r0 < 0; ++r) {
+                bool ok = true;
+                for (int i = 2; i < n - 1; ++i)
+                    if (efm[cyc[r]] & efm[cyc[(r + i) % n]]) ok = false;
+                if (ok) r0 = r;
+            }
+            if (r0 < 0) r0 = 0;                       // never taken (checked by the tests)
+            for (int i = 1; i < n - 1; ++i) {
+                T.tri[cfg][3 * nt + 0] = (signed char)cyc[r0];
+                T.tri[cfg][3 * nt + 1] = (signed char)cyc[(r0 + i + 1) % n];
+                T.tri[cfg][3 * nt + 2] = (signed char)cyc[(r0 + i) % n];
+                ++nt;
+            }
+        }
+        T.ntri[cfg] = (unsigned char)nt;
+    }
+    return T;
+}
+
+constexpr McTables kMcHost = make_mc_tables();
+__constant__ McTables kMc = make_mc_tables();
+
+// ------------------------------------------------------------------------------ kernels
+constexpr int kChunk = 4096;          // points per scan chunk (256 threads x 16)
+constexpr int kPer = 16;
+
+__device__ __forceinline__ float grid_c(int i, float vs, float origin) {
+#pragma clang fp contract(off)
+    return i * vs + origin;             // A1: two roundings
+}
+
+// 1. classify: block (64, 4), grid (ceil(N/64), ceil(N/4), N)
+__global__ __launch_bounds__(256) void mc_classify_kernel(const float* __restrict__ vol, int N,
+                                                          float iso,
+                                                          unsigned short* __restrict__ code) {
+    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y, k = blockIdx.z;
+    if (i >= N || j >= N) return;
+    const int64_t NN = (int64_t)N * N;
+    const int64_t p = k * NN + (int64_t)j * N + i;
+    const bool in0 = vol[p] < iso;
+    unsigned m = 0;
+    if (i + 1 < N && ((vol[p + 1] < iso) != in0)) m |= 1;
+    if (j + 1 < N && ((vol[p + N] < iso) != in0)) m |= 2;
+    if (k + 1 < N && ((vol[p + NN] < iso) != in0)) m |= 4;
+    unsigned cfg = 0, nt = 0;
+    if (i + 1 < N && j + 1 < N && k + 1 < N) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int64_t q = p + (c & 1) + ((c >> 1) & 1) * (int64_t)N + ((c >> 2) & 1) * NN;
+            cfg |= (unsigned)(vol[q] < iso) << c;
+        }
+        nt = kMc.ntri[cfg];
+    }
+    code[p] = (unsigned short)(m | (nt << 3) | (cfg << 8));
+}
+
+__device__ __forceinline__ int nvert_of(unsigned c) { return __popc(c & 7u); }
+__device__ __forceinline__ int ntri_of(unsigned c) { return (c >> 3) & 7u; }
+
+// block-wide exclusive scan of one int per thread (256 threads); returns the block total
+__device__ __forceinline__ int block_excl_scan(int v, int* lds /*[4]*/, int* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wv] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w < wv) base += lds[w];
+        tot += lds[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// load the 16 codes of this thread's slice of chunk `blk` (zeros past n)
+__device__ __forceinline__ void load_codes(const unsigned short* __restrict__ code, int64_t n,
+                                           int blk, unsigned (&c)[kPer]) {
+    const int64_t p0 = (int64_t)blk * kChunk + threadIdx.x * kPer;
+    if (p0 + kPer <= n) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(code + p0);
+        const u32x4 a = src[0], b = src[1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            c[2 * q] = a[q] & 0xffffu;
+            c[2 * q + 1] = a[q] >> 16;
+            c[8 + 2 * q] = b[q] & 0xffffu;
+            c[8 + 2 * q + 1] = b[q] >> 16;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) c[q] = p0 + q < n ? code[p0 + q] : 0u;
+    }
+}
+
+// 2. per-chunk (#vertices, #triangles)
+__global__ __launch_bounds__(256) void mc_block_sums_kernel(const unsigned short* __restrict__ code,
+                                                            int64_t n, int2* __restrict__ bsum) {
+    __shared__ int lds[8];
+    unsigned c[kPer];
+    load_codes(code, n, blockIdx.x, c);
+    int nv = 0, nt = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        nv += nvert_of(c[q]);
+        nt += ntri_of(c[q]);
+    }
+    int tv, tt;
+    block_excl_scan(nv, lds, &tv);
+    block_excl_scan(nt, lds + 4, &tt);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = make_int2(tv, tt);
+}
+
+// 3. exclusive scan of the chunk sums (one workgroup) + totals
+__global__ __launch_bounds__(256) void mc_chunk_scan_kernel(const int2* __restrict__ bsum, int nb,
+                                                            int2* __restrict__ boff,
+                                                            int32_t* __restrict__ totals) {
+    __shared__ int lds[8];
+    int cv = 0, ct = 0;
+    for (int b0 = 0; b0 < nb; b0 += 256) {
+        const int b = b0 + threadIdx.x;
+        const int2 s = b < nb ? bsum[b] : make_int2(0, 0);
+        int tv, tt;
+        const int ev = block_excl_scan(s.x, lds, &tv);
+        const int et = block_excl_scan(s.y, lds + 4, &tt);
+        if (b < nb) boff[b] = make_int2(cv + ev, ct + et);
+        cv += tv;
+        ct += tt;
+    }
+    if (threadIdx.x == 0) {
+        totals[0] = cv;
+        totals[1] = ct;
+    }
+}
+
+// 4. vertices + per-point first vertex index
+__global__ __launch_bounds__(256) void mc_vertices_kernel(const float* __restrict__ vol, int N,
+                                                          float iso, float vs, float origin,
+                                                          const unsigned short* __restrict__ code,
+                                                          const int2* __restrict__ boff,
+                                                          int32_t* __restrict__ vofs,
+                                                          float* __restrict__ verts) {
+#pragma clang fp contract(off)
+    __shared__ int lds[4];
+    const int64_t NN = (int64_t)N * N, n = NN * N;
+    unsigned c[kPer];
+    load_codes(code, n, blockIdx.x, c);
+    int nv = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) nv += nvert_of(c[q]);
+    int tot;
+    int off = boff[blockIdx.x].x + block_excl_scan(nv, lds, &tot);
+    if (nv == 0) return;
+    const int64_t p0 = (int64_t)blockIdx.x * kChunk + threadIdx.x * kPer;
+    for (int q = 0; q < kPer; ++q) {
+        const unsigned m = c[q] & 7u;
+        if (!m) continue;
+        const int64_t p = p0 + q;
+        vofs[p] = off;
+        const int i = (int)(p % N), j = (int)((p / N) % N), k = (int)(p / NN);
+        const float v0 = vol[p];
+        const float x = grid_c(i, vs, origin), y = grid_c(j, vs, origin), z = grid_c(k, vs, origin);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (!(m & (1u << a))) continue;
+            const int64_t st = a == 0 ? 1 : (a == 1 ? (int64_t)N : NN);
+            const float v1 = vol[p + st];
+            const float t = (iso - v0) / (v1 - v0);
+            float o[3] = {x, y, z};
+            const int ia = a == 0 ? i : (a == 1 ? j : k);
+            const float c0 = o[a], c1 = grid_c(ia + 1, vs, origin);
+            const float d = c1 - c0;
+            const float td = t * d;
+            o[a] = c0 + td;
+            float* dst = verts + (int64_t)off * 3;
+            dst[0] = o[0];
+            dst[1] = o[1];
+            dst[2] = o[2];
+            ++off;
+        }
+    }
+}
+
+// 5. triangles
+__global__ __launch_bounds__(256) void mc_faces_kernel(int N, const unsigned short* __restrict__ code,
+                                                       const int2* __restrict__ boff,
+                                                       const int32_t* __restrict__ vofs,
+                                                       int32_t* __restrict__ faces) {
+    __shared__ int lds[4];
+    const int64_t NN = (int64_t)N * N, n = NN * N;
+    unsigned c[kPer];
+    load_codes(code, n, blockIdx.x, c);
+    int nt = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) nt += ntri_of(c[q]);
+    int tot;
+    int off = boff[blockIdx.x].y + block_excl_scan(nt, lds, &tot);
+    if (nt == 0) return;
+    const int64_t p0 = (int64_t)blockIdx.x * kChunk + threadIdx.x * kPer;
+    for (int q = 0; q < kPer; ++q) {
+        const int ntq = ntri_of(c[q]);
+        if (!ntq) continue;
+        const int64_t p = p0 + q;
+        const unsigned cfg = c[q] >> 8;
+        for (int t = 0; t < ntq; ++t) {
+            int32_t* dst = faces + (int64_t)off * 3;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const int e = kMc.tri[cfg][3 * t + r];
+                const int a = e >> 2, s = mc_edge_start(e);
+                const int64_t owner = p + (s & 1) + ((s >> 1) & 1) * (int64_t)N + ((s >> 2) & 1) * NN;
+                const unsigned om = code[owner] & 7u;
+                dst[r] = vofs[owner] + __popc(om & ((1u << a) - 1u));
+            }
+            ++off;
+        }
+    }
+}
+
+struct McWs {
+    unsigned short* code;
+    int2* bsum;
+    int2* boff;
+    int32_t* vofs;
+    size_t bytes;
+};
+
+McWs mc_ws_layout(int N, void* base) {
+    const int64_t n = (int64_t)N * N * N;
+    const int64_t nb = (n + kChunk - 1) / kChunk;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    McWs w{};
+    char* b = reinterpret_cast<char*>(base);
+    size_t o = 0;
+    w.code = reinterpret_cast<unsigned short*>(b + o);
+    o += up((size_t)nb * kChunk * 2);           // padded to whole chunks (vector loads)
+    w.bsum = reinterpret_cast<int2*>(b + o);
+    o += up((size_t)nb * sizeof(int2));
+    w.boff = reinterpret_cast<int2*>(b + o);
+    o += up((size_t)nb * sizeof(int2));
+    w.vofs = reinterpret_cast<int32_t*>(b + o);
+    o += up((size_t)n * 4);
+    w.bytes = o;
+    return w;
+}
+
+int check_mc(const float* vol, int N, const void* ws, size_t ws_bytes) {
+    LDM_REQUIRE(vol && ws, LDM_EINVAL, "marching cubes: NULL volume/workspace");
+    LDM_REQUIRE(N >= 2 && N <= 1290, LDM_EINVAL, "marching cubes: N = %d out of [2, 1290]", N);
+    LDM_REQUIRE(LDM_ALIGNED(ws, 256) && LDM_ALIGNED(vol, 16), LDM_EALIGN,
+                "marching cubes: workspace must be 256-B aligned");
+    const McWs w = mc_ws_layout(N, nullptr);
+    LDM_REQUIRE(ws_bytes >= w.bytes, LDM_ENOSPC, "marching cubes: workspace %zu < %zu B",
+                ws_bytes, w.bytes);
+    return 0;
+}
+
+}  // namespace
+}  // namespace ldm
+
+extern "C" size_t ldm_mc_workspace_bytes(int N) {
+    if (N < 2) return 0;
+    return ldm::mc_ws_layout(N, nullptr).bytes;
+}
+
+extern "C" int ldm_mc_table(int8_t* tri, uint8_t* ntri) {
+    LDM_REQUIRE(tri && ntri, LDM_EINVAL, "ldm_mc_table: NULL output");
+    memcpy(tri, ldm::kMcHost.tri, sizeof(ldm::kMcHost.tri));
+    memcpy(ntri, ldm::kMcHost.ntri, sizeof(ldm::kMcHost.ntri));
+    return 0;
+}
+
+extern "C" int ldm_mc_count(const float* vol, int N, float level, void* ws, size_t ws_bytes,
+                            int32_t* counts_out, ldm_stream_t s) {
+    using namespace ldm;
+    if (int e = check_mc(vol, N, ws, ws_bytes)) return e;
+    LDM_REQUIRE(counts_out, LDM_EINVAL, "ldm_mc_count: NULL counts_out");
+    const McWs w = mc_ws_layout(N, ws);
+    const int64_t n = (int64_t)N * N * N;
+    const int nb = (int)((n + kChunk - 1) / kChunk);
+    hipStream_t st = (hipStream_t)s;
+    // the chunk padding past n must read as zero codes
+    if ((int64_t)nb * kChunk > n) {
+        const hipError_t e = hipMemsetAsync(w.code + n, 0, ((int64_t)nb * kChunk - n) * 2, st);
+        LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_mc_count: memset: %s", hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(mc_classify_kernel, dim3((N + 63) / 64, (N + 3) / 4, N), dim3(64, 4), 0,
+                       st, vol, N, level, w.code);
+    hipLaunchKernelGGL(mc_block_sums_kernel, dim3(nb), dim3(256), 0, st, w.code, n, w.bsum);
+    hipLaunchKernelGGL(mc_chunk_scan_kernel, dim3(1), dim3(256), 0, st, w.bsum, nb, w.boff,
+                       counts_out);
+    return launch_status("ldm_mc_count");
+}
+
+extern "C" int ldm_mc_emit(const float* vol, int N, float level, float vs, float origin,
+                           void* ws, size_t ws_bytes, float* verts, int32_t* faces,
+                           ldm_stream_t s) {
+    using namespace ldm;
+    if (int e = check_mc(vol, N, ws, ws_bytes)) return e;
+    const McWs w = mc_ws_layout(N, ws);
+    const int64_t n = (int64_t)N * N * N;
+    const int nb = (int)((n + kChunk - 1) / kChunk);
+    hipStream_t st = (hipStream_t)s;
+    if (verts)
+        hipLaunchKernelGGL(mc_vertices_kernel, dim3(nb), dim3(256), 0, st, vol, N, level, vs,
+                           origin, w.code, w.boff, w.vofs, verts);
+    if (faces) {
+        LDM_REQUIRE(verts, LDM_EINVAL, "ldm_mc_emit: faces need the vertex pass");
+        hipLaunchKernelGGL(mc_faces_kernel, dim3(nb), dim3(256), 0, st, N, w.code, w.boff,
+                           w.vofs, faces);
+    }
+    return launch_status("ldm_mc_emit");
+}

@@ -111,6 +111,10 @@ SIGNATURES = [
     ("ldm_colsum", _i, [_fp, _i, _i, _fp, _i, _vp]),
     ("ldm_gather_rows", _i, [_fp, _vp, _i, _i, _fp, _vp]),
     ("ldm_conv1d", _i, [C.POINTER(ConvArgs), _vp]),
+    ("ldm_mc_workspace_bytes", _sz, [_i]),
+    ("ldm_mc_count", _i, [_fp, _i, _f, _vp, _sz, _vp, _vp]),
+    ("ldm_mc_emit", _i, [_fp, _i, _f, _f, _f, _vp, _sz, _fp, _vp, _vp]),
+    ("ldm_mc_table", _i, [_vp, _vp]),
 ]
 
 _lib: Optional[C.CDLL] = None

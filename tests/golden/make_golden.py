@@ -21,6 +21,7 @@ sys.path.insert(0, ROOT)
 
 from oracle import ref_cpu as R  # noqa: E402
 from oracle import ref_unet as U  # noqa: E402
+from oracle import ref_mc as MC  # noqa: E402
 
 DEC_SEED, LAT_SEED, PTS_SEED = 1234, 0, 7
 DEN_SEED, SAMPLE_SEED = 4321, 11
@@ -105,8 +106,20 @@ def unet_case(steps=10, B=2):
                 eps_mixed=eps_mixed.numpy(), steps=np.int32(steps))
 
 
+def mc_case(N=24):
+    """C18: marching cubes of a sphere-plus-noise volume (every ambiguous case occurs)."""
+    rng = np.random.default_rng(5)
+    c = MC._coords(N)
+    z, y, x = np.meshgrid(c, c, c, indexing="ij")
+    vol = (np.sqrt(x * x + y * y + z * z) - 0.6 + 0.15 * rng.standard_normal((N, N, N)))
+    vol = vol.astype(np.float32)
+    verts, faces = MC.marching_cubes(vol)
+    return dict(vol=vol, verts=verts, faces=faces)
+
+
 CASES = {"decoder_small": decoder_case, "decoder_widen": widen_case,
-         "sampling_20": sampling_case, "train_step": train_case, "unet_10": unet_case}
+         "sampling_20": sampling_case, "train_step": train_case, "unet_10": unet_case,
+         "mc_24": mc_case}
 
 
 def main():
