@@ -50,6 +50,8 @@ def parse():
                     help="skip config 5 (1D-UNet sampling on 1024-d latents -> fp16 decode "
                          "of a 512^3 grid with the widen-skip decoder)")
     ap.add_argument("--c5-batch", type=int, default=1)
+    ap.add_argument("--no-mc", action="store_true",
+                    help="skip C18 (marching cubes of one decoded 256^3 volume)")
     ap.add_argument("--config3", action="store_true",
                     help="also time sample(8) -> decode 128^3 end to end (adds a decoder "
                          "launch of another size to the profile)")
@@ -108,6 +110,41 @@ def cpu_baseline_sampling(budget_s: float, B: int):
     dt = time.perf_counter() - t0
     return {"value": steps / dt, "unit": "steps/s", "cores": torch.get_num_threads(),
             "kind": "port", "sample": f"{steps} reverse steps, B={B}, fp32 torch-CPU oracle"}
+
+
+def bench_mc(vol, args):
+    """C18: marching cubes of one decoded volume (shape 0 of the step), on the GPU, with the
+    oracle (numpy) timed on the same volume as the CPU baseline."""
+    import ldm_sdf
+    from ldm_sdf import _capi as capi
+    N = vol.shape[-1]
+    ws = torch.empty(capi.load().ldm_mc_workspace_bytes(N), device=vol.device, dtype=torch.uint8)
+    v, f = ldm_sdf.marching_cubes(vol, ws=ws)
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        v, f = ldm_sdf.marching_cubes(vol, ws=ws)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    nbytes = N ** 3 * 4 + v.shape[0] * 12 + f.shape[0] * 12
+    res = {"metric": "marching cubes of one decoded volume", "grid": N,
+           "vertices": int(v.shape[0]), "faces": int(f.shape[0]), "ms_per_mesh": dt * 1e3,
+           "note": "wall time incl. the one count read-back between the passes",
+           "roofline": {"bound": "hbm", "achieved": nbytes / dt / 1e9, "peak": 8000.0,
+                        "unit": "GB/s", "frac": nbytes / dt / 8e12,
+                        "algorithmic_bytes": nbytes}}
+    if not args.no_cpu:
+        from oracle import ref_mc as M
+        vn = vol.cpu().numpy()
+        t1 = time.perf_counter()
+        M.marching_cubes(vn)
+        res["cpu_baseline"] = {"value": 1.0 / (time.perf_counter() - t1), "unit": "meshes/s",
+                               "cores": 1, "kind": "port",
+                               "sample": f"oracle/ref_mc.py (numpy) on the same {N}^3 volume"}
+    res["value"] = 1.0 / dt
+    res["unit"] = "meshes/s"
+    return res
 
 
 FLOPS_PER_QUERY_WIDEN = 2 * (3 * 512 + 2 * 512 * 512 + 512 * 512 + 515 * 512 + 3 * 512 * 512
@@ -321,6 +358,8 @@ def main():
                                     "frac": sps * wbytes / 8e12,
                                     "bytes_per_step": wbytes},
                        "config3_sample_plus_decode128_s": e2e}
+    if rank == 0 and not args.no_mc:
+        res["mc"] = bench_mc(out[0], args)
     if not args.no_config5:
         res_c5 = config5(args, rank, world, dev, group, gen)
         if rank == 0:
