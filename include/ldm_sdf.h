@@ -178,7 +178,13 @@ typedef struct ldm_linear_args {
     const float* R;  int64_t srb;    /* residual rows (col stride 1) */
     float* Y;        int64_t syb, sym;
     float* A_out;    int64_t sab;    /* pre-activation rows (col stride 1) */
+    int32_t compute;                 /* LDM_COMPUTE_FP32 or LDM_COMPUTE_BF16 (below) */
 } ldm_linear_args_t;
+/* LDM_COMPUTE_FP32: exact fp32 products (VALU register-tiled kernel).
+ * LDM_COMPUTE_BF16: matrix cores -- X and W rounded to bf16 (RNE) as they are staged, fp32
+ * products and accumulation (mixed-precision training; any w_dtype). */
+#define LDM_COMPUTE_FP32 0
+#define LDM_COMPUTE_BF16 1
 int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s);
 
 /* SiLU backward on the block pre-activation: g = dy * silu'(a)  (A7). n elements. */

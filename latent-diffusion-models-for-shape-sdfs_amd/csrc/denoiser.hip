@@ -508,13 +508,30 @@ __global__ void silu_bwd_kernel(const float* __restrict__ dy, const float* __res
     if (i < n) g[i] = dy[i] * silu_grad(a[i]);
 }
 
-__global__ void colsum_kernel(const float* __restrict__ G, int Bn, int M, float* __restrict__ out,
-                              int accumulate) {
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= M) return;
-    float s = 0.f;
-    for (int b = 0; b < Bn; ++b) s += G[(size_t)b * M + m];
-    out[m] = accumulate ? out[m] + s : s;
+// Column sums, 64 columns per workgroup of 1024 threads: 16 row groups x 64 columns, each
+// thread 4 interleaved partial sums over rows r = ty + 16 i, then a fixed-order LDS reduce
+// (deterministic; one column per thread serialised ~1000 dependent loads before).
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ G, int Bn, int M,
+                                                     float* __restrict__ out, int accumulate) {
+    __shared__ float red[16][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int m = blockIdx.x * 64 + tx;
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
+    if (m < M) {
+        int b = ty;
+        for (; b + 48 < Bn; b += 64) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p[q] += G[(size_t)(b + 16 * q) * M + m];
+        }
+        for (int q = 0; b < Bn; b += 16, ++q) p[q & 3] += G[(size_t)b * M + m];
+    }
+    red[ty][tx] = (p[0] + p[1]) + (p[2] + p[3]);
+    __syncthreads();
+    if (ty == 0 && m < M) {
+        float s = 0.f;
+        for (int r = 0; r < 16; ++r) s += red[r][tx];
+        out[m] = accumulate ? out[m] + s : s;
+    }
 }
 
 __global__ void gather_rows_kernel(const float* __restrict__ table, const int32_t* __restrict__ idx,
@@ -637,6 +654,9 @@ extern "C" int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s) {
     LDM_REQUIRE((a->epi != LDM_EPI_RESID_SILU && a->epi != LDM_EPI_ADD_R) || a->R, LDM_EINVAL,
                 "epilogue needs R");
     LDM_REQUIRE(a->w_dtype == LDM_F32 || a->w_dtype == LDM_BF16, LDM_EINVAL, "bad w_dtype");
+    LDM_REQUIRE(a->compute == LDM_COMPUTE_FP32 || a->compute == LDM_COMPUTE_BF16, LDM_EINVAL,
+                "bad compute mode %d", a->compute);
+    if (a->compute == LDM_COMPUTE_BF16) return linear_mfma(*a, (hipStream_t)s);
     const bool xk = a->sxk == 1, wk = a->swk == 1;
     if (a->w_dtype == LDM_BF16) launch_tiled<unsigned short>(*a, xk, wk, (hipStream_t)s);
     else launch_tiled<float>(*a, xk, wk, (hipStream_t)s);
@@ -653,7 +673,7 @@ extern "C" int ldm_silu_bwd(const float* dy, const float* a, int n, float* g_out
 extern "C" int ldm_colsum(const float* G, int Bn, int M, float* out, int accumulate,
                           ldm_stream_t s) {
     LDM_REQUIRE(G && out && Bn >= 1 && M >= 1, LDM_EINVAL, "bad colsum args");
-    hipLaunchKernelGGL(colsum_kernel, dim3((M + 255) / 256), dim3(256), 0, (hipStream_t)s, G, Bn, M,
+    hipLaunchKernelGGL(colsum_kernel, dim3((M + 63) / 64), dim3(1024), 0, (hipStream_t)s, G, Bn, M,
                        out, accumulate);
     return launch_status("ldm_colsum");
 }

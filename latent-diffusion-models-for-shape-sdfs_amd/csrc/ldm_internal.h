@@ -59,4 +59,7 @@ int decoder_q_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, i
                   int N, int k0, float vs, float origin, float* out, void* ws, size_t ws_bytes,
                   hipStream_t s, int num_cus);
 
+// matrix-core path of ldm_linear (linear_mfma.hip)
+int linear_mfma(const ldm_linear_args_t& a, hipStream_t s);
+
 }  // namespace ldm

@@ -25,6 +25,8 @@ LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER = 0, 1
 LAYOUT_CODES = {"pass8": LAYOUT_PASS8, "quarter": LAYOUT_QUARTER}
 EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R = 0, 1, 2, 3, 4
+COMPUTE_FP32, COMPUTE_BF16 = 0, 1
+COMPUTE_CODES = {"fp32": COMPUTE_FP32, "bf16": COMPUTE_BF16}
 MAX_BLOCKS = 8
 
 DTYPE_CODES = {"fp32": LDM_F32, "bf16": LDM_BF16, "fp16": LDM_F16}
@@ -64,7 +66,7 @@ class LinearArgs(C.Structure):
                 ("W2", _vp), ("sw2m", C.c_int64), ("sw2k", C.c_int64),
                 ("bias", _vp), ("R", _vp), ("srb", C.c_int64),
                 ("Y", _vp), ("syb", C.c_int64), ("sym", C.c_int64),
-                ("A_out", _vp), ("sab", C.c_int64)]
+                ("A_out", _vp), ("sab", C.c_int64), ("compute", C.c_int32)]
 
 
 CONV_DIRECT, CONV_UP2 = 0, 1

@@ -167,16 +167,20 @@ def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
                grads: Optional[Dict[str, torch.Tensor]] = None,
                group=None) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
     """One DDPM training forward/backward (Alg. 1): q_sample -> eps_hat -> MSE -> grads.
-    Returns (loss [1], grads) -- gradients are averaged over ranks when a group is given."""
+    ``dtype`` "fp32": exact fp32 GEMMs; "bf16": bf16 weights and matrix-core GEMMs with
+    operands rounded to bf16 (fp32 accumulate).  Returns (loss [1], grads) -- gradients are
+    averaged over ranks when a group is given."""
     device = x0.device
     dev = denoiser.device_pack(dtype, device, with_tables=False)
     sd = schedule.device(device)
     xt = ops.q_sample(sd["desc"], x0.contiguous(), eps.contiguous(), t.to(torch.int32).contiguous())
-    eps_hat, sv = ops.denoiser_forward_train(denoiser, dev, xt, t.to(torch.int32).contiguous())
+    cp = capi.COMPUTE_CODES[dtype]
+    eps_hat, sv = ops.denoiser_forward_train(denoiser, dev, xt, t.to(torch.int32).contiguous(),
+                                             compute=cp)
     loss, g_out = ops.eps_mse_loss(eps_hat, eps.contiguous())
     if grads is None:
         grads = {n: torch.empty_like(denoiser.params[n], device=device) for n in denoiser.names()}
-    ops.denoiser_backward_train(denoiser, dev, sv, g_out, grads)
+    ops.denoiser_backward_train(denoiser, dev, sv, g_out, grads, compute=cp)
     ldist.allreduce_mean_([grads[n] for n in denoiser.names()], group=group)
     return loss, grads
 

@@ -168,8 +168,10 @@ def sample_step(desc: capi.Denoiser, sched_desc: capi.Sched, x: torch.Tensor,
 def linear(X: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, *, epi: int = capi.EPI_BIAS,
            bias: Optional[torch.Tensor] = None, X2: Optional[torch.Tensor] = None,
            W2: Optional[torch.Tensor] = None, R: Optional[torch.Tensor] = None,
-           A_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           A_out: Optional[torch.Tensor] = None, compute: int = capi.COMPUTE_FP32) -> torch.Tensor:
     """``Y = epi(X @ W.T [+ X2 @ W2.T] + bias)`` on strided 2-D views (any strides).
+    ``compute``: COMPUTE_FP32 (exact fp32, VALU) or COMPUTE_BF16 (matrix cores, operands
+    rounded to bf16, fp32 accumulate).
 
     X: [Bn, K] view, W: [M, K] view (fp32 or bf16), Y: [Bn, M] view.  Transposed views give
     the backward products, e.g. ``linear(G.T, X.T, dW)`` = ``G^T X``.
@@ -181,6 +183,7 @@ def linear(X: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, *, epi: int = capi
     a = capi.LinearArgs()
     a.Bn, a.M, a.K = Bn, M, K
     a.epi = epi
+    a.compute = compute
     if W.dtype == torch.bfloat16:
         a.w_dtype = capi.LDM_BF16
     elif W.dtype == torch.float32:
@@ -336,14 +339,14 @@ def conv1d(segs, Y: torch.Tensor, **kw) -> torch.Tensor:
 
 # ---------------------------------------------------------------------------------------- A5
 def temb_forward(dev: Dict[str, object], e: torch.Tensor, H: int,
-                 save: Optional[dict] = None) -> torch.Tensor:
+                 save: Optional[dict] = None, compute: int = capi.COMPUTE_FP32) -> torch.Tensor:
     """temb = Wt2 SiLU(Wt1 e + bt1) + bt2 for a batch of embeddings e [Bn, TE]."""
     Bn = e.shape[0]
     u = torch.empty(Bn, H, device=e.device, dtype=torch.float32)
     a_t = torch.empty_like(u) if save is not None else None
-    linear(e, dev["Wt1"], u, epi=capi.EPI_SILU, bias=dev["bt1"], A_out=a_t)
+    linear(e, dev["Wt1"], u, epi=capi.EPI_SILU, bias=dev["bt1"], A_out=a_t, compute=compute)
     temb = torch.empty(Bn, H, device=e.device, dtype=torch.float32)
-    linear(u, dev["Wt2"], temb, epi=capi.EPI_BIAS, bias=dev["bt2"])
+    linear(u, dev["Wt2"], temb, epi=capi.EPI_BIAS, bias=dev["bt2"], compute=compute)
     if save is not None:
         save.update(e=e, u=u, a_t=a_t, temb=temb)
     return temb
@@ -365,63 +368,67 @@ def build_e_tables(model, dev: Dict[str, object], dtype: str) -> List[torch.Tens
 
 # ---------------------------------------------------------------------------------------- A6/A7
 def denoiser_forward_train(model, dev: Dict[str, object], xt: torch.Tensor,
-                           t: torch.Tensor) -> Tuple[torch.Tensor, dict]:
+                           t: torch.Tensor, compute: int = capi.COMPUTE_FP32
+                           ) -> Tuple[torch.Tensor, dict]:
     """Training forward (per-sample t) saving what the backward needs."""
     H, nb = model.H, model.n_blocks
     Bn = xt.shape[0]
+    cp = compute
     sv: dict = {"xt": xt}
     e = gather_rows(dev["emb_table"], t)
-    temb = temb_forward(dev, e, H, save=sv)
+    temb = temb_forward(dev, e, H, save=sv, compute=cp)
     h = torch.empty(Bn, H, device=xt.device, dtype=torch.float32)
-    linear(xt, dev["Win"], h, epi=capi.EPI_BIAS, bias=dev["bin"])
+    linear(xt, dev["Win"], h, epi=capi.EPI_BIAS, bias=dev["bin"], compute=cp)
     hs, pre = [h], []
     for k in range(nb):
         W = dev[f"Wblk{k}"]
         a = torch.empty(Bn, H, device=xt.device, dtype=torch.float32)
         hn = torch.empty(Bn, H, device=xt.device, dtype=torch.float32)
         linear(h, W[:, :H], hn, epi=capi.EPI_RESID_SILU, bias=dev[f"bblk{k}"], X2=temb,
-               W2=W[:, H:], R=h, A_out=a)
+               W2=W[:, H:], R=h, A_out=a, compute=cp)
         hs.append(hn)
         pre.append(a)
         h = hn
     eps_hat = torch.empty(Bn, model.D, device=xt.device, dtype=torch.float32)
-    linear(h, dev["Wout"], eps_hat, epi=capi.EPI_BIAS, bias=dev["bout"])
+    linear(h, dev["Wout"], eps_hat, epi=capi.EPI_BIAS, bias=dev["bout"], compute=cp)
     sv.update(hs=hs, pre=pre)
     return eps_hat, sv
 
 
 def denoiser_backward_train(model, dev: Dict[str, object], sv: dict,
-                            g_out: torch.Tensor, grads: Dict[str, torch.Tensor]) -> None:
+                            g_out: torch.Tensor, grads: Dict[str, torch.Tensor],
+                            compute: int = capi.COMPUTE_FP32) -> None:
     """A7: gradients of every parameter given dL/d eps_hat (written into ``grads``)."""
     H, nb = model.H, model.n_blocks
+    cp = compute
     Bn = g_out.shape[0]
     hs, pre = sv["hs"], sv["pre"]
     # eps_hat = Wout h + bout
-    linear(g_out.T, hs[-1].T, grads["Wout"])
+    linear(g_out.T, hs[-1].T, grads["Wout"], compute=cp)
     colsum(g_out, grads["bout"])
     dh = torch.empty(Bn, H, device=g_out.device, dtype=torch.float32)
-    linear(g_out, dev["Wout"].T, dh)
+    linear(g_out, dev["Wout"].T, dh, compute=cp)
     dtemb = torch.zeros(Bn, H, device=g_out.device, dtype=torch.float32)
     g = torch.empty_like(dh)
     for k in range(nb - 1, -1, -1):
         W = dev[f"Wblk{k}"]
         silu_bwd(dh, pre[k], out=g)                                  # g = dh * silu'(a)
         dW = grads[f"Wblk{k}"]
-        linear(g.T, hs[k].T, dW[:, :H])                              # dW_k = g^T h_k
-        linear(g.T, sv["temb"].T, dW[:, H:])                         # dU_k = g^T temb
+        linear(g.T, hs[k].T, dW[:, :H], compute=cp)                  # dW_k = g^T h_k
+        linear(g.T, sv["temb"].T, dW[:, H:], compute=cp)             # dU_k = g^T temb
         colsum(g, grads[f"bblk{k}"])
-        linear(g, W[:, H:].T, dtemb, epi=capi.EPI_ACCUM)             # dtemb += g U_k
+        linear(g, W[:, H:].T, dtemb, epi=capi.EPI_ACCUM, compute=cp)  # dtemb += g U_k
         dh_new = torch.empty_like(dh)
-        linear(g, W[:, :H].T, dh_new, epi=capi.EPI_ADD_R, R=dh)      # dh = dh + g W_k
+        linear(g, W[:, :H].T, dh_new, epi=capi.EPI_ADD_R, R=dh, compute=cp)  # dh += g W_k
         dh = dh_new
     # h0 = Win xt + bin
-    linear(dh.T, sv["xt"].T, grads["Win"])
+    linear(dh.T, sv["xt"].T, grads["Win"], compute=cp)
     colsum(dh, grads["bin"])
     # temb = Wt2 u + bt2 ; u = silu(a_t) ; a_t = Wt1 e + bt1
-    linear(dtemb.T, sv["u"].T, grads["Wt2"])
+    linear(dtemb.T, sv["u"].T, grads["Wt2"], compute=cp)
     colsum(dtemb, grads["bt2"])
     du = torch.empty(Bn, H, device=g_out.device, dtype=torch.float32)
-    linear(dtemb, dev["Wt2"].T, du)
+    linear(dtemb, dev["Wt2"].T, du, compute=cp)
     gt = silu_bwd(du, sv["a_t"])
-    linear(gt.T, sv["e"].T, grads["Wt1"])
+    linear(gt.T, sv["e"].T, grads["Wt1"], compute=cp)
     colsum(gt, grads["bt1"])

@@ -168,3 +168,68 @@ def test_train_step_grads_vs_golden(dev, den):
         got = v.cpu().double().numpy()
         got = got if k.startswith("b") else got[:8]
         assert np.abs(got - want).max() <= 1e-4 * np.abs(want).max() + 1e-9, k
+
+
+def _bf(t):
+    """The bf16 rounding the matrix-core path applies to an operand (RNE), back in fp64."""
+    return t.float().bfloat16().double()
+
+
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Bn,M,K,K2", [(1000, 1024, 1024, 1024), (37, 100, 70, 0),
+                                       (64, 256, 256, 128), (1, 8, 16, 0), (129, 65, 200, 3)])
+def test_linear_bf16_mfma(dev, wdt, Bn, M, K, K2):
+    """compute=BF16 (linear_mfma.hip): equals the fp64 product of the bf16-ROUNDED operands up
+    to fp32 accumulation, for the forward, G^T X and G W forms and the epilogues."""
+    from ldm_sdf import ops, _capi as capi
+    BF = capi.COMPUTE_BF16
+    g = torch.Generator().manual_seed(Bn * 7 + M)
+    X = torch.randn(Bn, K, generator=g).to(dev)
+    W = torch.randn(M, K, generator=g).to(dev).to(wdt)
+    b = torch.randn(M, generator=g).to(dev)
+    Y = torch.empty(Bn, M, device=dev)
+    kw = {}
+    ref = _bf(X) @ _bf(W).T + b.double()
+    if K2:
+        X2 = torch.randn(Bn, K2, generator=g).to(dev)
+        W2 = torch.randn(M, K2, generator=g).to(dev).to(wdt)
+        kw = dict(X2=X2, W2=W2)
+        ref = ref + _bf(X2) @ _bf(W2).T
+    tol = 2e-6 * (K + K2) ** 0.5 * 4
+    ops.linear(X, W, Y, bias=b, compute=BF, **kw)
+    assert (Y.double() - ref).abs().max() < tol
+    G = torch.randn(Bn, M, generator=g).to(dev)
+    dW = torch.empty(M, K, device=dev)
+    ops.linear(G.T, X.T, dW, compute=BF)
+    assert (dW.double() - _bf(G).T @ _bf(X)).abs().max() < 8e-6 * Bn ** 0.5
+    dX = torch.empty(Bn, K, device=dev)
+    ops.linear(G, W.T, dX, compute=BF)
+    assert (dX.double() - _bf(G) @ _bf(W)).abs().max() < 8e-6 * M ** 0.5
+    R_ = torch.randn(Bn, M, generator=g).to(dev)
+    A = torch.empty(Bn, M, device=dev)
+    ops.linear(X, W, Y, epi=capi.EPI_RESID_SILU, bias=b, R=R_, A_out=A, compute=BF, **kw)
+    assert (A.double() - ref).abs().max() < tol
+    assert (Y.double() - (R_.double() + ref * torch.sigmoid(ref))).abs().max() < 2 * tol
+
+
+def test_train_step_bf16_grads_close_to_fp64(dev, den):
+    """Mixed-precision training step (bf16 weights, matrix-core GEMMs) vs the fp64 oracle's
+    autograd: loss within 1e-3 relative, every gradient's norm within 2 %, direction cosine
+    >= 0.999 (bf16 operand rounding; the fp32 path is pinned to 1e-4 above)."""
+    import ldm_sdf
+    model, _ = den
+    g = dict(np.load(os.path.join(GOLD, "train_step.npz")))
+    model.to_device(dev)
+    loss, grads = ldm_sdf.train_step(model, ldm_sdf.DDPMSchedule(),
+                                     torch.from_numpy(g["x0"]).to(dev),
+                                     torch.from_numpy(g["t"]).to(dev),
+                                     torch.from_numpy(g["eps"]).to(dev), dtype="bf16")
+    assert abs(float(loss) - float(g["loss"])) / float(g["loss"]) < 1e-3
+    for k, v in grads.items():
+        want_norm = float(g["gnorm_" + k])
+        assert abs(float(v.double().norm()) - want_norm) <= 2e-2 * want_norm + 1e-9, k
+        want = torch.from_numpy(g["g_" + k]).double().flatten()
+        got = v.cpu().double()
+        got = (got if k.startswith("b") else got[:8]).flatten()
+        cos = float(got @ want / (got.norm() * want.norm() + 1e-30))
+        assert cos >= 0.999, (k, cos)
