@@ -36,32 +36,92 @@ __device__ __forceinline__ float ld_elem(const T* p, int64_t i) {
 }
 
 // One operand tile: rows [r0, r0+64) x k [k0, k0+64) of a strided matrix, 16 values per
-// thread held in registers between the load and the LDS store.
-template <typename T, bool KC>
+// thread held in registers between the load and the LDS store.  VEC: 16-byte vector loads
+// along the contiguous dimension (requires its stride 1, the other stride and the base
+// 16-byte aligned, and the contiguous extent a multiple of the vector); lanes of a wave then
+// cover whole 256-byte (fp32) / 128-byte (bf16) row segments.  Otherwise scalar loads.
+template <typename T, bool KC, bool VEC>
 struct Tile {
+    static constexpr int EPV = 16 / sizeof(T);        // elements per 16-byte vector
+    static constexpr int VPR = 64 / EPV;              // vectors per 64-element line
+    static constexpr int NV = 64 * VPR / 256;         // vectors per thread (4 fp32, 2 bf16)
     float v[16];
     __device__ __forceinline__ void load(const T* __restrict__ P, int64_t sr, int64_t sk,
                                          int rows, int K, int r0, int k0) {
         const int t = threadIdx.x;
-        if (KC) {   // contiguous along k: thread -> (row t/4, k 16*(t%4) .. +15)
+        if constexpr (VEC) {
+#pragma unroll
+            for (int u = 0; u < NV; ++u) {
+                const int id = u * 256 + t;
+                const int line = id / VPR, e = (id % VPR) * EPV;    // line = row (KC) or k
+                const int r = KC ? r0 + line : r0 + e, k = KC ? k0 + e : k0 + line;
+                // branch-free: a conditional load makes hipcc wait vmcnt(0) per element
+                const bool ok = r < rows && k < K;
+                const int64_t gi = ok ? (int64_t)r * sr + (int64_t)k * sk : 0;
+                u32x4 w = *reinterpret_cast<const u32x4*>(P + gi);
+                if (!ok) w = u32x4{0u, 0u, 0u, 0u};
+                // copy each element out first: __builtin_bit_cast of an ext-vector element
+                // lvalue (w[q]) reads element 0 whatever q is
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned wq = w[q];
+                    if constexpr (sizeof(T) == 2) {
+                        v[u * 8 + 2 * q] = __builtin_bit_cast(float, wq << 16);
+                        v[u * 8 + 2 * q + 1] = __builtin_bit_cast(float, wq & 0xffff0000u);
+                    } else {
+                        v[u * 4 + q] = __builtin_bit_cast(float, wq);
+                    }
+                }
+            }
+        } else if (KC) {   // contiguous along k: thread -> (row t/4, k 16*(t%4) .. +15)
             const int r = r0 + (t >> 2), kb = k0 + (t & 3) * 16;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int k = kb + j;
-                v[j] = (r < rows && k < K) ? ld_elem(P, (int64_t)r * sr + (int64_t)k * sk) : 0.f;
+                const bool ok = r < rows && k < K;
+                const float x = ld_elem(P, ok ? (int64_t)r * sr + (int64_t)k * sk : 0);
+                v[j] = ok ? x : 0.f;
             }
         } else {    // contiguous along rows: thread -> (k t/4, rows 16*(t%4) .. +15)
             const int k = k0 + (t >> 2), rb = r0 + (t & 3) * 16;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int r = rb + j;
-                v[j] = (r < rows && k < K) ? ld_elem(P, (int64_t)r * sr + (int64_t)k * sk) : 0.f;
+                const bool ok = r < rows && k < K;
+                const float x = ld_elem(P, ok ? (int64_t)r * sr + (int64_t)k * sk : 0);
+                v[j] = ok ? x : 0.f;
             }
         }
     }
     __device__ __forceinline__ void store(unsigned short* __restrict__ S) const {
         const int t = threadIdx.x;
-        if (KC) {
+        if constexpr (VEC) {
+#pragma unroll
+            for (int u = 0; u < NV; ++u) {
+                const int id = u * 256 + t;
+                const int line = id / VPR, e = (id % VPR) * EPV;
+                const float* x = v + u * EPV;
+                if (KC) {        // EPV consecutive k of one row -> one 8- or 16-byte store
+                    if constexpr (EPV == 8) {
+                        u32x4 w;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) w[q] = pack_bf16(x[2 * q], x[2 * q + 1]);
+                        *reinterpret_cast<u32x4*>(S + line * kLd + e) = w;
+                    } else {
+                        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                        const u32x2 w = {pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3])};
+                        *reinterpret_cast<u32x2*>(S + line * kLd + e) = w;
+                    }
+                } else {         // EPV consecutive rows of one k -> scattered 2-byte stores
+#pragma unroll
+                    for (int q = 0; q < EPV; q += 2) {
+                        const unsigned p = pack_bf16(x[q], x[q + 1]);
+                        S[(e + q) * kLd + line] = (unsigned short)(p & 0xffffu);
+                        S[(e + q + 1) * kLd + line] = (unsigned short)(p >> 16);
+                    }
+                }
+            }
+        } else if (KC) {
             const int r = t >> 2, kb = (t & 3) * 16;
             u32x4 w0, w1;
 #pragma unroll
@@ -83,57 +143,61 @@ struct Tile {
     }
 };
 
-template <typename TW, bool XK, bool WK>
+template <typename TW, bool XK, bool WK, bool XV, bool WV>
 __device__ __forceinline__ void mfma_segment(f32x16& acc, unsigned short* __restrict__ sm,
                                              const float* X, int64_t sxb, int64_t sxk,
                                              const void* Wv, int64_t swm, int64_t swk, int K,
                                              int Bn, int M, int b0, int m0) {
     const TW* W = reinterpret_cast<const TW*>(Wv);
-    unsigned short* Xs[2] = {sm, sm + 64 * kLd};
-    unsigned short* Ws[2] = {sm + 2 * 64 * kLd, sm + 3 * 64 * kLd};
+    // buffers addressed as sm + offset (not through a pointer array, which loses the LDS
+    // address space and turns the fragment reads into flat loads): X0 X1 W0 W1
+    constexpr int kBuf = 64 * kLd;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const int r = lane & 31, h = lane >> 5;
-    Tile<float, XK> tx;
-    Tile<TW, WK> tw;
+    Tile<float, XK, XV> tx;
+    Tile<TW, WK, WV> tw;
     const int nk = (K + kKC - 1) / kKC;
     tx.load(X, sxb, sxk, Bn, K, b0, 0);
     tw.load(W, swm, swk, M, K, m0, 0);
-    tx.store(Xs[0]);
-    tw.store(Ws[0]);
+    tx.store(sm);
+    tw.store(sm + 2 * kBuf);
     __syncthreads();
     for (int kc = 0; kc < nk; ++kc) {
-        const int cur = kc & 1;
+        const int cur = (kc & 1) * kBuf, nxt = kBuf - cur;
         if (kc + 1 < nk) {
             tx.load(X, sxb, sxk, Bn, K, b0, (kc + 1) * kKC);
             tw.load(W, swm, swk, M, K, m0, (kc + 1) * kKC);
         }
+        const unsigned short* xa = sm + cur + (wr + r) * kLd + 8 * h;
+        const unsigned short* wb = sm + 2 * kBuf + cur + (wc + r) * kLd + 8 * h;
 #pragma unroll
         for (int ks = 0; ks < kKC / 16; ++ks) {
-            const u32x4 af = *reinterpret_cast<const u32x4*>(Xs[cur] + (wr + r) * kLd + ks * 16 + 8 * h);
-            const u32x4 bf = *reinterpret_cast<const u32x4*>(Ws[cur] + (wc + r) * kLd + ks * 16 + 8 * h);
+            const u32x4 af = *reinterpret_cast<const u32x4*>(xa + ks * 16);
+            const u32x4 bf = *reinterpret_cast<const u32x4*>(wb + ks * 16);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af),
                                                           __builtin_bit_cast(bf16x8, bf), acc, 0,
                                                           0, 0);
         }
         if (kc + 1 < nk) {
-            tx.store(Xs[cur ^ 1]);
-            tw.store(Ws[cur ^ 1]);
+            tx.store(sm + nxt);
+            tw.store(sm + 2 * kBuf + nxt);
         }
         __syncthreads();
     }
 }
 
-template <typename TW, bool XK, bool WK>
+template <typename TW, bool XK, bool WK, bool XV, bool WV>
 __global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a) {
     __shared__ __attribute__((aligned(16))) unsigned short sm[4 * 64 * kLd];
     const int b0 = blockIdx.y * 64, m0 = blockIdx.x * 64;
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    mfma_segment<TW, XK, WK>(acc, sm, a.X, a.sxb, a.sxk, a.W, a.swm, a.swk, a.K, a.Bn, a.M, b0, m0);
+    mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X, a.sxb, a.sxk, a.W, a.swm, a.swk, a.K, a.Bn,
+                                     a.M, b0, m0);
     if (a.K2 > 0)
-        mfma_segment<TW, XK, WK>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k, a.K2, a.Bn,
+        mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k, a.K2, a.Bn,
                                  a.M, b0, m0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = m0 + (wave & 1) * 32 + (lane & 31);
@@ -161,13 +225,43 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a) {
     }
 }
 
+// Can an operand use 16-byte vector loads?  Its contiguous dimension must have stride 1 and
+// an extent that is a multiple of the vector, the other stride and the base 16-byte aligned.
+bool vec_ok(const void* P, int64_t s_row, int64_t s_k, int rows, int K, int esize) {
+    const int epv = 16 / esize;
+    const bool kc = s_k == 1;
+    const int64_t other = kc ? s_row : s_k;
+    const int ext = kc ? K : rows;
+    return (kc || s_row == 1) && (((uintptr_t)P) & 15) == 0 && other % epv == 0 &&
+           ext % epv == 0;
+}
+
+template <typename TW, bool XK, bool WK>
+void launch_mfma3(const ldm_linear_args_t& a, bool xv, bool wv, hipStream_t s) {
+    const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64);
+    if (xv && wv) hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, true, true>), grid, dim3(256), 0, s, a);
+    else if (xv) hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, true, false>), grid, dim3(256), 0, s, a);
+    else if (wv) hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, false, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, false, false>), grid, dim3(256), 0, s, a);
+}
+
 template <typename TW>
 void launch_mfma(const ldm_linear_args_t& a, bool xk, bool wk, hipStream_t s) {
-    const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64);
-    if (xk && wk) hipLaunchKernelGGL((linear_mfma_kernel<TW, true, true>), grid, dim3(256), 0, s, a);
-    else if (xk) hipLaunchKernelGGL((linear_mfma_kernel<TW, true, false>), grid, dim3(256), 0, s, a);
-    else if (wk) hipLaunchKernelGGL((linear_mfma_kernel<TW, false, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((linear_mfma_kernel<TW, false, false>), grid, dim3(256), 0, s, a);
+    const int es = (int)sizeof(TW);
+    static const bool vec_on = [] {      // development A/B knob: LDM_LINEAR_VEC=0 -> scalar tiles
+        const char* e = getenv("LDM_LINEAR_VEC");
+        return !(e && e[0] == '0');
+    }();
+    bool xv = vec_on && vec_ok(a.X, a.sxb, a.sxk, a.Bn, a.K, 4);
+    bool wv = vec_on && vec_ok(a.W, a.swm, a.swk, a.M, a.K, es);
+    if (a.K2 > 0) {
+        xv = xv && vec_ok(a.X2, a.sx2b, a.sx2k, a.Bn, a.K2, 4);
+        wv = wv && vec_ok(a.W2, a.sw2m, a.sw2k, a.M, a.K2, es);
+    }
+    if (xk && wk) launch_mfma3<TW, true, true>(a, xv, wv, s);
+    else if (xk) launch_mfma3<TW, true, false>(a, xv, wv, s);
+    else if (wk) launch_mfma3<TW, false, true>(a, xv, wv, s);
+    else launch_mfma3<TW, false, false>(a, xv, wv, s);
 }
 
 }  // namespace
