@@ -43,14 +43,47 @@ __global__ void q_sample_kernel(const float* __restrict__ sab, const float* __re
     xt[i] = a + b;
 }
 
+// One block, fixed summation order (deterministic).  The loads of U groups are issued before
+// any is consumed (index clamped, use predicated) so the block pays one memory round trip per
+// U x 1024 groups instead of one per group.  V4: groups of 4 via 16-byte loads (all pointers
+// 16-byte aligned), the n % 4 tail scalar.
+template <bool V4>
 __global__ __launch_bounds__(1024) void mse_loss_kernel(const float* __restrict__ eh,
                                                         const float* __restrict__ e, int n,
                                                         float* __restrict__ loss,
                                                         float* __restrict__ grad) {
     __shared__ float red[1024];
+    constexpr int U = 8;
+    constexpr int G = V4 ? 4 : 1;
+    typedef float vec_t __attribute__((ext_vector_type(G)));
     float s = 0.f;
     const float g = 2.f / (float)n;
-    for (int i = threadIdx.x; i < n; i += 1024) {
+    const int ng = n / G;
+    const vec_t* A = reinterpret_cast<const vec_t*>(eh);
+    const vec_t* Bv = reinterpret_cast<const vec_t*>(e);
+    const int tid = (int)threadIdx.x;
+    for (int base = 0; base < ng; base += 1024 * U) {
+        vec_t a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * 1024 + tid;
+            const int ii = i < ng ? i : 0;
+            a[u] = A[ii];
+            b[u] = Bv[ii];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * 1024 + tid;
+            if (i < ng) {
+                const vec_t d = a[u] - b[u];
+#pragma unroll
+                for (int q = 0; q < G; ++q) s = fmaf(d[q], d[q], s);
+                if (grad) reinterpret_cast<vec_t*>(grad)[i] = g * d;
+            }
+        }
+    }
+    if (tid < n - ng * G) {
+        const int i = ng * G + tid;
         const float d = eh[i] - e[i];
         s = fmaf(d, d, s);
         if (grad) grad[i] = g * d;
@@ -354,6 +387,130 @@ __global__ __launch_bounds__(256) void small_linear_v3(SmallArgs a) {
     }
 }
 
+// v4: v3 with every global load unconditional (index clamped, value selected afterwards) so a
+// wave issues all of its loads back to back -- a load under a divergent branch makes hipcc
+// wait vmcnt(0) before leaving the branch, one round trip per load -- and the activation
+// staging batched 8 x 16 B per thread before any LDS store.  NJ = ceil(K / 8 / 64) weight
+// chunks per lane (K <= 2048).
+template <typename TW, int EPI, int MB, int NJ>
+__global__ __launch_bounds__(256) void small_linear_v4(SmallArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];   // [B][K]
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int mm = m < a.M ? m : a.M - 1;
+    const int nch = a.K >> 3;
+    float w[NJ][8];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        const bool on = c < nch;
+        const size_t off = (size_t)mm * a.ldw + (on ? c : 0) * 8;
+        if constexpr (sizeof(TW) == 2) {
+            uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const unsigned short*>(a.W) + off);
+            const unsigned q[4] = {on ? u.x : 0u, on ? u.y : 0u, on ? u.z : 0u, on ? u.w : 0u};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[j][2 * i] = __builtin_bit_cast(float, q[i] << 16);
+                w[j][2 * i + 1] = __builtin_bit_cast(float, q[i] & 0xffff0000u);
+            }
+        } else {
+            const float* wp = reinterpret_cast<const float*>(a.W) + off;
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(wp);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(wp + 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[j][i] = on ? w0[i] : 0.f;
+                w[j][4 + i] = on ? w1[i] : 0.f;
+            }
+        }
+    }
+    const int n4 = (a.B * a.K) >> 2;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(a.X);
+    for (int base = 0; base < n4; base += 256 * 8) {
+        f32x4 t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 256 + (int)threadIdx.x;
+            t[u] = X4[i < n4 ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 256 + (int)threadIdx.x;
+            if (i < n4) reinterpret_cast<f32x4*>(xs)[i] = t[u];
+        }
+    }
+    __syncthreads();
+    float acc[MB];
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[b] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        const int cc = c < nch ? c : 0;       // off lanes: zero weights times a valid row
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+            const int bb = b < a.B ? b : 0;   // rows past B are never written out
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(xs + bb * a.K + cc * 8);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(xs + bb * a.K + cc * 8 + 4);
+            float t = acc[b];
+            t = fmaf(w[j][0], x0[0], t); t = fmaf(w[j][1], x0[1], t);
+            t = fmaf(w[j][2], x0[2], t); t = fmaf(w[j][3], x0[3], t);
+            t = fmaf(w[j][4], x1[0], t); t = fmaf(w[j][5], x1[1], t);
+            t = fmaf(w[j][6], x1[2], t); t = fmaf(w[j][7], x1[3], t);
+            acc[b] = t;
+        }
+    }
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        const int o = 32 >> lv;
+        const int n = MB >> lv;
+        const bool upper = (lane & o) != 0;
+        if (n > 1) {
+            const int half = n >> 1;
+#pragma unroll
+            for (int i = 0; i < half; ++i) {
+                const float send = upper ? acc[i] : acc[i + half];
+                const float keep = upper ? acc[i + half] : acc[i];
+                acc[i] = keep + __shfl_xor(send, o);
+            }
+        } else {
+            acc[0] += __shfl_xor(acc[0], o);
+        }
+    }
+    constexpr int LB = (MB >= 16) ? 4 : 3;
+    const int b = lane >> (6 - LB);
+    const bool writer = (lane & ((1 << (6 - LB)) - 1)) == 0;
+    if (m < a.M && writer && b < a.B) {
+        const float pre = acc[0] + a.bias[m];
+        const size_t i = (size_t)b * a.M + m;
+        if (EPI == SE_BIAS) {
+            a.Y[i] = pre;
+        } else if (EPI == SE_BLOCK) {
+            a.Y[i] = xs[b * a.K + m] + silu(pre);
+        } else {
+            const bool noise = a.t > 0;
+            a.Y[i] = ddpm_update(a.xlat[i], pre, noise ? a.z[i] : 0.f, a.c1t[a.t], a.c2t[a.t],
+                                 a.sgt[a.t], noise);
+        }
+    }
+}
+
+template <typename TW, int EPI, int MB>
+void launch_small_v4_nj(const SmallArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)a.B * a.K * sizeof(float);
+    const dim3 grid((a.M + 3) / 4);
+    const int nj = ((a.K >> 3) + 63) / 64;
+    if (nj <= 1) hipLaunchKernelGGL((small_linear_v4<TW, EPI, MB, 1>), grid, dim3(256), lds, s, a);
+    else if (nj <= 2) hipLaunchKernelGGL((small_linear_v4<TW, EPI, MB, 2>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((small_linear_v4<TW, EPI, MB, 4>), grid, dim3(256), lds, s, a);
+}
+
+template <typename TW, int EPI>
+void launch_small_v4(const SmallArgs& a, hipStream_t s) {
+    if (a.B <= 8) launch_small_v4_nj<TW, EPI, 8>(a, s);
+    else launch_small_v4_nj<TW, EPI, 16>(a, s);
+}
+
 template <typename TW, int EPI>
 void launch_small_v3(const SmallArgs& a, hipStream_t s) {
     const size_t lds = (size_t)a.B * a.K * sizeof(float);
@@ -365,8 +522,8 @@ void launch_small_v3(const SmallArgs& a, hipStream_t s) {
 }
 
 int small_version() {
-    const char* e = getenv("LDM_SMALL_LINEAR");   // development A/B knob: 1, 2, 3 (default)
-    return (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 3;
+    const char* e = getenv("LDM_SMALL_LINEAR");   // development A/B knob: 1, 2, 3, 4 (default)
+    return (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 4;
 }
 
 template <typename TW, int EPI>
@@ -386,6 +543,11 @@ int launch_small(const SmallArgs& a, int w_dtype, hipStream_t s) {
         if (w_dtype == LDM_BF16) launch_small_v2<unsigned short, EPI>(a, s);
         else launch_small_v2<float, EPI>(a, s);
         return launch_status("small_linear_v2");
+    }
+    if (ver == 4) {
+        if (w_dtype == LDM_BF16) launch_small_v4<unsigned short, EPI>(a, s);
+        else launch_small_v4<float, EPI>(a, s);
+        return launch_status("small_linear_v4");
     }
     if (ver == 3) {
         if (w_dtype == LDM_BF16) launch_small_v3<unsigned short, EPI>(a, s);
@@ -555,6 +717,8 @@ int check_denoiser(const ldm_denoiser_t* w, int B) {
                 kSmallMaxB);
     LDM_REQUIRE(w->n_blocks >= 1 && w->n_blocks <= LDM_MAX_BLOCKS, LDM_EINVAL, "bad n_blocks");
     LDM_REQUIRE(w->D % 8 == 0 && w->H % 8 == 0, LDM_EINVAL, "D and H must be multiples of 8");
+    LDM_REQUIRE(w->D <= 2048 && w->H <= 2048, LDM_ENOSYS,
+                "D and H must be <= 2048 for the sampling GEMV (8 k per lane, 4 chunks)");
     LDM_REQUIRE((size_t)B * (w->H > w->D ? w->H : w->D) * 4 <= 64 * 1024, LDM_ENOSYS,
                 "B*H too large for the LDS-staged sampling kernel");
     return 0;
@@ -607,8 +771,13 @@ extern "C" int ldm_q_sample(const ldm_sched_t* sc, const float* x0, const float*
 extern "C" int ldm_eps_mse_loss(const float* eps_hat, const float* eps, int n, float* loss_out,
                                 float* grad_out, ldm_stream_t s) {
     LDM_REQUIRE(eps_hat && eps && loss_out && n >= 1, LDM_EINVAL, "bad loss args");
-    hipLaunchKernelGGL(mse_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, eps_hat, eps, n,
-                       loss_out, grad_out);
+    const bool v4 = LDM_ALIGNED(eps_hat, 16) && LDM_ALIGNED(eps, 16) && LDM_ALIGNED(grad_out, 16);
+    if (v4)
+        hipLaunchKernelGGL(mse_loss_kernel<true>, dim3(1), dim3(1024), 0, (hipStream_t)s, eps_hat,
+                           eps, n, loss_out, grad_out);
+    else
+        hipLaunchKernelGGL(mse_loss_kernel<false>, dim3(1), dim3(1024), 0, (hipStream_t)s, eps_hat,
+                           eps, n, loss_out, grad_out);
     return launch_status("ldm_eps_mse_loss");
 }
 

@@ -8,20 +8,25 @@
 // exact path (compute = LDM_COMPUTE_FP32) that the fp64 gradient parity test pins.
 //
 // Tiling: a workgroup (4 waves) owns a 64 (rows b) x 64 (cols m) tile, each wave a 32 x 32
-// MFMA tile.  K advances in 64-wide chunks through two LDS buffers: the next chunk's global
-// loads are issued into registers before the current chunk's MFMAs (one barrier per chunk).
-// An operand contiguous along k is loaded 8 k per thread (one 16-byte LDS store); a
-// transposed view (contiguous along rows) is loaded 8 rows per thread and scattered.
-// LDS rows are 64 + 8 bf16 (144 B), so the 16-byte fragment reads of a 16-lane group land
-// in distinct banks.
+// MFMA tile.  K advances in 128-deep chunks through two LDS buffers per operand: the next
+// chunk's global loads are issued into registers before the current chunk's MFMAs (one barrier
+// per chunk).  At the training shapes (1000 x 1024 x 1024..2048, 256 workgroups = one per CU)
+// the kernel is bound by that chain of per-chunk load latencies, so the chunk is deep: 128
+// halves the chain of the first 64-deep version.  Operand tiles load with 16-byte vectors along
+// the contiguous dimension when strides and alignment allow (vec_ok), else element-wise; every
+// load is unconditional (clamped index, value selected) so a wave keeps them all in flight.
+// LDS rows are 128 + 8 bf16 (272 B): the 16-byte fragment reads of 16 consecutive rows land
+// 4 banks apart, conflict-free.
 #include "ldm_internal.h"
 #include "ddpm_common.h"
 
 namespace ldm {
 namespace {
 
-constexpr int kKC = 64;              // k per chunk
+constexpr int kKC = 128;             // k per chunk
 constexpr int kLd = kKC + 8;         // LDS row pitch (bf16 elements)
+constexpr int kBuf = 64 * kLd;       // one operand buffer (elements)
+constexpr int kLdsBytes = 4 * kBuf * (int)sizeof(unsigned short);   // X0 X1 W0 W1 = 68 KiB
 
 __device__ __forceinline__ unsigned pack_bf16(float a, float b) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -35,17 +40,23 @@ __device__ __forceinline__ float ld_elem(const T* p, int64_t i) {
     else return p[i];
 }
 
-// One operand tile: rows [r0, r0+64) x k [k0, k0+64) of a strided matrix, 16 values per
-// thread held in registers between the load and the LDS store.  VEC: 16-byte vector loads
-// along the contiguous dimension (requires its stride 1, the other stride and the base
-// 16-byte aligned, and the contiguous extent a multiple of the vector); lanes of a wave then
-// cover whole 256-byte (fp32) / 128-byte (bf16) row segments.  Otherwise scalar loads.
+// One operand tile: rows [r0, r0+64) x k [k0, k0+kKC) of a strided matrix, E values per thread
+// held in registers between the load and the LDS store.  A "line" is a run along the
+// contiguous dimension: a row (KC, contiguous along k) or a k column (rows contiguous).
+// VEC: 16-byte vector loads along the line (its stride 1, the other stride and the base
+// 16-byte aligned, the line extent a multiple of the vector); lanes of a wave then cover whole
+// 256-byte (fp32) / 128-byte (bf16) segments.  Otherwise TPL threads per line, E consecutive
+// elements each.
 template <typename T, bool KC, bool VEC>
 struct Tile {
+    static constexpr int E = 64 * kKC / 256;          // values per thread
     static constexpr int EPV = 16 / sizeof(T);        // elements per 16-byte vector
-    static constexpr int VPR = 64 / EPV;              // vectors per 64-element line
-    static constexpr int NV = 64 * VPR / 256;         // vectors per thread (4 fp32, 2 bf16)
-    float v[16];
+    static constexpr int LEN = KC ? kKC : 64;         // line length
+    static constexpr int VPL = LEN / EPV;             // vectors per line
+    static constexpr int NV = E / EPV;                // vectors per thread
+    static constexpr int TPL = LEN / E;               // scalar path: threads per line
+    float v[E];
+
     __device__ __forceinline__ void load(const T* __restrict__ P, int64_t sr, int64_t sk,
                                          int rows, int K, int r0, int k0) {
         const int t = threadIdx.x;
@@ -53,9 +64,8 @@ struct Tile {
 #pragma unroll
             for (int u = 0; u < NV; ++u) {
                 const int id = u * 256 + t;
-                const int line = id / VPR, e = (id % VPR) * EPV;    // line = row (KC) or k
+                const int line = id / VPL, e = (id % VPL) * EPV;
                 const int r = KC ? r0 + line : r0 + e, k = KC ? k0 + e : k0 + line;
-                // branch-free: a conditional load makes hipcc wait vmcnt(0) per element
                 const bool ok = r < rows && k < K;
                 const int64_t gi = ok ? (int64_t)r * sr + (int64_t)k * sk : 0;
                 u32x4 w = *reinterpret_cast<const u32x4*>(P + gi);
@@ -73,35 +83,28 @@ struct Tile {
                     }
                 }
             }
-        } else if (KC) {   // contiguous along k: thread -> (row t/4, k 16*(t%4) .. +15)
-            const int r = r0 + (t >> 2), kb = k0 + (t & 3) * 16;
+        } else {
+            const int line = t / TPL, eb = (t % TPL) * E;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int k = kb + j;
-                const bool ok = r < rows && k < K;
-                const float x = ld_elem(P, ok ? (int64_t)r * sr + (int64_t)k * sk : 0);
-                v[j] = ok ? x : 0.f;
-            }
-        } else {    // contiguous along rows: thread -> (k t/4, rows 16*(t%4) .. +15)
-            const int k = k0 + (t >> 2), rb = r0 + (t & 3) * 16;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int r = rb + j;
+            for (int j = 0; j < E; ++j) {
+                const int r = KC ? r0 + line : r0 + eb + j, k = KC ? k0 + eb + j : k0 + line;
                 const bool ok = r < rows && k < K;
                 const float x = ld_elem(P, ok ? (int64_t)r * sr + (int64_t)k * sk : 0);
                 v[j] = ok ? x : 0.f;
             }
         }
     }
+
+    // S: [64 rows][kLd] bf16, row-major in (row, k) whatever the source layout.
     __device__ __forceinline__ void store(unsigned short* __restrict__ S) const {
         const int t = threadIdx.x;
         if constexpr (VEC) {
 #pragma unroll
             for (int u = 0; u < NV; ++u) {
                 const int id = u * 256 + t;
-                const int line = id / VPR, e = (id % VPR) * EPV;
+                const int line = id / VPL, e = (id % VPL) * EPV;
                 const float* x = v + u * EPV;
-                if (KC) {        // EPV consecutive k of one row -> one 8- or 16-byte store
+                if constexpr (KC) {      // EPV consecutive k of one row -> one 8/16-byte store
                     if constexpr (EPV == 8) {
                         u32x4 w;
 #pragma unroll
@@ -112,7 +115,7 @@ struct Tile {
                         const u32x2 w = {pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3])};
                         *reinterpret_cast<u32x2*>(S + line * kLd + e) = w;
                     }
-                } else {         // EPV consecutive rows of one k -> scattered 2-byte stores
+                } else {                 // EPV consecutive rows of one k -> 2-byte stores
 #pragma unroll
                     for (int q = 0; q < EPV; q += 2) {
                         const unsigned p = pack_bf16(x[q], x[q + 1]);
@@ -121,23 +124,23 @@ struct Tile {
                     }
                 }
             }
-        } else if (KC) {
-            const int r = t >> 2, kb = (t & 3) * 16;
-            u32x4 w0, w1;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                w0[q] = pack_bf16(v[2 * q], v[2 * q + 1]);
-                w1[q] = pack_bf16(v[8 + 2 * q], v[8 + 2 * q + 1]);
-            }
-            *reinterpret_cast<u32x4*>(S + r * kLd + kb) = w0;
-            *reinterpret_cast<u32x4*>(S + r * kLd + kb + 8) = w1;
         } else {
-            const int k = t >> 2, rb = (t & 3) * 16;
+            const int line = t / TPL, eb = (t % TPL) * E;
+            if constexpr (KC) {
 #pragma unroll
-            for (int j = 0; j < 16; j += 2) {
-                const unsigned p = pack_bf16(v[j], v[j + 1]);
-                S[(rb + j) * kLd + k] = (unsigned short)(p & 0xffffu);
-                S[(rb + j + 1) * kLd + k] = (unsigned short)(p >> 16);
+                for (int c = 0; c < E / 8; ++c) {
+                    u32x4 w;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) w[q] = pack_bf16(v[8 * c + 2 * q], v[8 * c + 2 * q + 1]);
+                    *reinterpret_cast<u32x4*>(S + line * kLd + eb + 8 * c) = w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < E; j += 2) {
+                    const unsigned p = pack_bf16(v[j], v[j + 1]);
+                    S[(eb + j) * kLd + line] = (unsigned short)(p & 0xffffu);
+                    S[(eb + j + 1) * kLd + line] = (unsigned short)(p >> 16);
+                }
             }
         }
     }
@@ -151,7 +154,6 @@ __device__ __forceinline__ void mfma_segment(f32x16& acc, unsigned short* __rest
     const TW* W = reinterpret_cast<const TW*>(Wv);
     // buffers addressed as sm + offset (not through a pointer array, which loses the LDS
     // address space and turns the fragment reads into flat loads): X0 X1 W0 W1
-    constexpr int kBuf = 64 * kLd;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const int r = lane & 31, h = lane >> 5;
@@ -189,16 +191,26 @@ __device__ __forceinline__ void mfma_segment(f32x16& acc, unsigned short* __rest
 
 template <typename TW, bool XK, bool WK, bool XV, bool WV>
 __global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a) {
-    __shared__ __attribute__((aligned(16))) unsigned short sm[4 * 64 * kLd];
-    const int b0 = blockIdx.y * 64, m0 = blockIdx.x * 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned short sm[];   // kLdsBytes
+    // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs (linear id % 8),
+    // each with its own L2.  Give XCD x the contiguous logical tiles [x*T/8, (x+1)*T/8) and
+    // walk logical tiles in groups of kGH tile-rows, column-major inside a group: the 32
+    // tiles an XCD holds at the training shapes form a 4 x 8 block, so its L2 fetches 4 X
+    // row-panels and 8 W column-panels instead of (up to) 32 of each.
+    constexpr int kGH = 4;
+    const int nx = gridDim.x, ny = gridDim.y, T = nx * ny;
+    const int lid = blockIdx.x + nx * blockIdx.y;
+    const int t = (T % 8 == 0) ? (lid % 8) * (T / 8) + lid / 8 : lid;
+    const int g = t / (kGH * nx), gh = min(kGH, ny - g * kGH), i = t - g * kGH * nx;
+    const int b0 = (g * kGH + i % gh) * 64, m0 = (i / gh) * 64;
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X, a.sxb, a.sxk, a.W, a.swm, a.swk, a.K, a.Bn,
                                      a.M, b0, m0);
     if (a.K2 > 0)
-        mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k, a.K2, a.Bn,
-                                 a.M, b0, m0);
+        mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k,
+                                         a.K2, a.Bn, a.M, b0, m0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = m0 + (wave & 1) * 32 + (lane & 31);
     if (m >= a.M) return;
@@ -236,17 +248,33 @@ bool vec_ok(const void* P, int64_t s_row, int64_t s_k, int rows, int K, int esiz
            ext % epv == 0;
 }
 
-template <typename TW, bool XK, bool WK>
-void launch_mfma3(const ldm_linear_args_t& a, bool xv, bool wv, hipStream_t s) {
+template <typename TW, bool XK, bool WK, bool XV, bool WV>
+int launch_one(const ldm_linear_args_t& a, hipStream_t s) {
+    auto* k = &linear_mfma_kernel<TW, XK, WK, XV, WV>;
+    static bool attr_set = false;     // one per instantiation; idempotent if raced
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 kLdsBytes);
+        LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_linear (mfma): hipFuncSetAttribute: %s",
+                    hipGetErrorString(e));
+        attr_set = true;
+    }
     const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64);
-    if (xv && wv) hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, true, true>), grid, dim3(256), 0, s, a);
-    else if (xv) hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, true, false>), grid, dim3(256), 0, s, a);
-    else if (wv) hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, false, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((linear_mfma_kernel<TW, XK, WK, false, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k, grid, dim3(256), kLdsBytes, s, a);
+    return 0;
+}
+
+template <typename TW, bool XK, bool WK>
+int launch_mfma3(const ldm_linear_args_t& a, bool xv, bool wv, hipStream_t s) {
+    if (xv && wv) return launch_one<TW, XK, WK, true, true>(a, s);
+    if (xv) return launch_one<TW, XK, WK, true, false>(a, s);
+    if (wv) return launch_one<TW, XK, WK, false, true>(a, s);
+    return launch_one<TW, XK, WK, false, false>(a, s);
 }
 
 template <typename TW>
-void launch_mfma(const ldm_linear_args_t& a, bool xk, bool wk, hipStream_t s) {
+int launch_mfma(const ldm_linear_args_t& a, bool xk, bool wk, hipStream_t s) {
     const int es = (int)sizeof(TW);
     static const bool vec_on = [] {      // development A/B knob: LDM_LINEAR_VEC=0 -> scalar tiles
         const char* e = getenv("LDM_LINEAR_VEC");
@@ -258,18 +286,19 @@ void launch_mfma(const ldm_linear_args_t& a, bool xk, bool wk, hipStream_t s) {
         xv = xv && vec_ok(a.X2, a.sx2b, a.sx2k, a.Bn, a.K2, 4);
         wv = wv && vec_ok(a.W2, a.sw2m, a.sw2k, a.M, a.K2, es);
     }
-    if (xk && wk) launch_mfma3<TW, true, true>(a, xv, wv, s);
-    else if (xk) launch_mfma3<TW, true, false>(a, xv, wv, s);
-    else if (wk) launch_mfma3<TW, false, true>(a, xv, wv, s);
-    else launch_mfma3<TW, false, false>(a, xv, wv, s);
+    if (xk && wk) return launch_mfma3<TW, true, true>(a, xv, wv, s);
+    if (xk) return launch_mfma3<TW, true, false>(a, xv, wv, s);
+    if (wk) return launch_mfma3<TW, false, true>(a, xv, wv, s);
+    return launch_mfma3<TW, false, false>(a, xv, wv, s);
 }
 
 }  // namespace
 
 int linear_mfma(const ldm_linear_args_t& a, hipStream_t s) {
     const bool xk = a.sxk == 1, wk = a.swk == 1;
-    if (a.w_dtype == LDM_BF16) launch_mfma<unsigned short>(a, xk, wk, s);
-    else launch_mfma<float>(a, xk, wk, s);
+    const int e = a.w_dtype == LDM_BF16 ? launch_mfma<unsigned short>(a, xk, wk, s)
+                                        : launch_mfma<float>(a, xk, wk, s);
+    if (e) return e;
     return launch_status("ldm_linear (mfma)");
 }
 

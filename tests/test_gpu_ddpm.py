@@ -57,11 +57,15 @@ def test_q_sample_bit_exact(dev):
     assert torch.equal(got, R.q_sample(tab, x0, e, t))
 
 
-def test_loss_and_grad(dev):
+@pytest.mark.parametrize("n,off", [(256000, 0), (1001 * 7, 0), (3, 0), (70001, 1)])
+def test_loss_and_grad(dev, n, off):
+    """Vector path (aligned, n % 4 tail) and scalar path (1-float offset views)."""
     from ldm_sdf import ops
     g = torch.Generator().manual_seed(2)
-    a, b = torch.randn(1000, 256, generator=g), torch.randn(1000, 256, generator=g)
-    loss, grad = ops.eps_mse_loss(a.to(dev), b.to(dev))
+    a, b = torch.randn(n + off, generator=g), torch.randn(n + off, generator=g)
+    a_d, b_d = a.to(dev)[off:], b.to(dev)[off:]
+    a, b = a[off:], b[off:]
+    loss, grad = ops.eps_mse_loss(a_d, b_d)
     ad = a.double()
     want = ((ad - b.double()) ** 2).mean()
     assert abs(float(loss) - float(want)) / float(want) < 1e-6
