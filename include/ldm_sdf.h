@@ -160,12 +160,14 @@ int ldm_sample_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float*
  *   LDM_EPI_RESID_SILU  Y = R + SiLU(pre);  A_out = pre (if A_out)      (A6 block)
  *   LDM_EPI_ACCUM       Y = Y + pre
  *   LDM_EPI_ADD_R       Y = R + pre                                     (A7 dh = dy + W^T g)
+ *   LDM_EPI_RELU        Y = max(pre, 0)                    (C19 decoder hidden layers)
  * w_dtype: LDM_F32 or LDM_BF16 (elements of W and W2). */
 #define LDM_EPI_BIAS 0
 #define LDM_EPI_SILU 1
 #define LDM_EPI_RESID_SILU 2
 #define LDM_EPI_ACCUM 3
 #define LDM_EPI_ADD_R 4
+#define LDM_EPI_RELU 5
 typedef struct ldm_linear_args {
     int32_t Bn, M, K, K2;
     int32_t epi;
@@ -194,6 +196,30 @@ int ldm_colsum(const float* G, int Bn, int M, float* out, int accumulate, ldm_st
 /* Row gather: out[b][:] = table[idx[b]][:] (timestep-embedding lookup, A5). */
 int ldm_gather_rows(const float* table, const int32_t* idx, int Bn, int C, float* out,
                     ldm_stream_t s);
+
+/* ---- C19 auto-decoder training (DeepSDF decoder backward + latent codes) --- */
+/* The decoder forward/backward GEMMs are ldm_linear (LDM_EPI_RELU forward; G W and G^T X
+ * backward) and the bias gradients ldm_colsum; these are the remaining pieces.
+ * ReLU backward on the post-activation: g = dy * (y > 0).  n elements. */
+int ldm_relu_bwd(const float* dy, const float* y, int n, float* g_out, ldm_stream_t s);
+/* DeepSDF clamped L1 on the decoder's pre-tanh output (deep_sdf train loop, enforce_minmax):
+ * pred = tanh(pre), loss_out[0] = scale * sum_i |clamp(pred_i) - clamp(gt_i)| with clamp to
+ * [-delta, delta], and grad_out[i] = d loss / d pre_i
+ *   = scale * sign(clamp(pred_i) - clamp(gt_i)) * [-delta <= pred_i <= delta] * (1 - pred_i^2)
+ * (sign(0) = 0; the clamp passes the gradient on the closed interval).  One workgroup, fixed
+ * summation order.  grad_out may be NULL. */
+int ldm_sdf_l1_loss(const float* pre, const float* gt, int n, float delta, float scale,
+                    float* loss_out, float* grad_out, ldm_stream_t s);
+/* Segmented column sums: out[s][m] (+)= sum_{p<P} G[s*P + p][m] for s < S (per-shape latent
+ * gradients: S shapes of P samples each, rows grouped by shape).  Deterministic. */
+int ldm_colsum_segments(const float* G, int S, int P, int M, float* out, int accumulate,
+                        ldm_stream_t s);
+/* DeepSDF code regulariser, per-sample L2 norm: loss_io[0] += coef * sum_s |z_s| and
+ * grad_io[s][:] += coef * z_s / |z_s| (0 where z_s = 0), z fp32 [S][L].  With S shapes of P
+ * samples each out of N = S P, DeepSDF's lambda * min(1, epoch/100) * sum_samples |z| / N is
+ * coef = lambda * min(1, epoch/100) / S.  One workgroup, fixed order. */
+int ldm_latent_l2_reg(const float* z, int S, int L, float coef, float* loss_io, float* grad_io,
+                      ldm_stream_t s);
 
 /* ---- C17 1D-UNet denoiser: fused conv1d (implicit GEMM) ------------------ */
 /* Y[b][co][l] = epi( sum_s sum_{ci<C_s} sum_{k<ksize_s} W_s(co,ci,k) * act_s(Xsrc_s(b,ci,l,k))

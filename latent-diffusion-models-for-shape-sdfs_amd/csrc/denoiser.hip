@@ -649,6 +649,7 @@ __global__ __launch_bounds__(256) void linear_tiled_kernel(ldm_linear_args_t a) 
                     *y = a.R[(int64_t)b * a.srb + m] + silu(pre);
                     break;
                 case LDM_EPI_ACCUM: *y = *y + pre; break;
+                case LDM_EPI_RELU: *y = fmaxf(pre, 0.f); break;
                 default: *y = a.R[(int64_t)b * a.srb + m] + pre; break;
             }
         }
@@ -678,6 +679,8 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
     __shared__ float red[16][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int m = blockIdx.x * 64 + tx;
+    G += (size_t)blockIdx.y * Bn * M;       // segment (ldm_colsum_segments); 0 for ldm_colsum
+    out += (size_t)blockIdx.y * M;
     float p[4] = {0.f, 0.f, 0.f, 0.f};
     if (m < M) {
         int b = ty;
@@ -819,7 +822,7 @@ extern "C" int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s) {
     LDM_REQUIRE(a && a->X && a->W && a->Y && a->Bn >= 1 && a->M >= 1 && a->K >= 1, LDM_EINVAL,
                 "bad linear args");
     LDM_REQUIRE(a->K2 == 0 || (a->X2 && a->W2), LDM_EINVAL, "second segment NULL");
-    LDM_REQUIRE(a->epi >= 0 && a->epi <= 4, LDM_EINVAL, "bad epilogue %d", a->epi);
+    LDM_REQUIRE(a->epi >= 0 && a->epi <= LDM_EPI_RELU, LDM_EINVAL, "bad epilogue %d", a->epi);
     LDM_REQUIRE((a->epi != LDM_EPI_RESID_SILU && a->epi != LDM_EPI_ADD_R) || a->R, LDM_EINVAL,
                 "epilogue needs R");
     LDM_REQUIRE(a->w_dtype == LDM_F32 || a->w_dtype == LDM_BF16, LDM_EINVAL, "bad w_dtype");
@@ -845,6 +848,15 @@ extern "C" int ldm_colsum(const float* G, int Bn, int M, float* out, int accumul
     hipLaunchKernelGGL(colsum_kernel, dim3((M + 63) / 64), dim3(1024), 0, (hipStream_t)s, G, Bn, M,
                        out, accumulate);
     return launch_status("ldm_colsum");
+}
+
+extern "C" int ldm_colsum_segments(const float* G, int S, int P, int M, float* out,
+                                   int accumulate, ldm_stream_t s) {
+    LDM_REQUIRE(G && out && S >= 1 && P >= 1 && M >= 1, LDM_EINVAL, "bad colsum_segments args");
+    LDM_REQUIRE(S <= 65535, LDM_EINVAL, "too many segments (%d)", S);
+    hipLaunchKernelGGL(colsum_kernel, dim3((M + 63) / 64, S), dim3(1024), 0, (hipStream_t)s, G, P,
+                       M, out, accumulate);
+    return launch_status("ldm_colsum_segments");
 }
 
 extern "C" int ldm_gather_rows(const float* table, const int32_t* idx, int Bn, int C, float* out,

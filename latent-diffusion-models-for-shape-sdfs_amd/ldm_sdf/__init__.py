@@ -9,6 +9,8 @@ from .models import DDPMSchedule, MLPDenoiser, SDFDecoder, decoder_layer_dims  #
 from .unet import UNet1DDenoiser  # noqa: F401
 from .mesh import marching_cubes, marching_cubes_batch, mc_table, write_ply  # noqa: F401
 from .api import Sampler, TrainState, decode, decode_points, sample, train, train_step  # noqa: F401
+from .autodecoder import (AutoDecoderState, autodecoder_train_step,  # noqa: F401
+                          train_autodecoder)
 from . import ops, dist, pack  # noqa: F401
 from ._capi import LdmError, load as load_library  # noqa: F401
 

@@ -24,7 +24,7 @@ LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER = 0, 1
 LAYOUT_CODES = {"pass8": LAYOUT_PASS8, "quarter": LAYOUT_QUARTER}
-EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R = 0, 1, 2, 3, 4
+EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R, EPI_RELU = 0, 1, 2, 3, 4, 5
 COMPUTE_FP32, COMPUTE_BF16 = 0, 1
 COMPUTE_CODES = {"fp32": COMPUTE_FP32, "bf16": COMPUTE_BF16}
 MAX_BLOCKS = 8
@@ -112,6 +112,10 @@ SIGNATURES = [
     ("ldm_silu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),
     ("ldm_colsum", _i, [_fp, _i, _i, _fp, _i, _vp]),
     ("ldm_gather_rows", _i, [_fp, _vp, _i, _i, _fp, _vp]),
+    ("ldm_relu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),
+    ("ldm_sdf_l1_loss", _i, [_fp, _fp, _i, _f, _f, _fp, _fp, _vp]),
+    ("ldm_colsum_segments", _i, [_fp, _i, _i, _i, _fp, _i, _vp]),
+    ("ldm_latent_l2_reg", _i, [_fp, _i, _i, _f, _fp, _fp, _vp]),
     ("ldm_conv1d", _i, [C.POINTER(ConvArgs), _vp]),
     ("ldm_mc_workspace_bytes", _sz, [_i]),
     ("ldm_mc_count", _i, [_fp, _i, _f, _vp, _sz, _vp, _vp]),

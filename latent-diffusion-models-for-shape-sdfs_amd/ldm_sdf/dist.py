@@ -97,12 +97,22 @@ def all_gather_rows(local: torch.Tensor, n: int, group=None) -> torch.Tensor:
 
 def allreduce_mean_(tensors, group=None) -> None:
     """Average gradients over ranks: flatten into one bucket, one all-reduce (RCCL)."""
+    _allreduce_(tensors, group, mean=True)
+
+
+def allreduce_sum_(tensors, group=None) -> None:
+    """Sum over ranks in place (one bucket, one all-reduce)."""
+    _allreduce_(tensors, group, mean=False)
+
+
+def _allreduce_(tensors, group, mean: bool) -> None:
     world, _ = world_and_rank(group)
     if world == 1:
         return
     flat = torch.cat([t.reshape(-1) for t in tensors])
     dist.all_reduce(flat, group=group)
-    flat.div_(world)
+    if mean:
+        flat.div_(world)
     off = 0
     for t in tensors:
         n = t.numel()

@@ -82,6 +82,10 @@ class SDFDecoder:
 
     DEFAULT_LAYOUT = "quarter"
 
+    def invalidate(self) -> None:
+        """Call after the weights changed (auto-decoder training): drops the packed copies."""
+        self._dev.clear()
+
     def device_pack(self, dtype: str, device: torch.device,
                     layout: Optional[str] = None) -> Dict[str, object]:
         """Packed device arrays + ``ldm_decoder_t`` (cached per dtype/device/layout)."""

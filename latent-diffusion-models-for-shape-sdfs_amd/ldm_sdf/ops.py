@@ -242,6 +242,54 @@ def gather_rows(table: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# ---------------------------------------------------------------------------------------- C19
+def relu_bwd(dy: torch.Tensor, y: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``dy * (y > 0)`` on the post-activation ``y``."""
+    _contig(dy, y)
+    out = torch.empty_like(dy) if out is None else out
+    capi.check(capi.load().ldm_relu_bwd(dy.data_ptr(), y.data_ptr(), dy.numel(), out.data_ptr(),
+                                        capi.stream_handle(dy.device)), "ldm_relu_bwd")
+    return out
+
+
+def sdf_l1_loss(pre: torch.Tensor, gt: torch.Tensor, delta: float, scale: float,
+                with_grad: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """DeepSDF clamped L1 on ``tanh(pre)`` (see ``ldm_sdf_l1_loss``): (loss [1], d/d pre)."""
+    capi.require_device(pre, gt)
+    _contig(pre, gt)
+    if pre.numel() != gt.numel():
+        raise capi.LdmError(f"sdf_l1_loss: {pre.numel()} predictions vs {gt.numel()} targets")
+    loss = torch.empty(1, device=pre.device, dtype=torch.float32)
+    grad = torch.empty_like(pre) if with_grad else None
+    capi.check(capi.load().ldm_sdf_l1_loss(pre.data_ptr(), gt.data_ptr(), pre.numel(), delta,
+                                           scale, loss.data_ptr(), capi.ptr(grad),
+                                           capi.stream_handle(pre.device)), "ldm_sdf_l1_loss")
+    return loss, grad
+
+
+def colsum_segments(G: torch.Tensor, S: int, out: torch.Tensor,
+                    accumulate: bool = False) -> torch.Tensor:
+    """``out[s] (+)= G[s*P:(s+1)*P].sum(0)`` for ``G`` [S*P, M] (rows grouped by segment)."""
+    _contig(G, out)
+    N, M = G.shape
+    if N % S or tuple(out.shape) != (S, M):
+        raise capi.LdmError(f"colsum_segments: G{tuple(G.shape)} S={S} out{tuple(out.shape)}")
+    capi.check(capi.load().ldm_colsum_segments(G.data_ptr(), S, N // S, M, out.data_ptr(),
+                                               int(accumulate), capi.stream_handle(G.device)),
+               "ldm_colsum_segments")
+    return out
+
+
+def latent_l2_reg(z: torch.Tensor, coef: float, loss_io: torch.Tensor,
+                  grad_io: Optional[torch.Tensor]) -> None:
+    """``loss_io += coef * sum_s |z_s|``, ``grad_io += coef * z_s / |z_s|`` (DeepSDF code_reg)."""
+    _contig(z, loss_io)
+    S, L = z.shape
+    capi.check(capi.load().ldm_latent_l2_reg(z.data_ptr(), S, L, coef, loss_io.data_ptr(),
+                                             capi.ptr(grad_io), capi.stream_handle(z.device)),
+               "ldm_latent_l2_reg")
+
+
 # ---------------------------------------------------------------------------------------- C17
 def _r16(n: int) -> int:
     return (n + 15) // 16 * 16
