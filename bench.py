@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--c5-batch", type=int, default=1)
     ap.add_argument("--no-mc", action="store_true",
                     help="skip C18 (marching cubes of one decoded 256^3 volume)")
+    ap.add_argument("--no-autodecoder", action="store_true",
+                    help="skip C19 (DeepSDF auto-decoder training at 64 shapes x 16384 samples)")
+    ap.add_argument("--ad-steps", type=int, default=5)
     ap.add_argument("--config3", action="store_true",
                     help="also time sample(8) -> decode 128^3 end to end (adds a decoder "
                          "launch of another size to the profile)")
@@ -149,6 +152,54 @@ def bench_mc(vol, args):
 
 FLOPS_PER_QUERY_WIDEN = 2 * (3 * 512 + 2 * 512 * 512 + 512 * 512 + 515 * 512 + 3 * 512 * 512
                              + 512)
+
+
+def bench_autodecoder(args, dev):
+    """C19: DeepSDF auto-decoder training steps at the DeepSDF batch (64 scenes x 16384 SDF
+    samples = 1,048,576 samples/step), bf16 matrix-core GEMMs, synthetic near-surface sphere
+    samples.  CPU baseline: the fp32 oracle step (torch autograd) on a 1 x 4096 sample."""
+    import ldm_sdf
+    S, P = 64, 16384
+    g = torch.Generator(device=dev).manual_seed(7)
+    radii = 0.3 + 0.5 * torch.rand(S, device=dev, generator=g)
+    d = torch.randn(S, P, 3, device=dev, generator=g)
+    d = d / d.norm(dim=2, keepdim=True)
+    r = radii[:, None] + 0.05 * torch.randn(S, P, device=dev, generator=g)
+    xyz = d * r[..., None]
+    sdf = xyz.norm(dim=2) - radii[:, None]
+    dec = ldm_sdf.SDFDecoder(seed=1234)
+    dec.weights[8] = dec.weights[8] * 0.01
+    st = ldm_sdf.train_autodecoder(dec, xyz, sdf, steps=1, shapes_per_batch=S,
+                                   samples_per_shape=P, dtype="bf16", generator=g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = ldm_sdf.train_autodecoder(dec, xyz, sdf, steps=args.ad_steps, shapes_per_batch=S,
+                                   samples_per_shape=P, dtype="bf16", generator=g, state=st)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.ad_steps
+    fwd = sum(2 * i * o for (i, o) in ldm_sdf.decoder_layer_dims(256, 512))   # per sample
+    res = {"metric": "DeepSDF auto-decoder training steps/sec (64 x 16384 samples)",
+           "value": 1.0 / dt, "unit": "steps/s", "ms_per_step": dt * 1e3,
+           "samples_per_s": S * P / dt, "flops_per_sample_fwd": fwd,
+           "tflops_fwd_bwd": 3 * fwd * S * P / dt / 1e12, "dtype": "bf16",
+           "loss_first_last": [st.losses[0], st.losses[-1]]}
+    if not args.no_cpu:
+        from oracle import ref_cpu as R
+        from oracle import ref_autodecoder as A
+        torch.set_num_threads(host_cores())
+        p = R.make_decoder_params(seed=1234, dtype=torch.float32)
+        zc = torch.randn(1, 256) / 16
+        xc, sc = xyz[:1, :4096].cpu(), sdf[:1, :4096].cpu()
+        A.autodecoder_grads(p, zc, xc, sc)
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < min(5.0, args.cpu_seconds):
+            A.autodecoder_grads(p, zc, xc, sc)
+            n += 1
+        sps = n * 4096 / (time.perf_counter() - t1)
+        res["cpu_baseline"] = {"value": sps, "unit": "samples/s", "cores": host_cores(),
+                               "kind": "port", "sample": f"{n} fp32 oracle steps (torch "
+                               "autograd) of 1 shape x 4096 samples"}
+    return res
 
 
 def config5(args, rank, world, dev, group, gen):
@@ -382,6 +433,8 @@ def main():
                         "unit": "steps/s", "batch": 1000, "ms_per_step": dtt * 1e3,
                         "tflops_fwd_bwd": 3 * 2 * macs / dtt / 1e12,
                         "loss_first_last": [st.losses[0], st.losses[-1]]}
+    if rank == 0 and not args.no_autodecoder:
+        res["autodecoder"] = bench_autodecoder(args, dev)
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_decode(N, args.cpu_seconds)
         if "ddpm" in res:

@@ -161,6 +161,8 @@ int ldm_sample_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float*
  *   LDM_EPI_ACCUM       Y = Y + pre
  *   LDM_EPI_ADD_R       Y = R + pre                                     (A7 dh = dy + W^T g)
  *   LDM_EPI_RELU        Y = max(pre, 0)                    (C19 decoder hidden layers)
+ *   LDM_EPI_MASK_R      Y = R > 0 ? pre : 0   (C19: ReLU backward through the post-activation
+ *                                              R, fused into the G W product)
  * w_dtype: LDM_F32 or LDM_BF16 (elements of W and W2). */
 #define LDM_EPI_BIAS 0
 #define LDM_EPI_SILU 1
@@ -168,6 +170,7 @@ int ldm_sample_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float*
 #define LDM_EPI_ACCUM 3
 #define LDM_EPI_ADD_R 4
 #define LDM_EPI_RELU 5
+#define LDM_EPI_MASK_R 6
 typedef struct ldm_linear_args {
     int32_t Bn, M, K, K2;
     int32_t epi;
@@ -181,6 +184,7 @@ typedef struct ldm_linear_args {
     float* Y;        int64_t syb, sym;
     float* A_out;    int64_t sab;    /* pre-activation rows (col stride 1) */
     int32_t compute;                 /* LDM_COMPUTE_FP32 or LDM_COMPUTE_BF16 (below) */
+    float* ws; int64_t ws_floats;    /* optional split-K workspace (LDM_COMPUTE_BF16), or NULL */
 } ldm_linear_args_t;
 /* LDM_COMPUTE_FP32: exact fp32 products (VALU register-tiled kernel).
  * LDM_COMPUTE_BF16: matrix cores -- X and W rounded to bf16 (RNE) as they are staged, fp32
@@ -188,6 +192,13 @@ typedef struct ldm_linear_args {
 #define LDM_COMPUTE_FP32 0
 #define LDM_COMPUTE_BF16 1
 int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s);
+/* Split-K (LDM_COMPUTE_BF16, K2 == 0): when the output has too few 64x64 tiles to fill the
+ * chip and K is long -- the weight gradients G^T X over ~1M samples of C19 -- the K range is
+ * cut into slices that run as separate workgroups, each writing a partial [Bn][M] into ws,
+ * and a second kernel sums the slices in fixed order (deterministic) and applies the
+ * epilogue.  Returns the ws size (floats) that enables it for these args (0: not worth it);
+ * ldm_linear uses it when a->ws has at least that many floats, else runs unsplit. */
+int64_t ldm_linear_workspace_floats(const ldm_linear_args_t* a);
 
 /* SiLU backward on the block pre-activation: g = dy * silu'(a)  (A7). n elements. */
 int ldm_silu_bwd(const float* dy, const float* a, int n, float* g_out, ldm_stream_t s);

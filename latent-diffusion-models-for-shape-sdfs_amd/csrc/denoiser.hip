@@ -650,6 +650,7 @@ __global__ __launch_bounds__(256) void linear_tiled_kernel(ldm_linear_args_t a) 
                     break;
                 case LDM_EPI_ACCUM: *y = *y + pre; break;
                 case LDM_EPI_RELU: *y = fmaxf(pre, 0.f); break;
+                case LDM_EPI_MASK_R: *y = a.R[(int64_t)b * a.srb + m] > 0.f ? pre : 0.f; break;
                 default: *y = a.R[(int64_t)b * a.srb + m] + pre; break;
             }
         }
@@ -822,8 +823,8 @@ extern "C" int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s) {
     LDM_REQUIRE(a && a->X && a->W && a->Y && a->Bn >= 1 && a->M >= 1 && a->K >= 1, LDM_EINVAL,
                 "bad linear args");
     LDM_REQUIRE(a->K2 == 0 || (a->X2 && a->W2), LDM_EINVAL, "second segment NULL");
-    LDM_REQUIRE(a->epi >= 0 && a->epi <= LDM_EPI_RELU, LDM_EINVAL, "bad epilogue %d", a->epi);
-    LDM_REQUIRE((a->epi != LDM_EPI_RESID_SILU && a->epi != LDM_EPI_ADD_R) || a->R, LDM_EINVAL,
+    LDM_REQUIRE(a->epi >= 0 && a->epi <= LDM_EPI_MASK_R, LDM_EINVAL, "bad epilogue %d", a->epi);
+    LDM_REQUIRE((a->epi != LDM_EPI_RESID_SILU && a->epi != LDM_EPI_ADD_R && a->epi != LDM_EPI_MASK_R) || a->R, LDM_EINVAL,
                 "epilogue needs R");
     LDM_REQUIRE(a->w_dtype == LDM_F32 || a->w_dtype == LDM_BF16, LDM_EINVAL, "bad w_dtype");
     LDM_REQUIRE(a->compute == LDM_COMPUTE_FP32 || a->compute == LDM_COMPUTE_BF16, LDM_EINVAL,
@@ -833,6 +834,11 @@ extern "C" int ldm_linear(const ldm_linear_args_t* a, ldm_stream_t s) {
     if (a->w_dtype == LDM_BF16) launch_tiled<unsigned short>(*a, xk, wk, (hipStream_t)s);
     else launch_tiled<float>(*a, xk, wk, (hipStream_t)s);
     return launch_status("ldm_linear");
+}
+
+extern "C" int64_t ldm_linear_workspace_floats(const ldm_linear_args_t* a) {
+    if (!a || a->Bn < 1 || a->M < 1 || a->K < 1) return 0;
+    return linear_mfma_ws_floats(*a);
 }
 
 extern "C" int ldm_silu_bwd(const float* dy, const float* a, int n, float* g_out, ldm_stream_t s) {

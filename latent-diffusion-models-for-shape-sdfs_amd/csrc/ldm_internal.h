@@ -61,5 +61,6 @@ int decoder_q_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, i
 
 // matrix-core path of ldm_linear (linear_mfma.hip)
 int linear_mfma(const ldm_linear_args_t& a, hipStream_t s);
+int64_t linear_mfma_ws_floats(const ldm_linear_args_t& a);   // split-K workspace
 
 }  // namespace ldm

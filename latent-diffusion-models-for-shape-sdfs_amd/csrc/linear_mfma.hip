@@ -20,6 +20,8 @@
 #include "ldm_internal.h"
 #include "ddpm_common.h"
 
+#include <algorithm>
+
 namespace ldm {
 namespace {
 
@@ -189,8 +191,30 @@ __device__ __forceinline__ void mfma_segment(f32x16& acc, unsigned short* __rest
     }
 }
 
+__device__ __forceinline__ void apply_epi(const ldm_linear_args_t& a, int b, int m, float pre) {
+    float* y = a.Y + (int64_t)b * a.syb + (int64_t)m * a.sym;
+    switch (a.epi) {
+        case LDM_EPI_BIAS: *y = pre; break;
+        case LDM_EPI_SILU:
+            if (a.A_out) a.A_out[(int64_t)b * a.sab + m] = pre;
+            *y = silu(pre);
+            break;
+        case LDM_EPI_RESID_SILU:
+            if (a.A_out) a.A_out[(int64_t)b * a.sab + m] = pre;
+            *y = a.R[(int64_t)b * a.srb + m] + silu(pre);
+            break;
+        case LDM_EPI_ACCUM: *y = *y + pre; break;
+        case LDM_EPI_RELU: *y = fmaxf(pre, 0.f); break;
+        case LDM_EPI_MASK_R: *y = a.R[(int64_t)b * a.srb + m] > 0.f ? pre : 0.f; break;
+        default: *y = a.R[(int64_t)b * a.srb + m] + pre; break;
+    }
+}
+
+// gridDim.z > 1: split-K.  Slice z covers k in [z*kc_len, min(K, (z+1)*kc_len)) (kc_len a
+// multiple of kKC, every slice non-empty) and stores its raw partial to ws[z][b][m]; the
+// epilogue is split_reduce_kernel's.
 template <typename TW, bool XK, bool WK, bool XV, bool WV>
-__global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a) {
+__global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a, int kc_len) {
     extern __shared__ __attribute__((aligned(16))) unsigned short sm[];   // kLdsBytes
     // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs (linear id % 8),
     // each with its own L2.  Give XCD x the contiguous logical tiles [x*T/8, (x+1)*T/8) and
@@ -203,39 +227,54 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a) {
     const int t = (T % 8 == 0) ? (lid % 8) * (T / 8) + lid / 8 : lid;
     const int g = t / (kGH * nx), gh = min(kGH, ny - g * kGH), i = t - g * kGH * nx;
     const int b0 = (g * kGH + i % gh) * 64, m0 = (i / gh) * 64;
+    const bool split = gridDim.z > 1;
+    const int kb = blockIdx.z * kc_len, kl = min(a.K - kb, kc_len);
+    const TW* W = reinterpret_cast<const TW*>(a.W);
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X, a.sxb, a.sxk, a.W, a.swm, a.swk, a.K, a.Bn,
-                                     a.M, b0, m0);
+    mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X + (int64_t)kb * a.sxk, a.sxb, a.sxk,
+                                     W + (int64_t)kb * a.swk, a.swm, a.swk, kl, a.Bn, a.M, b0,
+                                     m0);
     if (a.K2 > 0)
         mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k,
                                          a.K2, a.Bn, a.M, b0, m0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = m0 + (wave & 1) * 32 + (lane & 31);
     if (m >= a.M) return;
-    const float bias = a.bias ? a.bias[m] : 0.f;
+    float* part = a.ws + (size_t)blockIdx.z * a.Bn * a.M;
+    const float bias = (!split && a.bias) ? a.bias[m] : 0.f;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
         const int b = b0 + (wave >> 1) * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
         if (b >= a.Bn) continue;
-        const float pre = acc[v] + bias;
-        float* y = a.Y + (int64_t)b * a.syb + (int64_t)m * a.sym;
-        switch (a.epi) {
-            case LDM_EPI_BIAS: *y = pre; break;
-            case LDM_EPI_SILU:
-                if (a.A_out) a.A_out[(int64_t)b * a.sab + m] = pre;
-                *y = silu(pre);
-                break;
-            case LDM_EPI_RESID_SILU:
-                if (a.A_out) a.A_out[(int64_t)b * a.sab + m] = pre;
-                *y = a.R[(int64_t)b * a.srb + m] + silu(pre);
-                break;
-            case LDM_EPI_ACCUM: *y = *y + pre; break;
-            case LDM_EPI_RELU: *y = fmaxf(pre, 0.f); break;
-            default: *y = a.R[(int64_t)b * a.srb + m] + pre; break;
-        }
+        if (split) part[(size_t)b * a.M + m] = acc[v];
+        else apply_epi(a, b, m, acc[v] + bias);
     }
+}
+
+// Split-K second pass: the slices' partials summed in slice order, then the epilogue.
+__global__ void split_reduce_kernel(ldm_linear_args_t a, int nz) {
+    const int64_t n = (int64_t)a.Bn * a.M;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int z = 0; z < nz; ++z) s += a.ws[(size_t)z * n + i];
+    const int b = (int)(i / a.M), m = (int)(i - (int64_t)b * a.M);
+    apply_epi(a, b, m, s + (a.bias ? a.bias[m] : 0.f));
+}
+
+// Split plan: slices so that tiles x slices reaches ~4 workgroups per CU, each slice at
+// least 8 chunks deep.  {slices, slice length}; slices == 1: no split.
+struct SplitPlan { int nz, kc_len; };
+SplitPlan split_plan(const ldm_linear_args_t& a) {
+    const int64_t tiles = (int64_t)((a.M + 63) / 64) * ((a.Bn + 63) / 64);
+    if (a.compute != LDM_COMPUTE_BF16 || a.K2 > 0 || tiles >= 256) return {1, a.K};
+    int nz = (int)std::min<int64_t>((1024 + tiles - 1) / tiles, a.K / (8 * kKC));
+    nz = std::min(nz, 256);
+    if (nz < 2) return {1, a.K};
+    const int kc = ((a.K + nz - 1) / nz + kKC - 1) / kKC * kKC;
+    return {(a.K + kc - 1) / kc, kc};
 }
 
 // Can an operand use 16-byte vector loads?  Its contiguous dimension must have stride 1 and
@@ -261,8 +300,15 @@ int launch_one(const ldm_linear_args_t& a, hipStream_t s) {
                     hipGetErrorString(e));
         attr_set = true;
     }
-    const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64);
-    hipLaunchKernelGGL(k, grid, dim3(256), kLdsBytes, s, a);
+    SplitPlan sp = split_plan(a);
+    if (sp.nz > 1 && (!a.ws || a.ws_floats < (int64_t)sp.nz * a.Bn * a.M)) sp = {1, a.K};
+    const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64, sp.nz);
+    hipLaunchKernelGGL(k, grid, dim3(256), kLdsBytes, s, a, sp.kc_len);
+    if (sp.nz > 1) {
+        const int64_t n = (int64_t)a.Bn * a.M;
+        hipLaunchKernelGGL(split_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           s, a, sp.nz);
+    }
     return 0;
 }
 
@@ -294,6 +340,11 @@ int launch_mfma(const ldm_linear_args_t& a, bool xk, bool wk, hipStream_t s) {
 }
 
 }  // namespace
+
+int64_t linear_mfma_ws_floats(const ldm_linear_args_t& a) {
+    const SplitPlan sp = split_plan(a);
+    return sp.nz > 1 ? (int64_t)sp.nz * a.Bn * a.M : 0;
+}
 
 int linear_mfma(const ldm_linear_args_t& a, hipStream_t s) {
     const bool xk = a.sxk == 1, wk = a.swk == 1;

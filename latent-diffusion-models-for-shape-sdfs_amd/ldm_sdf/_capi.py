@@ -24,7 +24,7 @@ LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER = 0, 1
 LAYOUT_CODES = {"pass8": LAYOUT_PASS8, "quarter": LAYOUT_QUARTER}
-EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R, EPI_RELU = 0, 1, 2, 3, 4, 5
+EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R, EPI_RELU, EPI_MASK_R = range(7)
 COMPUTE_FP32, COMPUTE_BF16 = 0, 1
 COMPUTE_CODES = {"fp32": COMPUTE_FP32, "bf16": COMPUTE_BF16}
 MAX_BLOCKS = 8
@@ -66,7 +66,8 @@ class LinearArgs(C.Structure):
                 ("W2", _vp), ("sw2m", C.c_int64), ("sw2k", C.c_int64),
                 ("bias", _vp), ("R", _vp), ("srb", C.c_int64),
                 ("Y", _vp), ("syb", C.c_int64), ("sym", C.c_int64),
-                ("A_out", _vp), ("sab", C.c_int64), ("compute", C.c_int32)]
+                ("A_out", _vp), ("sab", C.c_int64), ("compute", C.c_int32),
+                ("ws", _vp), ("ws_floats", C.c_int64)]
 
 
 CONV_DIRECT, CONV_UP2 = 0, 1
@@ -109,6 +110,7 @@ SIGNATURES = [
     ("ldm_sample_step", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _i, _i, _fp,
                              _fp, _vp]),
     ("ldm_linear", _i, [C.POINTER(LinearArgs), _vp]),
+    ("ldm_linear_workspace_floats", C.c_int64, [C.POINTER(LinearArgs)]),
     ("ldm_silu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),
     ("ldm_colsum", _i, [_fp, _i, _i, _fp, _i, _vp]),
     ("ldm_gather_rows", _i, [_fp, _vp, _i, _i, _fp, _vp]),

@@ -18,8 +18,10 @@ torch provides memory, the row gather's destination copies and Adam (plumbing), 
 Working layout (rebuilt from the fp32 masters each step, in the GEMM dtype).  It pads so that
 every operand row is a multiple of 16 bytes and the matrix-core path can use vector loads:
 
-* ``Zx`` [N, 260] = ``[z_s || xyz || 0]``. It is the input of layer 0 and the second
-  segment of layer 4.
+* ``Zx`` [N, 264] = ``[z_s || xyz || 0]`` (8-column multiple: 16-byte rows in bf16). It is the
+  input of layer 0 and the second segment of layer 4.
+* The backward's ``G W`` products apply the ReLU mask in their epilogue (``LDM_EPI_MASK_R``
+  with the saved post-activation), so ``relu_bwd`` is a separate pass nowhere.
 * Layer ``skip-1`` (253 outputs) is padded to 256 rows with zero weights and biases, so its
   ReLU output ``h3`` [N, 256] has 3 zero columns. Layer ``skip`` is two segments,
   ``h3 · W4h^T + Zx · W4z^T``.
@@ -53,7 +55,8 @@ def _check_decoder(dec: SDFDecoder) -> Tuple[int, int]:
 
 
 def _zx_width(L: int) -> int:
-    return (L + 3 + 3) // 4 * 4
+    """[z || xyz] padded to a multiple of 8 columns: 16-byte rows in bf16 as well as fp32."""
+    return (L + 3 + 7) // 8 * 8
 
 
 def _pad_rows(n: int) -> int:
@@ -186,9 +189,9 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
             ops.linear(g, w["W0"][:, :L].T, dz, epi=capi.EPI_ACCUM, compute=cp)
             break
         Wd = w["W4h"] if l == skip else w[f"W{l}"]
-        dh = torch.empty(N, Wd.shape[1], **f32)
-        ops.linear(g, Wd.T, dh, compute=cp)
-        g = ops.relu_bwd(dh, h[l - 1])
+        dh = torch.empty(N, Wd.shape[1], **f32)       # ReLU backward fused: R = post-act.
+        ops.linear(g, Wd.T, dh, epi=capi.EPI_MASK_R, R=h[l - 1], compute=cp)
+        g = dh
 
     gz = torch.empty(S, L, **f32)
     ops.colsum_segments(dz, S, gz)

@@ -212,7 +212,14 @@ def linear(X: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, *, epi: int = capi
         if A_out.stride(1) != 1:
             raise capi.LdmError("linear: A_out rows must be contiguous")
         a.A_out, a.sab = A_out.data_ptr(), A_out.stride(0)
-    capi.check(capi.load().ldm_linear(C.byref(a), capi.stream_handle(Y.device)), "ldm_linear")
+    lib = capi.load()
+    ws = None
+    if compute == capi.COMPUTE_BF16:
+        n = lib.ldm_linear_workspace_floats(C.byref(a))
+        if n > 0:     # split-K partials; freed to the stream-ordered cache after the launch
+            ws = torch.empty(n, device=Y.device, dtype=torch.float32)
+            a.ws, a.ws_floats = ws.data_ptr(), n
+    capi.check(lib.ldm_linear(C.byref(a), capi.stream_handle(Y.device)), "ldm_linear")
     return Y
 
 
@@ -225,8 +232,17 @@ def silu_bwd(dy: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] = No
 
 
 def colsum(G: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """``out (+)= G.sum(0)``, deterministic.  Tall G (>= 64k rows, e.g. C19's 1M samples) goes
+    in two passes -- per-segment sums over up to 256 row segments in parallel, then their sum --
+    because the one-pass kernel has only ceil(M/64) workgroups."""
     _contig(G)
     Bn, M = G.shape
+    if Bn >= 65536:
+        segs = next((s for s in (256, 128, 64, 32, 16) if Bn % s == 0), 0)
+        if segs:
+            part = torch.empty(segs, M, device=G.device, dtype=torch.float32)
+            colsum_segments(G, segs, part)
+            G, Bn = part, segs
     capi.check(capi.load().ldm_colsum(G.data_ptr(), Bn, M, out.data_ptr(), int(accumulate),
                                       capi.stream_handle(G.device)), "ldm_colsum")
     return out

@@ -1,0 +1,31 @@
+"""C19 workload for profilers: DeepSDF auto-decoder training at 64 shapes x 16384 samples,
+bf16 matrix-core GEMMs (AD_STEPS steps after one warm-up step)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "latent-diffusion-models-for-shape-sdfs_amd")]
+import torch  # noqa: E402
+import ldm_sdf  # noqa: E402
+
+S, P = int(os.environ.get("AD_S", "64")), int(os.environ.get("AD_P", "16384"))
+steps = int(os.environ.get("AD_STEPS", "3"))
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(7)
+radii = 0.3 + 0.5 * torch.rand(S, device=dev, generator=g)
+d = torch.randn(S, P, 3, device=dev, generator=g)
+d = d / d.norm(dim=2, keepdim=True)
+xyz = d * (radii[:, None] + 0.05 * torch.randn(S, P, device=dev, generator=g))[..., None]
+sdf = xyz.norm(dim=2) - radii[:, None]
+dec = ldm_sdf.SDFDecoder(seed=1234)
+dec.weights[8] = dec.weights[8] * 0.01
+st = ldm_sdf.train_autodecoder(dec, xyz, sdf, steps=1, shapes_per_batch=S, samples_per_shape=P,
+                               dtype="bf16", generator=g)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+st = ldm_sdf.train_autodecoder(dec, xyz, sdf, steps=steps, shapes_per_batch=S,
+                               samples_per_shape=P, dtype="bf16", generator=g, state=st)
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / steps
+print(f"autodecoder {S}x{P}: {dt * 1e3:.1f} ms/step, loss {st.losses[-1]:.4f}")

@@ -84,7 +84,7 @@ def test_work_layout_round_trip():
         m[f"W{l}"] = torch.randn(o, i, generator=g)
         m[f"b{l}"] = torch.randn(o, generator=g)
     w = work_weights(m, L, H, skip, torch.float32)
-    assert tuple(w["W0"].shape) == (H, 260) and float(w["W0"][:, 259].abs().sum()) == 0
+    assert tuple(w["W0"].shape) == (H, 264) and float(w["W0"][:, 259:].abs().sum()) == 0
     assert tuple(w["W3"].shape) == (256, H) and float(w["W3"][253:].abs().sum()) == 0
     assert float(w["b3p"][253:].abs().sum()) == 0
     assert float(w["W4h"][:, 253:].abs().sum()) == 0 and float(w["W4z"][:, 259:].abs().sum()) == 0

@@ -101,6 +101,31 @@ def _allreduce(rank, world):
     return bool(torch.allclose(a, torch.full_like(a, m)) and torch.allclose(b, torch.full_like(b, 2 * m)))
 
 
+def _latent_rows(rank, world):
+    """train_autodecoder's latent exchange: every rank draws the same shapes, owns a contiguous
+    share, writes its rows scaled by its share of the batch, and one all-reduce (sum) gives every
+    rank the same full table of row gradients."""
+    from ldm_sdf.dist import allreduce_sum_, batch_shard
+    n_shapes, S, L = 10, 6, 4
+    sidx = torch.randperm(n_shapes, generator=torch.Generator().manual_seed(3))[:S]
+    lo, hi = batch_shard(S, rank, world)
+    gz = torch.arange(lo, hi).float()[:, None].repeat(1, L) + 1.0   # "local grads" of my rows
+    lat = torch.zeros(n_shapes, L)
+    lat[sidx[lo:hi]] = gz * ((hi - lo) / S)
+    allreduce_sum_([lat])
+    want = torch.zeros(n_shapes, L)
+    for r in range(world):
+        a, b = batch_shard(S, r, world)
+        want[sidx[a:b]] = (torch.arange(a, b).float()[:, None].repeat(1, L) + 1.0) * ((b - a) / S)
+    return bool(torch.equal(lat, want))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_autodecoder_latent_exchange(world):
+    res = _run("_latent_rows", world)
+    assert all(res[r] is True for r in range(world)), res
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_zslab_reassembly_exact(world):
     res = _run("_volume_exact", world)

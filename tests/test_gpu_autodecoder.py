@@ -148,3 +148,21 @@ def test_fit_lowers_loss_on_spheres(dev):
     assert torch.equal(dec.weights[0], st.masters["W0"].cpu())
     out = ldm_sdf.decode_points(dec, st.latents[:1], xyz[0, :256], dtype="fp32")
     assert torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_linear_mask_r_epilogue(dev, compute):
+    """LDM_EPI_MASK_R (the fused ReLU backward of the G W products): Y = R > 0 ? pre : 0."""
+    from ldm_sdf import ops, _capi as capi
+    cp = capi.COMPUTE_CODES[compute]
+    g = torch.Generator().manual_seed(4)
+    G = torch.randn(300, 128, generator=g).to(dev)
+    W = torch.randn(128, 200, generator=g).to(dev)          # W.T: [200, 128] rows contiguous
+    R = torch.randn(300, 200, generator=g).clamp_min(0).to(dev)
+    Y = torch.empty(300, 200, device=dev)
+    ops.linear(G, W.T, Y, epi=capi.EPI_MASK_R, R=R, compute=cp)
+    rd = (lambda t: t.double()) if compute == "fp32" else (lambda t: t.float().bfloat16().double())
+    pre = rd(G) @ rd(W)
+    want = torch.where(R.double() > 0, pre, torch.zeros_like(pre))
+    assert (Y.double() - want).abs().max() < 1e-4
+    assert torch.equal(Y[R == 0], torch.zeros_like(Y[R == 0]))

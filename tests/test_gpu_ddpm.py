@@ -1,6 +1,7 @@
 """T2 DDPM-side parity on the MI355X: step / q_sample bit-exact vs the fp32 oracle, the fused
 linear kernel vs torch, denoiser forward + 20-step sampling trajectory + training gradients
 vs the fp64 oracle / goldens."""
+import ctypes
 import os
 
 import numpy as np
@@ -214,6 +215,30 @@ def test_linear_bf16_mfma(dev, wdt, Bn, M, K, K2):
     ops.linear(X, W, Y, epi=capi.EPI_RESID_SILU, bias=b, R=R_, A_out=A, compute=BF, **kw)
     assert (A.double() - ref).abs().max() < tol
     assert (Y.double() - (R_.double() + ref * torch.sigmoid(ref))).abs().max() < 2 * tol
+
+
+@pytest.mark.parametrize("Bn,M,K,epi", [(1, 512, 300001, "bias"), (64, 70, 100003, "relu"),
+                                         (130, 64, 50000, "accum")])
+def test_linear_bf16_split_k(dev, Bn, M, K, epi):
+    """Few output tiles x long K (C19's G^T X over ~1M samples): the split-K path (workspace
+    from ldm_linear_workspace_floats, fixed-order slice reduce) against the fp64 product of
+    the bf16-rounded operands, through transposed views, with its epilogues."""
+    from ldm_sdf import ops, _capi as capi
+    BF = capi.COMPUTE_BF16
+    g = torch.Generator().manual_seed(K)
+    Gt = torch.randn(K, Bn, generator=g).to(dev)          # X = Gt.T: [Bn, K], k-stride Bn
+    Xs = torch.randn(K, M, generator=g).to(dev)           # W = Xs.T: [M, K]
+    b = torch.randn(M, generator=g).to(dev)
+    Y0 = torch.randn(Bn, M, generator=g).to(dev)
+    a = capi.LinearArgs()
+    a.Bn, a.M, a.K, a.compute = Bn, M, K, BF
+    assert capi.load().ldm_linear_workspace_floats(ctypes.byref(a)) > 0   # split engages
+    Y = Y0.clone()
+    e = {"bias": capi.EPI_BIAS, "relu": capi.EPI_RELU, "accum": capi.EPI_ACCUM}[epi]
+    ops.linear(Gt.T, Xs.T, Y, epi=e, bias=b, compute=BF)
+    pre = _bf(Gt).T @ _bf(Xs) + b.double()
+    want = {"bias": pre, "relu": pre.clamp_min(0), "accum": Y0.double() + pre}[epi]
+    assert (Y.double() - want).abs().max() < 2e-6 * K ** 0.5 * 4
 
 
 def test_train_step_bf16_grads_close_to_fp64(dev, den):
