@@ -11,7 +11,7 @@ from .mesh import marching_cubes, marching_cubes_batch, mc_table, write_ply  # n
 from .api import Sampler, TrainState, decode, decode_points, sample, train, train_step  # noqa: F401
 from .autodecoder import (AutoDecoderState, autodecoder_train_step,  # noqa: F401
                           train_autodecoder)
-from . import ops, dist, pack  # noqa: F401
+from . import ops, dist, pack, data  # noqa: F401
 from ._capi import LdmError, load as load_library  # noqa: F401
 
 __version__ = "0.1.0"
