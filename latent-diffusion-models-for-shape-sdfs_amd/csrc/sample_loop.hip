@@ -1,0 +1,326 @@
+// A10 as ONE launch: the whole T-step DDPM reverse loop of the MLP denoiser in a persistent,
+// cooperatively launched kernel (SURVEY.md §8(a) A6 + A8 + A10).
+//
+// Why: the graph-replayed loop (denoiser.hip small_linear_v4) is 6 dependent launches per step
+// at the ~5 us floor of a dependent launch; the GEMVs themselves are far from any bandwidth
+// limit.  Here the grid is H/4 workgroups of 4 waves, one wave per output row, and
+//   * every wave keeps ITS weight rows in registers for the whole loop (in-proj row, one row of
+//     each block, one out-proj row when gw < D: 88 fp32 values per lane at D=256, H=1024), so
+//     the 9.45 MB of bf16 weights are read from HBM once per loop instead of once per step;
+//   * the layer boundary is a grid barrier (write-through sc1 activation stores, one agent
+//     atomic per workgroup, sc1 polling with s_sleep, sc1 loads of the activations) instead of
+//     a kernel boundary;
+//   * per layer each workgroup stages the [B][K] activations into LDS once.
+// Arithmetic is the v4 GEMV's exactly (same k-to-lane mapping, same fma order, same shuffle
+// reduce-scatter, same epilogues), so the loop is bit-identical to the graph path
+// (tests/test_gpu_ddpm.py::test_sample_loop_persistent_matches_graph).
+//
+// Termination: every barrier wait is bounded (kSpinLimit polls); a workgroup that times out
+// raises an abort flag that every other waiter also polls, so all waves exit and the host
+// sees LDM_ETIMEOUT-style failure through the status word instead of a hung GPU.
+#include "ldm_internal.h"
+#include "ddpm_common.h"
+
+namespace ldm {
+namespace {
+
+constexpr unsigned kSpinLimit = 1u << 22;   // x s_sleep(2) ~ 0.3 s per barrier, worst case
+
+struct LoopArgs {
+    const void* w_in;  const float* b_in;     // [H][D]
+    const void* w_blk[4];                     // [H][2H] (the W_k half is read; U_k is in e_tab)
+    const float* e_tab[4];                    // [T][H]
+    const void* w_out; const float* b_out;    // [D][H]
+    const float* c1; const float* c2; const float* sg;
+    float* x;              // [2][B][D] ping-pong, x[0] = x_T; result in x[steps & 1]
+    const float* noise;    // [T][B][D]
+    float* h;              // [2][B][H]
+    unsigned* ctr;         // barrier counter (zeroed by the host before the launch)
+    unsigned* status;      // [0] abort flag
+    int B, D, H, t_hi, steps;
+};
+
+template <typename TW, int NJ>
+__device__ __forceinline__ void load_row(float (&w)[NJ][8], const void* W, int row, int ldw,
+                                         int K, int lane) {
+    const int nch = K >> 3;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        const bool on = c < nch;
+        const size_t off = (size_t)row * ldw + (on ? c : 0) * 8;
+        if constexpr (sizeof(TW) == 2) {
+            uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const unsigned short*>(W) + off);
+            const unsigned q[4] = {on ? u.x : 0u, on ? u.y : 0u, on ? u.z : 0u, on ? u.w : 0u};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[j][2 * i] = __builtin_bit_cast(float, q[i] << 16);
+                w[j][2 * i + 1] = __builtin_bit_cast(float, q[i] & 0xffff0000u);
+            }
+        } else {
+            const float* wp = reinterpret_cast<const float*>(W) + off;
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(wp);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(wp + 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[j][i] = on ? w0[i] : 0.f;
+                w[j][4 + i] = on ? w1[i] : 0.f;
+            }
+        }
+    }
+}
+
+// [B][K] fp32 activations -> LDS.  The activations were written by other workgroups in this
+// launch, so EVERY load of them is an agent-scope relaxed 8-byte load (global_load_dwordx2 sc1:
+// bypasses this CU's L1, served coherently; Guideline 16 table row 1), 8 in flight per thread.
+typedef unsigned long long u64;
+__device__ __forceinline__ void stage(float* xs, const float* X, int n2) {
+    const u64* X2 = reinterpret_cast<const u64*>(X);
+    for (int base = 0; base < n2; base += 256 * 8) {
+        u64 t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 256 + (int)threadIdx.x;
+            t[u] = __hip_atomic_load(X2 + (i < n2 ? i : 0), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 256 + (int)threadIdx.x;
+            if (i < n2) reinterpret_cast<u64*>(xs)[i] = t[u];
+        }
+    }
+}
+
+// Hand-off store of one activation: write-through (sc1) 4-byte store, no release fence needed.
+__device__ __forceinline__ void publish(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __builtin_bit_cast(unsigned, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave's row dot products for all batch rows, reduced so that lane `writer` of group b
+// holds acc[0] = sum_k X[b][k] w[k] (v4's reduce-scatter).  Returns acc[0].
+template <int MB, int NJ>
+__device__ __forceinline__ float row_dot(const float (&w)[NJ][8], const float* xs, int B, int K,
+                                         int lane) {
+    const int nch = K >> 3;
+    float acc[MB];
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[b] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        const int cc = c < nch ? c : 0;
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+            const int bb = b < B ? b : 0;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(xs + bb * K + cc * 8);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(xs + bb * K + cc * 8 + 4);
+            float t = acc[b];
+            t = fmaf(w[j][0], x0[0], t); t = fmaf(w[j][1], x0[1], t);
+            t = fmaf(w[j][2], x0[2], t); t = fmaf(w[j][3], x0[3], t);
+            t = fmaf(w[j][4], x1[0], t); t = fmaf(w[j][5], x1[1], t);
+            t = fmaf(w[j][6], x1[2], t); t = fmaf(w[j][7], x1[3], t);
+            acc[b] = t;
+        }
+    }
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        const int o = 32 >> lv;
+        const int n = MB >> lv;
+        const bool upper = (lane & o) != 0;
+        if (n > 1) {
+            const int half = n >> 1;
+#pragma unroll
+            for (int i = 0; i < half; ++i) {
+                const float send = upper ? acc[i] : acc[i + half];
+                const float keep = upper ? acc[i + half] : acc[i];
+                acc[i] = keep + __shfl_xor(send, o);
+            }
+        } else {
+            acc[0] += __shfl_xor(acc[0], o);
+        }
+    }
+    return acc[0];
+}
+
+// Grid barrier (MI355X guide, Guideline 16 table row 1): every wave drains its sc1 stores,
+// workgroup barrier, ONE lane adds to the monotonic counter (agent atomic) and polls it with
+// relaxed sc1 loads + s_sleep; the other waves wait at the workgroup barrier.  All later loads
+// of handed-off bytes are sc1 loads (stage()), so no acquire fence is needed.  Bounded: a
+// timeout raises status[0], which every poller also watches, so every workgroup exits.
+__device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned* status, unsigned target,
+                                          int* ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int good = 1;
+        unsigned spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if ((spins & 63) == 63 &&
+                __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                good = 0;
+                break;
+            }
+            if (++spins > kSpinLimit) {
+                __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                good = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *ok = good;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: no hoisting
+    __syncthreads();
+    return *ok != 0;
+}
+
+template <typename TW, int MB, int NJD, int NJH, int NB>
+__global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];  // [4] flag words, [B][max(D,H)]
+    int* ok = reinterpret_cast<int*>(smem);
+    float* xs = smem + 4;
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);           // this wave's row
+    const bool has_out = m < a.D;
+    const int mo = has_out ? m : a.D - 1;
+    const int B = a.B, D = a.D, H = a.H;
+
+    float wi[NJD][8], wb[NB][NJH][8], wo[NJH][8];
+    load_row<TW, NJD>(wi, a.w_in, m, D, D, lane);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) load_row<TW, NJH>(wb[k], a.w_blk[k], m, 2 * H, H, lane);
+    load_row<TW, NJH>(wo, a.w_out, mo, H, H, lane);
+    const float bi = a.b_in[m];
+    const float bo = a.b_out[mo];
+
+    constexpr int LB = (MB >= 16) ? 4 : 3;
+    const int b = lane >> (6 - LB);
+    const bool writer = (lane & ((1 << (6 - LB)) - 1)) == 0 && b < B;
+    const unsigned G = gridDim.x;
+    unsigned phase = 0;
+
+    for (int s = 0; s < a.steps; ++s) {
+        const int t = a.t_hi - s;
+        const float* xin = a.x + (size_t)(s & 1) * B * D;
+        float* xout = a.x + (size_t)((s & 1) ^ 1) * B * D;
+        // in-projection: h0 = W_in x + b_in
+        stage(xs, xin, (B * D) >> 1);
+        __syncthreads();
+        {
+            const float acc = row_dot<MB, NJD>(wi, xs, B, D, lane);
+            if (writer) publish(a.h + (size_t)b * H + m, acc + bi);
+        }
+        if (!grid_sync(a.ctr, a.status, ++phase * G, ok)) return;
+        // residual blocks: h <- h + SiLU(W_k h + E_k[t])
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const float* hin = a.h + (size_t)(k & 1) * B * H;
+            float* hout = a.h + (size_t)((k + 1) & 1) * B * H;
+            stage(xs, hin, (B * H) >> 1);
+            __syncthreads();
+            const float acc = row_dot<MB, NJH>(wb[k], xs, B, H, lane);
+            if (writer) {
+                const float pre = acc + a.e_tab[k][(size_t)t * H + m];
+                publish(hout + (size_t)b * H + m, xs[b * H + m] + silu(pre));
+            }
+            if (!grid_sync(a.ctr, a.status, ++phase * G, ok)) return;
+        }
+        // out-projection with the A8 update fused
+        stage(xs, a.h + (size_t)(NB & 1) * B * H, (B * H) >> 1);
+        __syncthreads();
+        if (has_out) {
+            const float acc = row_dot<MB, NJH>(wo, xs, B, H, lane);
+            if (writer) {
+                const float pre = acc + bo;
+                const size_t i = (size_t)b * D + m;
+                const bool noise = t > 0;
+                const float zz = noise ? a.noise[(size_t)t * B * D + i] : 0.f;
+                const float xv = __builtin_bit_cast(float, __hip_atomic_load(
+                    reinterpret_cast<const unsigned*>(xin + i), __ATOMIC_RELAXED,
+                    __HIP_MEMORY_SCOPE_AGENT));
+                publish(xout + i, ddpm_update(xv, pre, zz, a.c1[t], a.c2[t], a.sg[t], noise));
+            }
+        }
+        if (!grid_sync(a.ctr, a.status, ++phase * G, ok)) return;
+    }
+}
+
+template <typename TW, int MB>
+int launch_loop(const LoopArgs& a, int nblk, hipStream_t s) {
+    const size_t lds = 16 + (size_t)a.B * (a.H > a.D ? a.H : a.D) * sizeof(float);
+    const dim3 grid(a.H / 4), block(256);
+    void* args[] = {const_cast<LoopArgs*>(&a)};
+    hipError_t e = hipErrorInvalidValue;
+    if (a.D == 256 && a.H == 1024 && nblk == 4)
+        e = hipLaunchCooperativeKernel((const void*)sample_loop_kernel<TW, MB, 1, 2, 4>, grid,
+                                       block, args, lds, s);
+    else if (a.D == 512 && a.H == 1024 && nblk == 4)
+        e = hipLaunchCooperativeKernel((const void*)sample_loop_kernel<TW, MB, 1, 2, 4>, grid,
+                                       block, args, lds, s);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("sample_loop: cooperative launch failed: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return 0;
+}
+
+}  // namespace
+}  // namespace ldm
+
+using namespace ldm;
+
+extern "C" size_t ldm_sample_loop_ws_bytes(int B, int H) {
+    return (size_t)2 * B * H * sizeof(float) + 256;
+}
+
+extern "C" int ldm_sample_loop_supported(const ldm_denoiser_t* w, int B) {
+    if (!w || B < 1 || B > 16) return 0;
+    if (w->n_blocks != 4 || w->H != 1024) return 0;
+    if (w->D != 256 && w->D != 512) return 0;
+    return w->dtype == LDM_BF16 || w->dtype == LDM_F32;
+}
+
+extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, float* x,
+                               const float* noise, int t_hi, int steps, int B, float* ws,
+                               size_t ws_bytes, ldm_stream_t s) {
+    LDM_REQUIRE(w && sc && x && noise && ws, LDM_EINVAL, "sample_loop: null argument");
+    LDM_REQUIRE(ldm_sample_loop_supported(w, B), LDM_ENOSYS,
+                "sample_loop: persistent path needs H=1024, D in {256,512}, 4 blocks, B<=16 "
+                "(got H=%d D=%d blocks=%d B=%d)", w->H, w->D, w->n_blocks, B);
+    LDM_REQUIRE(steps >= 1 && t_hi >= 0 && t_hi < w->T && t_hi < sc->T && t_hi - steps + 1 >= 0,
+                LDM_EINVAL, "sample_loop: steps %d from t=%d outside the schedule", steps, t_hi);
+    LDM_REQUIRE(ws_bytes >= ldm_sample_loop_ws_bytes(B, w->H), LDM_EINVAL,
+                "sample_loop: workspace %zu B < %zu B", ws_bytes, ldm_sample_loop_ws_bytes(B, w->H));
+    LDM_REQUIRE(LDM_ALIGNED(x, 16) && LDM_ALIGNED(ws, 256) && LDM_ALIGNED(noise, 16),
+                LDM_EALIGN, "sample_loop: misaligned buffers");
+    LoopArgs a = {};
+    a.w_in = w->w_in; a.b_in = w->b_in;
+    for (int k = 0; k < 4; ++k) { a.w_blk[k] = w->w_blk[k]; a.e_tab[k] = w->e_tab[k]; }
+    a.w_out = w->w_out; a.b_out = w->b_out;
+    a.c1 = sc->c1; a.c2 = sc->c2; a.sg = sc->sigma;
+    a.x = x; a.noise = noise;
+    a.h = ws;
+    a.ctr = reinterpret_cast<unsigned*>(ws + (size_t)2 * B * w->H);
+    a.status = a.ctr + 32;                    // separate 128-byte line from the counter
+    a.B = B; a.D = w->D; a.H = w->H; a.t_hi = t_hi; a.steps = steps;
+    for (int k = 0; k < 4; ++k)
+        LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
+    hipStream_t st = (hipStream_t)s;
+    if (hipMemsetAsync(a.ctr, 0, 256, st) != hipSuccess) return launch_status("sample_loop memset");
+    if (w->dtype == LDM_BF16)
+        return B <= 8 ? launch_loop<unsigned short, 8>(a, 4, st) : launch_loop<unsigned short, 16>(a, 4, st);
+    return B <= 8 ? launch_loop<float, 8>(a, 4, st) : launch_loop<float, 16>(a, 4, st);
+}
+
+extern "C" int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host,
+                                      ldm_stream_t s) {
+    const unsigned* st = reinterpret_cast<const unsigned*>(ws + (size_t)2 * B * H) + 32;
+    hipError_t e = hipMemcpyAsync(status_host, st, sizeof(unsigned), hipMemcpyDeviceToHost,
+                                  (hipStream_t)s);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
+    return e == hipSuccess ? 0 : (int)e;
+}

@@ -109,6 +109,11 @@ SIGNATURES = [
     ("ldm_denoiser_fwd_uniform_t", _i, [C.POINTER(Denoiser), _fp, _i, _i, _fp, _fp, _vp]),
     ("ldm_sample_step", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _i, _i, _fp,
                              _fp, _vp]),
+    ("ldm_sample_loop_supported", _i, [C.POINTER(Denoiser), _i]),
+    ("ldm_sample_loop_ws_bytes", _sz, [_i, _i]),
+    ("ldm_sample_loop", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _i, _i, _i, _fp,
+                             _sz, _vp]),
+    ("ldm_sample_loop_status", _i, [_fp, _i, _i, C.POINTER(C.c_uint), _vp]),
     ("ldm_linear", _i, [C.POINTER(LinearArgs), _vp]),
     ("ldm_linear_workspace_floats", C.c_int64, [C.POINTER(LinearArgs)]),
     ("ldm_silu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),

@@ -81,7 +81,7 @@ class Sampler:
 
     def __init__(self, denoiser, schedule: DDPMSchedule, n: int, *,
                  steps: Optional[int] = None, dtype: str = "bf16", device=None,
-                 use_graph: bool = True):
+                 use_graph: bool = True, persistent: Optional[bool] = None):
         self.device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
         self.model, self.schedule, self.n = denoiser, schedule, n
         self.T = schedule.T
@@ -90,11 +90,21 @@ class Sampler:
             raise ValueError("steps must be in [1, T]")
         self.sd = schedule.device(self.device)
         D = denoiser.D
-        self.x = [torch.empty(n, D, device=self.device) for _ in range(2)]
+        self.x2 = torch.empty(2, n, D, device=self.device)
+        self.x = [self.x2[0], self.x2[1]]
         self.noise = torch.empty(self.T, n, D, device=self.device)
         self.step = denoiser.make_stepper(n, dtype, self.device, self.sd["desc"])
         self.graph = None
         self.use_graph = use_graph
+        # persistent=True: the whole loop as one cooperative launch (ldm_sample_loop), bit-
+        # identical but slower on MI355X (grid barriers cost more than kernel boundaries:
+        # DESIGN.md §5); default False/None: per-step launches, graph-replayed when use_graph.
+        make_loop = getattr(denoiser, "make_loop", None)
+        self.loop = None
+        if persistent and make_loop is not None:
+            self.loop = make_loop(n, dtype, self.device, self.sd["desc"])
+        if persistent and self.loop is None:
+            raise RuntimeError("no persistent sampling kernel for this denoiser/batch")
 
     def _loop(self) -> None:
         cur = 0
@@ -109,6 +119,9 @@ class Sampler:
     def run(self, x_T: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
         self.x[0].copy_(x_T)
         self.noise[:noise.shape[0]].copy_(noise)
+        if self.loop is not None:
+            self.loop(self.x2, self.noise, self.T - 1, self.steps)
+            return self.result
         if not self.use_graph:
             self._loop()
             return self.result
@@ -130,7 +143,8 @@ class Sampler:
 def sample(denoiser, schedule: DDPMSchedule, n: int, *,
            steps: Optional[int] = None, dtype: str = "bf16", x_T: Optional[torch.Tensor] = None,
            noise: Optional[torch.Tensor] = None, generator: Optional[torch.Generator] = None,
-           device=None, use_graph: bool = True, group=None) -> torch.Tensor:
+           device=None, use_graph: bool = True, persistent: Optional[bool] = None,
+           group=None) -> torch.Tensor:
     """DDPM ancestral sampling (DDPM Alg. 2) of ``n`` latent codes.
 
     ``x_T [n, D]`` and ``noise [T, n, D]`` may be given (parity mode: the same numbers the
@@ -149,7 +163,7 @@ def sample(denoiser, schedule: DDPMSchedule, n: int, *,
     x_T = x_T.to(device, torch.float32)[lo:hi].contiguous()
     noise = noise.to(device, torch.float32)[:, lo:hi].contiguous()
     out = Sampler(denoiser, schedule, nl, steps=steps, dtype=dtype, device=device,
-                  use_graph=use_graph).run(x_T, noise).clone()
+                  use_graph=use_graph, persistent=persistent).run(x_T, noise).clone()
     return ldist.all_gather_rows(out, n, group=group)
 
 

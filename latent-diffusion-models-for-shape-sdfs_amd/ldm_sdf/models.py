@@ -252,6 +252,22 @@ class MLPDenoiser:
             ops.sample_step(desc, sched_desc, x, z, t, x_out, ws)
         return step
 
+    def make_loop(self, n: int, dtype: str, device, sched_desc):
+        """Callable ``loop(x2, noise, t_hi, steps)`` running the whole reverse loop as one
+        persistent launch (``ldm_sample_loop``), or None when the shape has no persistent
+        kernel (the per-step stepper is used then)."""
+        from . import ops
+        desc = self.device_pack(dtype, device)["desc"]
+        if not ops.sample_loop_supported(desc, n):
+            return None
+        ws = ops.sample_loop_workspace(desc, n, device)
+
+        def loop(x2, noise, t_hi, steps):
+            ops.sample_loop(desc, sched_desc, x2, noise, t_hi, steps, ws)
+            return ws
+        loop.status = lambda: ops.sample_loop_status(desc, ws, n)
+        return loop
+
     def device_pack(self, dtype: str, device, with_tables: bool = True) -> Dict[str, object]:
         """Weights in ``dtype`` on ``device`` + the per-block E tables (A5):
         ``E_k[t] = U_k temb(t) + b_k`` for all t, computed with the device GEMM kernel."""

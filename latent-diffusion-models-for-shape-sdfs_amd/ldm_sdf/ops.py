@@ -164,6 +164,37 @@ def sample_step(desc: capi.Denoiser, sched_desc: capi.Sched, x: torch.Tensor,
                "ldm_sample_step")
 
 
+def sample_loop_supported(desc: capi.Denoiser, B: int) -> bool:
+    return bool(capi.load().ldm_sample_loop_supported(C.byref(desc), int(B)))
+
+
+def sample_loop_workspace(desc: capi.Denoiser, B: int, device) -> torch.Tensor:
+    nbytes = int(capi.load().ldm_sample_loop_ws_bytes(int(B), desc.H))
+    return torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32)
+
+
+def sample_loop(desc: capi.Denoiser, sched_desc: capi.Sched, x2: torch.Tensor,
+                noise: torch.Tensor, t_hi: int, steps: int, ws: torch.Tensor) -> None:
+    """A10 in one persistent launch (``ldm_sample_loop``): ``x2 [2, B, D]`` holds x_T in
+    ``x2[0]`` and the result in ``x2[steps & 1]``; ``noise [T, B, D]``."""
+    B = x2.shape[1]
+    capi.check(capi.load().ldm_sample_loop(C.byref(desc), C.byref(sched_desc), x2.data_ptr(),
+                                           noise.data_ptr(), int(t_hi), int(steps), B,
+                                           ws.data_ptr(), ws.numel() * 4,
+                                           capi.stream_handle(x2.device)),
+               "ldm_sample_loop")
+
+
+def sample_loop_status(desc: capi.Denoiser, ws: torch.Tensor, B: int) -> int:
+    """0 when the last ``sample_loop`` on ``ws`` completed, 1 when a barrier timed out.
+    Synchronises the stream."""
+    st = C.c_uint(0)
+    capi.check(capi.load().ldm_sample_loop_status(ws.data_ptr(), int(B), desc.H, C.byref(st),
+                                                  capi.stream_handle(ws.device)),
+               "ldm_sample_loop_status")
+    return int(st.value)
+
+
 # ---------------------------------------------------------------------------------------- GEMM
 def linear(X: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, *, epi: int = capi.EPI_BIAS,
            bias: Optional[torch.Tensor] = None, X2: Optional[torch.Tensor] = None,

@@ -127,8 +127,8 @@ def test_denoiser_forward_vs_golden(dev, den):
     assert err < 1e-4 * max(1.0, np.abs(want).max()), err
 
 
-@pytest.mark.parametrize("use_graph", [False, True])
-def test_sampling_20_steps_vs_golden(dev, den, use_graph):
+@pytest.mark.parametrize("use_graph,persistent", [(False, False), (True, False), (False, True)])
+def test_sampling_20_steps_vs_golden(dev, den, use_graph, persistent):
     import ldm_sdf
     model, p = den
     g = dict(np.load(os.path.join(GOLD, "sampling_20.npz")))
@@ -137,7 +137,7 @@ def test_sampling_20_steps_vs_golden(dev, den, use_graph):
     noise[1000 - steps:] = torch.from_numpy(g["noise_tail"])
     x = ldm_sdf.sample(model, ldm_sdf.DDPMSchedule(), 4, steps=steps, dtype="fp32",
                        x_T=torch.from_numpy(g["x_T"]), noise=noise, device=dev,
-                       use_graph=use_graph)
+                       use_graph=use_graph, persistent=persistent)
     want = g["traj"][-1]
     err = np.abs(x.cpu().double().numpy() - want).max()
     assert err < 1e-4, err
@@ -150,10 +150,46 @@ def test_sampling_graph_equals_eager_bf16(dev, den):
     xT = torch.randn(8, 256, generator=gen)
     noise = torch.randn(1000, 8, 256, generator=gen)
     sch = ldm_sdf.DDPMSchedule()
-    a = ldm_sdf.sample(model, sch, 8, steps=50, x_T=xT, noise=noise, device=dev, use_graph=False)
-    b = ldm_sdf.sample(model, sch, 8, steps=50, x_T=xT, noise=noise, device=dev, use_graph=True)
+    a = ldm_sdf.sample(model, sch, 8, steps=50, x_T=xT, noise=noise, device=dev, use_graph=False,
+                       persistent=False)
+    b = ldm_sdf.sample(model, sch, 8, steps=50, x_T=xT, noise=noise, device=dev, use_graph=True,
+                       persistent=False)
     assert torch.equal(a, b)
     assert torch.isfinite(a).all()
+
+
+@pytest.mark.parametrize("dtype,n,steps", [("bf16", 8, 1000), ("bf16", 1, 40), ("bf16", 5, 40),
+                                           ("bf16", 16, 40), ("fp32", 8, 40), ("fp32", 13, 40)])
+def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps):
+    """The one-launch loop (ldm_sample_loop) is bit-identical to the per-step launches: same
+    k-to-lane mapping, fma order, shuffle reduce and epilogues; every barrier completed."""
+    import ldm_sdf
+    model, _ = den
+    gen = torch.Generator().manual_seed(11 + n)
+    xT = torch.randn(n, 256, generator=gen).to(dev)
+    noise = torch.randn(1000, n, 256, generator=gen).to(dev)
+    sch = ldm_sdf.DDPMSchedule()
+    sp = ldm_sdf.Sampler(model, sch, n, steps=steps, dtype=dtype, device=dev, persistent=True)
+    sg = ldm_sdf.Sampler(model, sch, n, steps=steps, dtype=dtype, device=dev, persistent=False)
+    a = sp.run(xT, noise).clone()
+    assert sp.loop.status() == 0
+    b = sg.run(xT, noise).clone()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), float((a - b).abs().max())
+    # replay: the counter/status words are re-zeroed per call, so a second run is identical
+    c = sp.run(xT, noise).clone()
+    assert sp.loop.status() == 0 and torch.equal(a, c)
+
+
+def test_sample_loop_rejects_unsupported(dev):
+    """Shapes without a persistent kernel: ENOSYS through the C ABI, graph path in Sampler."""
+    import ldm_sdf
+    small = ldm_sdf.MLPDenoiser(D=64, H=256, n_blocks=2, seed=3)
+    sch = ldm_sdf.DDPMSchedule()
+    s = ldm_sdf.Sampler(small, sch, 4, steps=3, dtype="bf16", device=dev)
+    assert s.loop is None
+    with pytest.raises(RuntimeError):
+        ldm_sdf.Sampler(small, sch, 4, steps=3, dtype="bf16", device=dev, persistent=True)
 
 
 def test_train_step_grads_vs_golden(dev, den):
