@@ -21,6 +21,8 @@
 #include "ldm_internal.h"
 #include "ddpm_common.h"
 
+#include <stdlib.h>
+
 namespace ldm {
 namespace {
 
@@ -35,9 +37,11 @@ struct LoopArgs {
     float* x;              // [2][B][D] ping-pong, x[0] = x_T; result in x[steps & 1]
     const float* noise;    // [T][B][D]
     float* h;              // [2][B][H]
-    unsigned* ctr;         // barrier counter (zeroed by the host before the launch)
-    unsigned* status;      // [0] abort flag
+    unsigned* ctr;         // sync words (kSyncBytes, zeroed by the host before the launch):
+                           // one 128-B line each (32 words): see SyncLine
+    unsigned* status;      // abort flag (ctr + 32 * L_STATUS)
     int B, D, H, t_hi, steps;
+    int hier;              // 1: XCD-hierarchical barrier, 0: one flat counter
 };
 
 template <typename TW, int NJ>
@@ -177,6 +181,83 @@ __device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned* status, unsig
     return *ok != 0;
 }
 
+// XCD-hierarchical variant (the guide's barrier-xcd shape): only the last arriver of each XCD
+// touches the chip-wide counter; the others poll their XCD's generation word.  Arrival counts
+// per XCD come from a start-up census (every workgroup adds 1 to its XCD's count, then one flat
+// barrier).  Data hand-off rules are the flat barrier's (sc1 stores drained before the first
+// add, sc1 loads after the last poll).
+enum SyncLine { L_TOP = 0, L_STATUS = 1, L_START = 2, L_CNT = 3, L_ARR = 11, L_GEN = 19,
+                L_COUNT = 27 };
+constexpr size_t kSyncBytes = 4096;
+static_assert(L_COUNT * 128 <= (int)kSyncBytes, "sync words overflow");
+
+__device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, unsigned* status) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        if ((spins & 63) == 63 &&
+            __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+            return false;
+        if (++spins > kSpinLimit) {
+            __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
+struct XcdState { unsigned xcc, n_local, n_active; };
+
+__device__ __forceinline__ bool grid_sync_xcd(unsigned* sync, const XcdState& xs_,
+                                              unsigned phase, int* ok) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* status = sync + 32 * L_STATUS;
+        unsigned* gen = sync + 32 * (L_GEN + xs_.xcc);
+        const unsigned t = __hip_atomic_fetch_add(sync + 32 * (L_ARR + xs_.xcc), 1u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool good;
+        if (t + 1 == phase * xs_.n_local) {          // last of this XCD: go chip-wide
+            __hip_atomic_fetch_add(sync + 32 * L_TOP, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status);
+            if (good) __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            good = spin_until(gen, phase, status);
+        }
+        *ok = good;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    return *ok != 0;
+}
+
+// Start-up census for grid_sync_xcd: thread 0 of every workgroup learns its XCD, the number of
+// workgroups on it and the number of XCDs holding any.  Returns false on timeout.
+__device__ __forceinline__ bool xcd_census(unsigned* sync, unsigned G, XcdState* st, int* ok) {
+    if (threadIdx.x == 0) {
+        // HW_REG_XCC_ID (hwreg 20), bits [3:0]
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
+        __hip_atomic_fetch_add(sync + 32 * (L_CNT + xcc), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(sync + 32 * L_START, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        bool good = spin_until(sync + 32 * L_START, G, sync + 32 * L_STATUS);
+        unsigned n_act = 0, n_loc = 0;
+        for (unsigned x = 0; x < 8; ++x) {
+            const unsigned c = __hip_atomic_load(sync + 32 * (L_CNT + x), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            n_act += c > 0;
+            if (x == xcc) n_loc = c;
+        }
+        st->xcc = xcc; st->n_local = n_loc; st->n_active = n_act;
+        *ok = good;
+    }
+    __syncthreads();
+    return *ok != 0;
+}
+
 template <typename TW, int MB, int NJD, int NJH, int NB>
 __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];  // [4] flag words, [B][max(D,H)]
@@ -201,6 +282,8 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
     const bool writer = (lane & ((1 << (6 - LB)) - 1)) == 0 && b < B;
     const unsigned G = gridDim.x;
     unsigned phase = 0;
+    XcdState xst = {0, 0, 0};
+    if (a.hier && !xcd_census(a.ctr, G, &xst, ok)) return;
 
     for (int s = 0; s < a.steps; ++s) {
         const int t = a.t_hi - s;
@@ -213,7 +296,9 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
             const float acc = row_dot<MB, NJD>(wi, xs, B, D, lane);
             if (writer) publish(a.h + (size_t)b * H + m, acc + bi);
         }
-        if (!grid_sync(a.ctr, a.status, ++phase * G, ok)) return;
+        ++phase;
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok)
+                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
         // residual blocks: h <- h + SiLU(W_k h + E_k[t])
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
@@ -226,7 +311,9 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
                 const float pre = acc + a.e_tab[k][(size_t)t * H + m];
                 publish(hout + (size_t)b * H + m, xs[b * H + m] + silu(pre));
             }
-            if (!grid_sync(a.ctr, a.status, ++phase * G, ok)) return;
+            ++phase;
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok)
+                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
         }
         // out-projection with the A8 update fused
         stage(xs, a.h + (size_t)(NB & 1) * B * H, (B * H) >> 1);
@@ -244,7 +331,9 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
                 publish(xout + i, ddpm_update(xv, pre, zz, a.c1[t], a.c2[t], a.sg[t], noise));
             }
         }
-        if (!grid_sync(a.ctr, a.status, ++phase * G, ok)) return;
+        ++phase;
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok)
+                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
     }
 }
 
@@ -274,7 +363,7 @@ int launch_loop(const LoopArgs& a, int nblk, hipStream_t s) {
 using namespace ldm;
 
 extern "C" size_t ldm_sample_loop_ws_bytes(int B, int H) {
-    return (size_t)2 * B * H * sizeof(float) + 256;
+    return (size_t)2 * B * H * sizeof(float) + kSyncBytes;
 }
 
 extern "C" int ldm_sample_loop_supported(const ldm_denoiser_t* w, int B) {
@@ -305,12 +394,14 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
     a.x = x; a.noise = noise;
     a.h = ws;
     a.ctr = reinterpret_cast<unsigned*>(ws + (size_t)2 * B * w->H);
-    a.status = a.ctr + 32;                    // separate 128-byte line from the counter
+    a.status = a.ctr + 32 * L_STATUS;
+    const char* bar = getenv("LDM_SAMPLE_LOOP_BARRIER");
+    a.hier = !(bar && bar[0] == 'f');        // "flat" selects the single counter
     a.B = B; a.D = w->D; a.H = w->H; a.t_hi = t_hi; a.steps = steps;
     for (int k = 0; k < 4; ++k)
         LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
     hipStream_t st = (hipStream_t)s;
-    if (hipMemsetAsync(a.ctr, 0, 256, st) != hipSuccess) return launch_status("sample_loop memset");
+    if (hipMemsetAsync(a.ctr, 0, kSyncBytes, st) != hipSuccess) return launch_status("sample_loop memset");
     if (w->dtype == LDM_BF16)
         return B <= 8 ? launch_loop<unsigned short, 8>(a, 4, st) : launch_loop<unsigned short, 16>(a, 4, st);
     return B <= 8 ? launch_loop<float, 8>(a, 4, st) : launch_loop<float, 16>(a, 4, st);
@@ -318,7 +409,7 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
 
 extern "C" int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host,
                                       ldm_stream_t s) {
-    const unsigned* st = reinterpret_cast<const unsigned*>(ws + (size_t)2 * B * H) + 32;
+    const unsigned* st = reinterpret_cast<const unsigned*>(ws + (size_t)2 * B * H) + 32 * L_STATUS;
     hipError_t e = hipMemcpyAsync(status_host, st, sizeof(unsigned), hipMemcpyDeviceToHost,
                                   (hipStream_t)s);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);

@@ -96,12 +96,13 @@ class Sampler:
         self.step = denoiser.make_stepper(n, dtype, self.device, self.sd["desc"])
         self.graph = None
         self.use_graph = use_graph
-        # persistent=True: the whole loop as one cooperative launch (ldm_sample_loop), bit-
-        # identical but slower on MI355X (grid barriers cost more than kernel boundaries:
-        # DESIGN.md §5); default False/None: per-step launches, graph-replayed when use_graph.
+        # persistent=None (default): the whole loop as one cooperative launch (ldm_sample_loop,
+        # bit-identical, +10-13 % on MI355X: DESIGN.md §5) whenever the denoiser has a kernel
+        # for this shape, else per-step launches; True: require it; False: per-step launches,
+        # graph-replayed when use_graph.
         make_loop = getattr(denoiser, "make_loop", None)
         self.loop = None
-        if persistent and make_loop is not None:
+        if persistent is not False and make_loop is not None:
             self.loop = make_loop(n, dtype, self.device, self.sd["desc"])
         if persistent and self.loop is None:
             raise RuntimeError("no persistent sampling kernel for this denoiser/batch")

@@ -158,12 +158,16 @@ def test_sampling_graph_equals_eager_bf16(dev, den):
     assert torch.isfinite(a).all()
 
 
-@pytest.mark.parametrize("dtype,n,steps", [("bf16", 8, 1000), ("bf16", 1, 40), ("bf16", 5, 40),
-                                           ("bf16", 16, 40), ("fp32", 8, 40), ("fp32", 13, 40)])
-def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps):
+@pytest.mark.parametrize("dtype,n,steps,barrier",
+                         [("bf16", 8, 1000, "xcd"), ("bf16", 1, 40, "xcd"), ("bf16", 5, 40, "xcd"),
+                          ("bf16", 16, 40, "xcd"), ("fp32", 8, 40, "xcd"), ("fp32", 13, 40, "xcd"),
+                          ("bf16", 8, 200, "flat"), ("fp32", 3, 40, "flat")])
+def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps, barrier, monkeypatch):
     """The one-launch loop (ldm_sample_loop) is bit-identical to the per-step launches: same
-    k-to-lane mapping, fma order, shuffle reduce and epilogues; every barrier completed."""
+    k-to-lane mapping, fma order, shuffle reduce and epilogues; every barrier completed.  Both
+    grid barriers (XCD-hierarchical default, flat counter) are covered."""
     import ldm_sdf
+    monkeypatch.setenv("LDM_SAMPLE_LOOP_BARRIER", barrier)
     model, _ = den
     gen = torch.Generator().manual_seed(11 + n)
     xT = torch.randn(n, 256, generator=gen).to(dev)
