@@ -76,20 +76,26 @@ __device__ __forceinline__ void load_row(float (&w)[NJ][8], const void* W, int r
 
 // [B][K] fp32 activations -> LDS.  The activations were written by other workgroups in this
 // launch, so EVERY load of them is an agent-scope relaxed 8-byte load (global_load_dwordx2 sc1:
-// bypasses this CU's L1, served coherently; Guideline 16 table row 1), 8 in flight per thread.
+// bypasses this CU's L1, served coherently; Guideline 16 table row 1), 16 in flight per
+// thread: one round trip for B*K <= 8192 (B=8, K=1024).
 typedef unsigned long long u64;
+#ifndef LDM_STAGE_IN_FLIGHT
+#define LDM_STAGE_IN_FLIGHT 16
+#endif
+constexpr int kStageInFlight = LDM_STAGE_IN_FLIGHT;   // 8-B loads per thread per round
 __device__ __forceinline__ void stage(float* xs, const float* X, int n2) {
+    constexpr int U = kStageInFlight;
     const u64* X2 = reinterpret_cast<const u64*>(X);
-    for (int base = 0; base < n2; base += 256 * 8) {
-        u64 t[8];
+    for (int base = 0; base < n2; base += 256 * U) {
+        u64 t[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int i = base + u * 256 + (int)threadIdx.x;
             t[u] = __hip_atomic_load(X2 + (i < n2 ? i : 0), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int i = base + u * 256 + (int)threadIdx.x;
             if (i < n2) reinterpret_cast<u64*>(xs)[i] = t[u];
         }
