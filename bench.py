@@ -415,7 +415,7 @@ def main():
         wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nb * den.D * 4
         res["ddpm"] = {"metric": "DDPM sample steps/sec", "value": sps, "unit": "steps/s",
                        "batch": nb, "T": 1000, "shape_steps_per_s": sps * nb,
-                       "path": ("one persistent cooperative launch for all 1000 steps "
+                       "path": ("one persistent launch for all 1000 steps "
                                 "(weights in registers, XCD-hierarchical grid barrier per "
                                 "layer)" if persistent
                                 else "hipGraph of 1000 fused steps (6 kernels each)"),
@@ -426,7 +426,11 @@ def main():
                        "roofline": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
                                     "peak": 8000.0, "unit": "GB/s",
                                     "frac": sps * wbytes / 8e12,
-                                    "bytes_per_step": wbytes},
+                                    "bytes_per_step": wbytes,
+                                    "note": "SURVEY §8(d) bytes: weights streamed once per "
+                                            "step + x, eps; the persistent loop holds weights "
+                                            "in registers, so it is grid-barrier-latency-bound "
+                                            "(~5 us per layer, DESIGN.md §5)"},
                        "config3_sample_plus_decode128_s": e2e}
     if rank == 0 and not args.no_mc:
         res["mc"] = bench_mc(out[0], args)

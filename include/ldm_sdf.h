@@ -149,13 +149,14 @@ int ldm_denoiser_fwd_uniform_t(const ldm_denoiser_t* w, const float* x, int t, i
  * x_out = c1[t] (x - c2[t] net(x,t)) + sigma[t] z  (z ignored at t = 0).  x_out != x. */
 int ldm_sample_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x,
                     const float* z, int t, int B, float* x_out, float* ws, ldm_stream_t s);
-/* The whole A10 loop as one persistent cooperative launch: steps t_hi, t_hi-1, ...,
+/* The whole A10 loop as one persistent launch (whole grid resident): steps t_hi, t_hi-1, ...,
  * t_hi-steps+1 of ldm_sample_step, bit-identical to calling it per step.  x fp32 [2][B][D]
  * ping-pong with x[0] = x_T on entry; the result is x[steps & 1].  noise fp32 [T][B][D]
  * (noise[t] is the z of step t).  ws: ldm_sample_loop_ws_bytes(B, H) bytes, 256-byte aligned.
  * LDM_ENOSYS unless ldm_sample_loop_supported(w, B) (H = 1024, D in {256, 512}, 4 blocks,
- * B <= 16); callers then use ldm_sample_step.  Every grid barrier is bounded: after the
- * launch, ldm_sample_loop_status() reads back 0 (completed) or 1 (abandoned on a timeout). */
+ * B <= 16, and H/4 workgroups co-resident on the current device); callers then use
+ * ldm_sample_step.  Every grid barrier is bounded: after the launch,
+ * ldm_sample_loop_status() reads back 0 (completed) or 1 (abandoned on a timeout). */
 int ldm_sample_loop_supported(const ldm_denoiser_t* w, int B);
 size_t ldm_sample_loop_ws_bytes(int B, int H);
 int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, float* x, const float* noise,

@@ -1,5 +1,5 @@
 // A10 as ONE launch: the whole T-step DDPM reverse loop of the MLP denoiser in a persistent,
-// cooperatively launched kernel (SURVEY.md §8(a) A6 + A8 + A10).
+// kernel whose whole grid is resident (SURVEY.md §8(a) A6 + A8 + A10).
 //
 // Why: the graph-replayed loop (denoiser.hip small_linear_v4) is 6 dependent launches per step
 // at the ~5 us floor of a dependent launch; the GEMVs themselves are far from any bandwidth
@@ -41,7 +41,8 @@ struct LoopArgs {
                            // one 128-B line each (32 words): see SyncLine
     unsigned* status;      // abort flag (ctr + 32 * L_STATUS)
     int B, D, H, t_hi, steps;
-    int hier;              // 1: XCD-hierarchical barrier, 0: one flat counter
+    int hier;              // 1: XCD-hierarchical, 2: hierarchical arrival + direct poll,
+                           // 0: one flat counter
 };
 
 template <typename TW, int NJ>
@@ -215,7 +216,7 @@ __device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, u
 struct XcdState { unsigned xcc, n_local, n_active; };
 
 __device__ __forceinline__ bool grid_sync_xcd(unsigned* sync, const XcdState& xs_,
-                                              unsigned phase, int* ok) {
+                                              unsigned phase, int* ok, bool direct) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -224,9 +225,13 @@ __device__ __forceinline__ bool grid_sync_xcd(unsigned* sync, const XcdState& xs
         const unsigned t = __hip_atomic_fetch_add(sync + 32 * (L_ARR + xs_.xcc), 1u,
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool good;
-        if (t + 1 == phase * xs_.n_local) {          // last of this XCD: go chip-wide
+        const bool last = t + 1 == phase * xs_.n_local;   // last of this XCD: go chip-wide
+        if (last)
             __hip_atomic_fetch_add(sync + 32 * L_TOP, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+        if (direct) {                                  // everyone polls the chip-wide word
+            good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status);
+        } else if (last) {
             good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status);
             if (good) __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
             if (writer) publish(a.h + (size_t)b * H + m, acc + bi);
         }
         ++phase;
-        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok)
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2)
                      : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
         // residual blocks: h <- h + SiLU(W_k h + E_k[t])
 #pragma unroll
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
                 publish(hout + (size_t)b * H + m, xs[b * H + m] + silu(pre));
             }
             ++phase;
-        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok)
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2)
                      : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
         }
         // out-projection with the A8 update fused
@@ -338,29 +343,40 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
             }
         }
         ++phase;
-        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok)
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2)
                      : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
     }
 }
 
+// Residency: every workgroup of the grid must be resident at once (the grid barriers wait for
+// all of them).  Checked against the occupancy query x CU count before each plain launch; a
+// cooperative launch would make the same check at +15-19 us per call (MI355X guide,
+// coop-launch) and crashed rocprofv3 at process exit here.  Spins stay bounded regardless.
 template <typename TW, int MB>
-int launch_loop(const LoopArgs& a, int nblk, hipStream_t s) {
+bool loop_resident(int B, int D, int H) {
+    const size_t lds = 16 + (size_t)B * (H > D ? H : D) * sizeof(float);
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, (const void*)sample_loop_kernel<TW, MB, 1, 2, 4>, 256, lds) != hipSuccess)
+        return false;
+    return (long)per_cu * cus >= H / 4;
+}
+
+bool loop_resident_any(int dtype, int B, int D, int H) {
+    if (dtype == LDM_BF16)
+        return B <= 8 ? loop_resident<unsigned short, 8>(B, D, H)
+                      : loop_resident<unsigned short, 16>(B, D, H);
+    return B <= 8 ? loop_resident<float, 8>(B, D, H) : loop_resident<float, 16>(B, D, H);
+}
+
+template <typename TW, int MB>
+int launch_loop(const LoopArgs& a, hipStream_t s) {
     const size_t lds = 16 + (size_t)a.B * (a.H > a.D ? a.H : a.D) * sizeof(float);
-    const dim3 grid(a.H / 4), block(256);
-    void* args[] = {const_cast<LoopArgs*>(&a)};
-    hipError_t e = hipErrorInvalidValue;
-    if (a.D == 256 && a.H == 1024 && nblk == 4)
-        e = hipLaunchCooperativeKernel((const void*)sample_loop_kernel<TW, MB, 1, 2, 4>, grid,
-                                       block, args, lds, s);
-    else if (a.D == 512 && a.H == 1024 && nblk == 4)
-        e = hipLaunchCooperativeKernel((const void*)sample_loop_kernel<TW, MB, 1, 2, 4>, grid,
-                                       block, args, lds, s);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        set_error("sample_loop: cooperative launch failed: %s", hipGetErrorString(e));
-        return (int)e;
-    }
-    return 0;
+    hipLaunchKernelGGL((sample_loop_kernel<TW, MB, 1, 2, 4>), dim3(a.H / 4), dim3(256), lds, s, a);
+    return launch_status("sample_loop");
 }
 
 }  // namespace
@@ -376,7 +392,8 @@ extern "C" int ldm_sample_loop_supported(const ldm_denoiser_t* w, int B) {
     if (!w || B < 1 || B > 16) return 0;
     if (w->n_blocks != 4 || w->H != 1024) return 0;
     if (w->D != 256 && w->D != 512) return 0;
-    return w->dtype == LDM_BF16 || w->dtype == LDM_F32;
+    if (w->dtype != LDM_BF16 && w->dtype != LDM_F32) return 0;
+    return loop_resident_any(w->dtype, B, w->D, w->H) ? 1 : 0;
 }
 
 extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, float* x,
@@ -402,15 +419,17 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
     a.ctr = reinterpret_cast<unsigned*>(ws + (size_t)2 * B * w->H);
     a.status = a.ctr + 32 * L_STATUS;
     const char* bar = getenv("LDM_SAMPLE_LOOP_BARRIER");
-    a.hier = !(bar && bar[0] == 'f');        // "flat" selects the single counter
+    // default / "xcd": XCD-hierarchical with per-XCD generation words; "direct": hierarchical
+    // arrival, every workgroup polls the chip-wide word; "flat": one counter for everything
+    a.hier = (bar && bar[0] == 'f') ? 0 : (bar && bar[0] == 'd') ? 2 : 1;
     a.B = B; a.D = w->D; a.H = w->H; a.t_hi = t_hi; a.steps = steps;
     for (int k = 0; k < 4; ++k)
         LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
     hipStream_t st = (hipStream_t)s;
     if (hipMemsetAsync(a.ctr, 0, kSyncBytes, st) != hipSuccess) return launch_status("sample_loop memset");
     if (w->dtype == LDM_BF16)
-        return B <= 8 ? launch_loop<unsigned short, 8>(a, 4, st) : launch_loop<unsigned short, 16>(a, 4, st);
-    return B <= 8 ? launch_loop<float, 8>(a, 4, st) : launch_loop<float, 16>(a, 4, st);
+        return B <= 8 ? launch_loop<unsigned short, 8>(a, st) : launch_loop<unsigned short, 16>(a, st);
+    return B <= 8 ? launch_loop<float, 8>(a, st) : launch_loop<float, 16>(a, st);
 }
 
 extern "C" int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host,

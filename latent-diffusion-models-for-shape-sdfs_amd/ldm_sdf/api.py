@@ -96,7 +96,7 @@ class Sampler:
         self.step = denoiser.make_stepper(n, dtype, self.device, self.sd["desc"])
         self.graph = None
         self.use_graph = use_graph
-        # persistent=None (default): the whole loop as one cooperative launch (ldm_sample_loop,
+        # persistent=None (default): the whole loop as one persistent launch (ldm_sample_loop,
         # bit-identical, +10-13 % on MI355X: DESIGN.md §5) whenever the denoiser has a kernel
         # for this shape, else per-step launches; True: require it; False: per-step launches,
         # graph-replayed when use_graph.

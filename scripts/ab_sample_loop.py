@@ -35,7 +35,7 @@ res = {"batch": B}
 sg = ldm_sdf.Sampler(den, sch, B, dtype="bf16", device=dev)
 ref = sg.run(xT, noise).clone()
 res["graph_steps_per_s"] = timeit(sg)
-for mode in ("flat", "xcd"):
+for mode in ("flat", "xcd", "direct"):
     os.environ["LDM_SAMPLE_LOOP_BARRIER"] = mode
     sp = ldm_sdf.Sampler(den, sch, B, dtype="bf16", device=dev, persistent=True)
     out = sp.run(xT, noise).clone()
