@@ -57,12 +57,35 @@ struct Tile {
     static constexpr int VPL = LEN / EPV;             // vectors per line
     static constexpr int NV = E / EPV;                // vectors per thread
     static constexpr int TPL = LEN / E;               // scalar path: threads per line
+    static constexpr int RG = 64 / EPV;               // !KC vector path: row groups
+    static_assert(KC || !VEC || NV * (256 / RG) == kKC, "!KC vector tile covers the chunk");
     float v[E];
 
     __device__ __forceinline__ void load(const T* __restrict__ P, int64_t sr, int64_t sk,
                                          int rows, int K, int r0, int k0) {
         const int t = threadIdx.x;
-        if constexpr (VEC) {
+        if constexpr (VEC && !KC) {
+            // rows contiguous: thread owns EPV rows x NV consecutive k (one 16-byte load per
+            // k; 64/EPV lanes cover one k's 64 rows), so store() writes whole k-runs per row
+#pragma unroll
+            for (int u = 0; u < NV; ++u) {
+                const int r = r0 + (t % RG) * EPV, k = k0 + (t / RG) * NV + u;
+                const bool ok = r < rows && k < K;
+                const int64_t gi = ok ? (int64_t)r * sr + (int64_t)k * sk : 0;
+                u32x4 w = *reinterpret_cast<const u32x4*>(P + gi);
+                if (!ok) w = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned wq = w[q];
+                    if constexpr (sizeof(T) == 2) {
+                        v[u * 8 + 2 * q] = __builtin_bit_cast(float, wq << 16);
+                        v[u * 8 + 2 * q + 1] = __builtin_bit_cast(float, wq & 0xffff0000u);
+                    } else {
+                        v[u * 4 + q] = __builtin_bit_cast(float, wq);
+                    }
+                }
+            }
+        } else if constexpr (VEC) {
 #pragma unroll
             for (int u = 0; u < NV; ++u) {
                 const int id = u * 256 + t;
@@ -100,7 +123,28 @@ struct Tile {
     // S: [64 rows][kLd] bf16, row-major in (row, k) whatever the source layout.
     __device__ __forceinline__ void store(unsigned short* __restrict__ S) const {
         const int t = threadIdx.x;
-        if constexpr (VEC) {
+        if constexpr (VEC && !KC) {   // per row: NV consecutive k -> one 16-B (fp32 source,
+                                      // NV = 8) or 8-B (bf16 source, NV = 4) LDS store
+            const int rl = (t % RG) * EPV, kl = (t / RG) * NV;
+#pragma unroll
+            for (int q = 0; q < EPV; ++q) {
+                unsigned short* d = S + (rl + q) * kLd + kl;
+                if constexpr (NV == 8) {
+                    u32x4 w;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        w[c] = pack_bf16(v[(2 * c) * EPV + q], v[(2 * c + 1) * EPV + q]);
+                    *reinterpret_cast<u32x4*>(d) = w;
+                } else {
+                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                    u32x2 w;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        w[c] = pack_bf16(v[(2 * c) * EPV + q], v[(2 * c + 1) * EPV + q]);
+                    *reinterpret_cast<u32x2*>(d) = w;
+                }
+            }
+        } else if constexpr (VEC) {
 #pragma unroll
             for (int u = 0; u < NV; ++u) {
                 const int id = u * 256 + t;
