@@ -25,7 +25,10 @@
 namespace ldm {
 namespace {
 
-constexpr int kKC = 128;             // k per chunk
+#ifndef LDM_LINEAR_KC
+#define LDM_LINEAR_KC 128
+#endif
+constexpr int kKC = LDM_LINEAR_KC;   // k per chunk
 constexpr int kLd = kKC + 8;         // LDS row pitch (bf16 elements)
 constexpr int kBuf = 64 * kLd;       // one operand buffer (elements)
 constexpr int kLdsBytes = 4 * kBuf * (int)sizeof(unsigned short);   // X0 X1 W0 W1 = 68 KiB
@@ -135,13 +138,16 @@ struct Tile {
                     for (int c = 0; c < 4; ++c)
                         w[c] = pack_bf16(v[(2 * c) * EPV + q], v[(2 * c + 1) * EPV + q]);
                     *reinterpret_cast<u32x4*>(d) = w;
-                } else {
+                } else if constexpr (NV == 4) {
                     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
                     u32x2 w;
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
                         w[c] = pack_bf16(v[(2 * c) * EPV + q], v[(2 * c + 1) * EPV + q]);
                     *reinterpret_cast<u32x2*>(d) = w;
+                } else {
+                    static_assert(NV == 2, "k-run of 2, 4 or 8");
+                    *reinterpret_cast<unsigned*>(d) = pack_bf16(v[q], v[EPV + q]);
                 }
             }
         } else if constexpr (VEC) {
