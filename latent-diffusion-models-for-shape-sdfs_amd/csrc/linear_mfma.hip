@@ -8,8 +8,8 @@
 // exact path (compute = LDM_COMPUTE_FP32) that the fp64 gradient parity test pins.
 //
 // Tiling: a workgroup (4 waves) owns a 64 (rows b) x 64 (cols m) tile, each wave a 32 x 32
-// MFMA tile.  K advances in 128-deep chunks through two LDS buffers per operand: the next
-// chunk's global loads are issued into registers before the current chunk's MFMAs (one barrier
+// MFMA tile.  K advances in KCH-deep chunks (64 or 128, see Chunk) through two LDS buffers
+// per operand: the next chunk's global loads are issued into registers before the current chunk's MFMAs (one barrier
 // per chunk).  At the training shapes (1000 x 1024 x 1024..2048, 256 workgroups = one per CU)
 // each workgroup walks K alone; 128-deep chunks (vs 64) and the XCD-grouped tile order below
 // each took ~5-10 % off.  Operand tiles load with 16-byte vectors along
@@ -25,13 +25,17 @@
 namespace ldm {
 namespace {
 
-#ifndef LDM_LINEAR_KC
-#define LDM_LINEAR_KC 128
-#endif
-constexpr int kKC = LDM_LINEAR_KC;   // k per chunk
-constexpr int kLd = kKC + 8;         // LDS row pitch (bf16 elements)
-constexpr int kBuf = 64 * kLd;       // one operand buffer (elements)
-constexpr int kLdsBytes = 4 * kBuf * (int)sizeof(unsigned short);   // X0 X1 W0 W1 = 68 KiB
+// Chunk depth KCH (k per LDS chunk) is a template parameter, picked per call (launch_mfma3):
+// 128 for few workgroups with long K (training, 1 workgroup per CU: deeper chunks amortise
+// the barrier), 64 for many workgroups (auto-decoder, 1M rows: 37 KiB of LDS instead of
+// 68 KiB doubles the workgroups per CU, which hides the operand-load latency).
+constexpr int kKCSplit = 128;        // split-K slice granularity (a multiple of every KCH)
+template <int KCH>
+struct Chunk {
+    static constexpr int Ld = KCH + 8;                               // LDS row pitch (bf16)
+    static constexpr int Buf = 64 * Ld;                              // one operand buffer
+    static constexpr int LdsBytes = 4 * Buf * (int)sizeof(unsigned short);   // X0 X1 W0 W1
+};
 
 __device__ __forceinline__ unsigned pack_bf16(float a, float b) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -52,8 +56,9 @@ __device__ __forceinline__ float ld_elem(const T* p, int64_t i) {
 // 16-byte aligned, the line extent a multiple of the vector); lanes of a wave then cover whole
 // 256-byte (fp32) / 128-byte (bf16) segments.  Otherwise TPL threads per line, E consecutive
 // elements each.
-template <typename T, bool KC, bool VEC>
+template <typename T, bool KC, bool VEC, int KCH>
 struct Tile {
+    static constexpr int kKC = KCH, kLd = Chunk<KCH>::Ld;
     static constexpr int E = 64 * kKC / 256;          // values per thread
     static constexpr int EPV = 16 / sizeof(T);        // elements per 16-byte vector
     static constexpr int LEN = KC ? kKC : 64;         // line length
@@ -198,7 +203,7 @@ struct Tile {
     }
 };
 
-template <typename TW, bool XK, bool WK, bool XV, bool WV>
+template <typename TW, bool XK, bool WK, bool XV, bool WV, int KCH>
 __device__ __forceinline__ void mfma_segment(f32x16& acc, unsigned short* __restrict__ sm,
                                              const float* X, int64_t sxb, int64_t sxk,
                                              const void* Wv, int64_t swm, int64_t swk, int K,
@@ -209,8 +214,9 @@ __device__ __forceinline__ void mfma_segment(f32x16& acc, unsigned short* __rest
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const int r = lane & 31, h = lane >> 5;
-    Tile<float, XK, XV> tx;
-    Tile<TW, WK, WV> tw;
+    constexpr int kKC = KCH, kLd = Chunk<KCH>::Ld, kBuf = Chunk<KCH>::Buf;
+    Tile<float, XK, XV, KCH> tx;
+    Tile<TW, WK, WV, KCH> tw;
     const int nk = (K + kKC - 1) / kKC;
     tx.load(X, sxb, sxk, Bn, K, b0, 0);
     tw.load(W, swm, swk, M, K, m0, 0);
@@ -263,7 +269,7 @@ __device__ __forceinline__ void apply_epi(const ldm_linear_args_t& a, int b, int
 // gridDim.z > 1: split-K.  Slice z covers k in [z*kc_len, min(K, (z+1)*kc_len)) (kc_len a
 // multiple of kKC, every slice non-empty) and stores its raw partial to ws[z][b][m]; the
 // epilogue is split_reduce_kernel's.
-template <typename TW, bool XK, bool WK, bool XV, bool WV>
+template <typename TW, bool XK, bool WK, bool XV, bool WV, int KCH>
 __global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a, int kc_len) {
     extern __shared__ __attribute__((aligned(16))) unsigned short sm[];   // kLdsBytes
     // XCD-aware tile order.  Workgroups are dealt round-robin to the 8 XCDs (linear id % 8),
@@ -283,11 +289,11 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(ldm_linear_args_t a, i
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X + (int64_t)kb * a.sxk, a.sxb, a.sxk,
+    mfma_segment<TW, XK, WK, XV, WV, KCH>(acc, sm, a.X + (int64_t)kb * a.sxk, a.sxb, a.sxk,
                                      W + (int64_t)kb * a.swk, a.swm, a.swk, kl, a.Bn, a.M, b0,
                                      m0);
     if (a.K2 > 0)
-        mfma_segment<TW, XK, WK, XV, WV>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k,
+        mfma_segment<TW, XK, WK, XV, WV, KCH>(acc, sm, a.X2, a.sx2b, a.sx2k, a.W2, a.sw2m, a.sw2k,
                                          a.K2, a.Bn, a.M, b0, m0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = m0 + (wave & 1) * 32 + (lane & 31);
@@ -320,10 +326,10 @@ struct SplitPlan { int nz, kc_len; };
 SplitPlan split_plan(const ldm_linear_args_t& a) {
     const int64_t tiles = (int64_t)((a.M + 63) / 64) * ((a.Bn + 63) / 64);
     if (a.compute != LDM_COMPUTE_BF16 || a.K2 > 0 || tiles >= 256) return {1, a.K};
-    int nz = (int)std::min<int64_t>((1024 + tiles - 1) / tiles, a.K / (8 * kKC));
+    int nz = (int)std::min<int64_t>((1024 + tiles - 1) / tiles, a.K / (8 * kKCSplit));
     nz = std::min(nz, 256);
     if (nz < 2) return {1, a.K};
-    const int kc = ((a.K + nz - 1) / nz + kKC - 1) / kKC * kKC;
+    const int kc = ((a.K + nz - 1) / nz + kKCSplit - 1) / kKCSplit * kKCSplit;
     return {(a.K + kc - 1) / kc, kc};
 }
 
@@ -338,9 +344,10 @@ bool vec_ok(const void* P, int64_t s_row, int64_t s_k, int rows, int K, int esiz
            ext % epv == 0;
 }
 
-template <typename TW, bool XK, bool WK, bool XV, bool WV>
-int launch_one(const ldm_linear_args_t& a, hipStream_t s) {
-    auto* k = &linear_mfma_kernel<TW, XK, WK, XV, WV>;
+template <typename TW, bool XK, bool WK, bool XV, bool WV, int KCH>
+int launch_one(const ldm_linear_args_t& a, const SplitPlan& sp, hipStream_t s) {
+    auto* k = &linear_mfma_kernel<TW, XK, WK, XV, WV, KCH>;
+    constexpr int kLdsBytes = Chunk<KCH>::LdsBytes;
     static bool attr_set = false;     // one per instantiation; idempotent if raced
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -350,8 +357,6 @@ int launch_one(const ldm_linear_args_t& a, hipStream_t s) {
                     hipGetErrorString(e));
         attr_set = true;
     }
-    SplitPlan sp = split_plan(a);
-    if (sp.nz > 1 && (!a.ws || a.ws_floats < (int64_t)sp.nz * a.Bn * a.M)) sp = {1, a.K};
     const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64, sp.nz);
     hipLaunchKernelGGL(k, grid, dim3(256), kLdsBytes, s, a, sp.kc_len);
     if (sp.nz > 1) {
@@ -362,12 +367,26 @@ int launch_one(const ldm_linear_args_t& a, hipStream_t s) {
     return 0;
 }
 
+template <typename TW, bool XK, bool WK, int KCH>
+int launch_mfma4(const ldm_linear_args_t& a, const SplitPlan& sp, bool xv, bool wv,
+                 hipStream_t s) {
+    if (xv && wv) return launch_one<TW, XK, WK, true, true, KCH>(a, sp, s);
+    if (xv) return launch_one<TW, XK, WK, true, false, KCH>(a, sp, s);
+    if (wv) return launch_one<TW, XK, WK, false, true, KCH>(a, sp, s);
+    return launch_one<TW, XK, WK, false, false, KCH>(a, sp, s);
+}
+
+// Chunk depth by grid size (measured: auto-decoder 1M x 512 x 512 products, 131k workgroups,
+// 96.9 -> 81.2 ms/step with 64; config-2 training, 256 workgroups, 1012 -> 911 steps/s with 64).
+constexpr int64_t kShallowChunkMinWG = 2048;
+
 template <typename TW, bool XK, bool WK>
 int launch_mfma3(const ldm_linear_args_t& a, bool xv, bool wv, hipStream_t s) {
-    if (xv && wv) return launch_one<TW, XK, WK, true, true>(a, s);
-    if (xv) return launch_one<TW, XK, WK, true, false>(a, s);
-    if (wv) return launch_one<TW, XK, WK, false, true>(a, s);
-    return launch_one<TW, XK, WK, false, false>(a, s);
+    SplitPlan sp = split_plan(a);
+    if (sp.nz > 1 && (!a.ws || a.ws_floats < (int64_t)sp.nz * a.Bn * a.M)) sp = {1, a.K};
+    const int64_t wgs = (int64_t)((a.M + 63) / 64) * ((a.Bn + 63) / 64) * sp.nz;
+    if (wgs >= kShallowChunkMinWG) return launch_mfma4<TW, XK, WK, 64>(a, sp, xv, wv, s);
+    return launch_mfma4<TW, XK, WK, 128>(a, sp, xv, wv, s);
 }
 
 template <typename TW>
