@@ -257,6 +257,31 @@ def test_linear_bf16_mfma(dev, wdt, Bn, M, K, K2):
     assert (Y.double() - (R_.double() + ref * torch.sigmoid(ref))).abs().max() < 2 * tol
 
 
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+def test_linear_bf16_shallow_chunks(dev, wdt):
+    """Calls with >= 2048 workgroups run 64-deep LDS chunks (linear_mfma.hip launch_mfma3):
+    k-contiguous and rows-contiguous operands (fp32 X, fp32/bf16 W) at that depth, against the
+    fp64 product of the bf16-rounded operands."""
+    from ldm_sdf import ops, _capi as capi
+    BF = capi.COMPUTE_BF16
+    Bn, M, K = 131072, 512, 256          # 2048 x 8 tiles
+    g = torch.Generator(device=dev).manual_seed(3)
+    Z = torch.randn(K, Bn, device=dev, generator=g)          # X = Z.T: rows contiguous
+    X = Z.T.contiguous()
+    W = torch.randn(M, K, device=dev, generator=g).to(wdt)
+    ref = _bf(X) @ _bf(W).T
+    tol = 2e-6 * K ** 0.5 * 4
+    for Xv in (X, Z.T):
+        Y = torch.empty(Bn, M, device=dev)
+        ops.linear(Xv, W, Y, compute=BF)
+        assert (Y.double() - ref).abs().max() < tol
+    # G W with W as a transposed view (rows-contiguous weight operand), 2048 x 4 tiles
+    G = torch.randn(Bn, M, device=dev, generator=g)
+    dX = torch.empty(Bn, K, device=dev)
+    ops.linear(G, W.T, dX, compute=BF)
+    assert (dX.double() - _bf(G) @ _bf(W)).abs().max() < 8e-6 * M ** 0.5
+
+
 @pytest.mark.parametrize("Bn,M,K,epi", [(1, 512, 300001, "bias"), (64, 70, 100003, "relu"),
                                          (130, 64, 50000, "accum")])
 def test_linear_bf16_split_k(dev, Bn, M, K, epi):
