@@ -415,7 +415,31 @@ int64_t linear_mfma_ws_floats(const ldm_linear_args_t& a) {
     return sp.nz > 1 ? (int64_t)sp.nz * a.Bn * a.M : 0;
 }
 
+namespace {
+// K == 1 (a rank-1 product, e.g. the auto-decoder's last-layer input gradient g W8): one
+// product per output, so no tile, LDS or MFMA.  Same numbers as the matrix-core kernel: the
+// operands rounded to bf16 (RNE) and multiplied in fp32 (exact for two bf16 values), then the
+// shared epilogue with the bias.  Memory-bound; one thread per output, m fastest.
+template <typename TW>
+__global__ __launch_bounds__(256) void outer_k1_kernel(ldm_linear_args_t a) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)a.Bn * a.M) return;
+    const int b = (int)(i / a.M), m = (int)(i - (int64_t)b * a.M);
+    const float x = bf16_to_f32((unsigned short)(pack_bf16(a.X[(int64_t)b * a.sxb], 0.f) & 0xffffu));
+    const float w = bf16_to_f32((unsigned short)(pack_bf16(
+        ld_elem(reinterpret_cast<const TW*>(a.W), (int64_t)m * a.swm), 0.f) & 0xffffu));
+    apply_epi(a, b, m, x * w + (a.bias ? a.bias[m] : 0.f));
+}
+}  // namespace
+
 int linear_mfma(const ldm_linear_args_t& a, hipStream_t s) {
+    if (a.K == 1 && a.K2 == 0) {
+        const int64_t n = (int64_t)a.Bn * a.M;
+        const dim3 grid((unsigned)((n + 255) / 256));
+        if (a.w_dtype == LDM_BF16) hipLaunchKernelGGL(outer_k1_kernel<unsigned short>, grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(outer_k1_kernel<float>, grid, dim3(256), 0, s, a);
+        return launch_status("ldm_linear (mfma, K=1)");
+    }
     const bool xk = a.sxk == 1, wk = a.swk == 1;
     const int e = a.w_dtype == LDM_BF16 ? launch_mfma<unsigned short>(a, xk, wk, s)
                                         : launch_mfma<float>(a, xk, wk, s);

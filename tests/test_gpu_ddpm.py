@@ -282,6 +282,26 @@ def test_linear_bf16_shallow_chunks(dev, wdt):
     assert (dX.double() - _bf(G) @ _bf(W)).abs().max() < 8e-6 * M ** 0.5
 
 
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+def test_linear_bf16_rank1(dev, wdt):
+    """K = 1 goes to the rank-1 kernel: exactly the bf16-rounded product (+ bias, epilogue),
+    bit-equal to the fp64 reference since a product of two bf16 values is exact in fp32."""
+    from ldm_sdf import ops, _capi as capi
+    BF = capi.COMPUTE_BF16
+    g = torch.Generator(device=dev).manual_seed(9)
+    Bn, M = 70001, 512
+    X = torch.randn(Bn, 1, device=dev, generator=g)
+    W8 = torch.randn(1, M, device=dev, generator=g).to(wdt)
+    R_ = torch.randn(Bn, M, device=dev, generator=g)
+    Y = torch.empty(Bn, M, device=dev)
+    ops.linear(X, W8.T, Y, epi=capi.EPI_MASK_R, R=R_, compute=BF)
+    want = (_bf(X) * _bf(W8)).float() * (R_ > 0)
+    assert torch.equal(Y, want)
+    b = torch.randn(M, device=dev, generator=g)
+    ops.linear(X, W8.T, Y, bias=b, compute=BF)
+    assert torch.equal(Y, (_bf(X) * _bf(W8)).float() + b)
+
+
 @pytest.mark.parametrize("Bn,M,K,epi", [(1, 512, 300001, "bias"), (64, 70, 100003, "relu"),
                                          (130, 64, 50000, "accum")])
 def test_linear_bf16_split_k(dev, Bn, M, K, epi):
