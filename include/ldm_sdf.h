@@ -163,6 +163,14 @@ int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, float* x, co
                     int t_hi, int steps, int B, float* ws, size_t ws_bytes, ldm_stream_t s);
 int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host, ldm_stream_t s);
 
+/* ---- optimizer (A7 training step) -------------------------------------------------------- */
+/* AdamW on fp32 masters p [n] with grads g, moments m, v (torch.optim.AdamW's order; step is
+ * 1-based).  p_bf16 (may be NULL): bf16 [n] working copy of the updated p, written in the same
+ * pass (RNE). */
+int ldm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n,
+                   double lr, double beta1, double beta2, double eps, double weight_decay,
+                   int step, ldm_stream_t s);
+
 /* ---- generic fused linear (A6/A7 building block, training) ---------------------------- */
 /* acc[b][m] = sum_{k<K} X[b][k] W[m][k]  +  sum_{k<K2} X2[b][k] W2[m][k]   (K2 may be 0)
  * with arbitrary element strides, so the forward (X W^T), input-gradient (G W) and

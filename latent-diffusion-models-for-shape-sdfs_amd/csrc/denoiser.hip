@@ -748,10 +748,50 @@ int denoiser_trunk(const ldm_denoiser_t* w, const float* x, int t, int B, float*
     return 0;
 }
 
+// AdamW (decoupled weight decay; torch.optim.AdamW's update order) on fp32 masters, with the
+// low-precision working copy the next step's GEMMs read written in the same pass:
+//   p *= 1 - lr*wd;  m += (1-b1)(g - m);  v = b2 v + (1-b2) g^2;
+//   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps);  p_bf16 = RNE(p)
+// One read of p, g, m, v and one write of p, m, v (+ 2 B) per parameter: HBM-bound.
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    unsigned short* __restrict__ pb, int64_t n,
+                                                    float decay, float omb1, float b2, float omb2,
+                                                    float eps, float step_size, float bc2_sqrt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float gi = g[i];
+    const float mi = m[i] + omb1 * (gi - m[i]);
+    const float vi = v[i] * b2 + omb2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    const float pi = p[i] * decay - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (pb) {   // round to nearest even
+        const unsigned u = __builtin_bit_cast(unsigned, pi);
+        pb[i] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
+}
+
 }  // namespace
 }  // namespace ldm
 
 using namespace ldm;
+
+extern "C" int ldm_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16,
+                              int64_t n, double lr, double beta1, double beta2, double eps,
+                              double weight_decay, int step, ldm_stream_t s) {
+    LDM_REQUIRE(p && g && m && v && n >= 0 && step >= 1, LDM_EINVAL, "adamw: bad arguments");
+    if (n == 0) return 0;
+    // scalars derived in double and rounded once, as torch does with its Python-float betas
+    const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
+    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)s, p, g, m, v, (unsigned short*)p_bf16, n,
+                       (float)(1.0 - lr * weight_decay), (float)(1.0 - beta1), (float)beta2,
+                       (float)(1.0 - beta2), (float)eps, (float)(lr / bc1), (float)sqrt(bc2));
+    return launch_status("adamw");
+}
 
 extern "C" int ldm_ddpm_step(const ldm_sched_t* sc, const float* x, const float* eps,
                              const float* z, int t, int n, float* x_out, ldm_stream_t s) {

@@ -114,6 +114,8 @@ SIGNATURES = [
     ("ldm_sample_loop", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _i, _i, _i, _fp,
                              _sz, _vp]),
     ("ldm_sample_loop_status", _i, [_fp, _i, _i, C.POINTER(C.c_uint), _vp]),
+    ("ldm_adamw_step", _i, [_fp, _fp, _fp, _fp, _vp, C.c_int64, C.c_double, C.c_double,
+                            C.c_double, C.c_double, C.c_double, _i, _vp]),
     ("ldm_linear", _i, [C.POINTER(LinearArgs), _vp]),
     ("ldm_linear_workspace_floats", C.c_int64, [C.POINTER(LinearArgs)]),
     ("ldm_silu_bwd", _i, [_fp, _fp, _i, _fp, _vp]),

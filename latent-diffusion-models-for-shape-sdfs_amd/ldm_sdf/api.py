@@ -173,8 +173,10 @@ def sample(denoiser, schedule: DDPMSchedule, n: int, *,
 class TrainState:
     step: int = 0
     losses: List[float] = field(default_factory=list)
-    optimizer: Optional[torch.optim.Optimizer] = None
+    optimizer: Optional[torch.optim.Optimizer] = None    # a torch optimizer, if one is given
     masters: Optional[Dict[str, torch.Tensor]] = None
+    adam: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None   # fused AdamW (m, v)
+    hparams: Dict[str, float] = field(default_factory=dict)
 
 
 def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
@@ -221,8 +223,11 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         state.masters = {n: denoiser.params[n] for n in denoiser.names()}
         for v in state.masters.values():
             v.requires_grad_(False)
-        state.optimizer = torch.optim.AdamW(list(state.masters.values()), lr=lr,
-                                            weight_decay=weight_decay)
+        # fused AdamW (ldm_adamw_step): one HIP pass per tensor updates the fp32 master and
+        # rewrites the bf16 working copy the next step's GEMMs read (no per-step re-pack)
+        state.adam = {n: (torch.zeros_like(v), torch.zeros_like(v))
+                      for n, v in state.masters.items()}
+        state.hparams = dict(lr=lr, weight_decay=weight_decay)
     grads = {n: torch.empty_like(v) for n, v in state.masters.items()}
     T = schedule.T
     for _ in range(steps):
@@ -234,11 +239,24 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         x0 = latents[idx[lo:hi]].contiguous()
         loss, grads = train_step(denoiser, schedule, x0, t[lo:hi], eps[lo:hi], dtype=dtype,
                                  grads=grads, group=group)
-        for n, p in state.masters.items():
-            p.grad = grads[n]
-        state.optimizer.step()
-        denoiser.invalidate()
+        if state.optimizer is not None:          # caller-supplied torch optimizer
+            for n, p in state.masters.items():
+                p.grad = grads[n]
+            state.optimizer.step()
+            denoiser.invalidate()
+        else:
+            work = denoiser.device_pack(dtype, device, with_tables=False)
+            for n, p in state.masters.items():
+                w = work[n]
+                low = w if (w.dtype == torch.bfloat16 and w.data_ptr() != p.data_ptr()) else None
+                m, v = state.adam[n]
+                ops.adamw_step(p, grads[n], m, v, low, lr=state.hparams["lr"],
+                               weight_decay=state.hparams["weight_decay"], step=state.step + 1)
+                if low is None and w.data_ptr() != p.data_ptr():
+                    w.copy_(p)                   # an fp32 working copy that is not the master
         state.step += 1
         state.losses.append(loss)
+    if state.optimizer is None:
+        denoiser.invalidate()    # E tables (sampling) are rebuilt from the trained masters
     state.losses = [float(l) if isinstance(l, torch.Tensor) else l for l in state.losses]
     return state

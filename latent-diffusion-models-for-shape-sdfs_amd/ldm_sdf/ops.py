@@ -164,6 +164,24 @@ def sample_step(desc: capi.Denoiser, sched_desc: capi.Sched, x: torch.Tensor,
                "ldm_sample_step")
 
 
+def adamw_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+               p_low: Optional[torch.Tensor], *, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
+               weight_decay: float = 0.0, step: int) -> None:
+    """Fused AdamW (``ldm_adamw_step``) on contiguous fp32 tensors; ``p_low`` (bf16, same shape)
+    receives the updated weights rounded to nearest even, or None."""
+    for t in (p, g, m, v):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.shape != p.shape:
+            raise capi.LdmError("adamw_step: p, g, m, v must be contiguous fp32 of one shape")
+    if p_low is not None and (p_low.dtype != torch.bfloat16 or not p_low.is_contiguous()
+                              or p_low.shape != p.shape):
+        raise capi.LdmError("adamw_step: p_low must be contiguous bf16 of p's shape")
+    capi.check(capi.load().ldm_adamw_step(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                          capi.ptr(p_low), p.numel(), float(lr), float(betas[0]),
+                                          float(betas[1]), float(eps), float(weight_decay),
+                                          int(step), capi.stream_handle(p.device)),
+               "ldm_adamw_step")
+
+
 def sample_loop_supported(desc: capi.Denoiser, B: int) -> bool:
     return bool(capi.load().ldm_sample_loop_supported(C.byref(desc), int(B)))
 

@@ -347,3 +347,56 @@ def test_train_step_bf16_grads_close_to_fp64(dev, den):
         got = (got if k.startswith("b") else got[:8]).flatten()
         cos = float(got @ want / (got.norm() * want.norm() + 1e-30))
         assert cos >= 0.999, (k, cos)
+
+
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_adamw_step_matches_torch(dev, wd):
+    """ldm_adamw_step vs torch.optim.AdamW over 5 steps (fp32 masters), and the fused bf16
+    working copy equals the updated master rounded to nearest even."""
+    from ldm_sdf import ops
+    g = torch.Generator(device=dev).manual_seed(4)
+    p = torch.randn(1000, 1031, device=dev, generator=g)
+    ref = p.clone().requires_grad_(False)
+    opt = torch.optim.AdamW([ref], lr=3e-3, weight_decay=wd)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    low = torch.empty_like(p, dtype=torch.bfloat16)
+    for step in range(1, 6):
+        grad = torch.randn(p.shape, device=dev, generator=g)
+        ref.grad = grad.clone()
+        opt.step()
+        ops.adamw_step(p, grad, m, v, low, lr=3e-3, weight_decay=wd, step=step)
+    torch.cuda.synchronize()
+    assert (p - ref).abs().max() <= 2e-6 * ref.abs().max()
+    st = opt.state[ref]
+    assert (m - st["exp_avg"]).abs().max() <= 1e-6 * st["exp_avg"].abs().max()
+    assert (v - st["exp_avg_sq"]).abs().max() <= 1e-6 * st["exp_avg_sq"].abs().max()
+    assert torch.equal(low, p.to(torch.bfloat16))
+
+
+def test_train_fused_adamw_matches_torch_optimizer(dev, den):
+    """train() with the fused AdamW (default) tracks the same run driven by torch's AdamW."""
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser
+    _, p = den
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"], params[f"bblk{k}"] = p.Wblk[k], p.bblk[k]
+    lat = torch.randn(256, 256, generator=torch.Generator().manual_seed(2)).to(dev) * 0.5
+    sch = ldm_sdf.DDPMSchedule()
+    runs = []
+    for use_torch in (False, True):
+        model = MLPDenoiser(params={k: v.clone() for k, v in params.items()})
+        model.to_device(dev)
+        st = None
+        if use_torch:
+            st = ldm_sdf.api.TrainState()
+            st.masters = {n: model.params[n] for n in model.names()}
+            st.optimizer = torch.optim.AdamW(list(st.masters.values()), lr=1e-4, weight_decay=0.0)
+        st = ldm_sdf.train(model, sch, lat, steps=5, batch=256, dtype="fp32", state=st,
+                           generator=torch.Generator(device=dev).manual_seed(8))
+        runs.append((st.losses, {n: t.clone() for n, t in model.params.items()}))
+    (la, pa), (lb, pb) = runs
+    assert max(abs(a - b) for a, b in zip(la, lb)) <= 1e-5 * max(lb)
+    for n in pa:
+        assert (pa[n] - pb[n]).abs().max() <= 1e-5 * pb[n].abs().max() + 1e-7, n
+
