@@ -23,6 +23,10 @@
 
 #include <stdlib.h>
 
+#ifndef LDM_LOOP_SLEEP
+#define LDM_LOOP_SLEEP 1     // s_sleep units (64 clocks) between polls of the XCD barrier
+#endif
+
 namespace ldm {
 namespace {
 
@@ -208,7 +212,9 @@ __device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, u
             __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+#if LDM_LOOP_SLEEP > 0
+        __builtin_amdgcn_s_sleep(LDM_LOOP_SLEEP);
+#endif
     }
     return true;
 }
