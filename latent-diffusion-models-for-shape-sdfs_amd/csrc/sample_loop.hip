@@ -306,6 +306,20 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
         const int t = a.t_hi - s;
         const float* xin = a.x + (size_t)(s & 1) * B * D;
         float* xout = a.x + (size_t)((s & 1) ^ 1) * B * D;
+        // This step's epilogue operands, loaded now so that their latency overlaps the
+        // in-projection's staging instead of sitting behind each layer's barrier: E_k[t][m],
+        // noise[t][b][m], x_t[b][m] (written by this same lane last step), c1/c2/sigma[t].
+        // Every lane loads (clamped index); only writer lanes use the values.
+        const int bq = b < B ? b : 0;
+        const size_t io = (size_t)bq * D + mo;
+        float ep[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) ep[k] = a.e_tab[k][(size_t)t * H + m];
+        const float zp = a.noise[(size_t)t * B * D + io];
+        const float xp = __builtin_bit_cast(float, __hip_atomic_load(
+            reinterpret_cast<const unsigned*>(xin + io), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
+        const float c1 = a.c1[t], c2 = a.c2[t], sg = a.sg[t];
         // in-projection: h0 = W_in x + b_in
         stage(xs, xin, (B * D) >> 1);
         __syncthreads();
@@ -325,7 +339,7 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
             __syncthreads();
             const float acc = row_dot<MB, NJH>(wb[k], xs, B, H, lane);
             if (writer) {
-                const float pre = acc + a.e_tab[k][(size_t)t * H + m];
+                const float pre = acc + ep[k];
                 publish(hout + (size_t)b * H + m, xs[b * H + m] + silu(pre));
             }
             ++phase;
@@ -341,11 +355,7 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
                 const float pre = acc + bo;
                 const size_t i = (size_t)b * D + m;
                 const bool noise = t > 0;
-                const float zz = noise ? a.noise[(size_t)t * B * D + i] : 0.f;
-                const float xv = __builtin_bit_cast(float, __hip_atomic_load(
-                    reinterpret_cast<const unsigned*>(xin + i), __ATOMIC_RELAXED,
-                    __HIP_MEMORY_SCOPE_AGENT));
-                publish(xout + i, ddpm_update(xv, pre, zz, a.c1[t], a.c2[t], a.sg[t], noise));
+                publish(xout + i, ddpm_update(xp, pre, noise ? zp : 0.f, c1, c2, sg, noise));
             }
         }
         ++phase;
