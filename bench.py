@@ -1,14 +1,17 @@
 """Benchmark: SDF queries/s on 256^3 grids (+ DDPM sample steps/s), 1..8 MI355X.
 
 One "step" = decode of ``--batch`` synthetic shapes on a ``--grid``^3 grid (config 4:
-B=64, 256^3), z-slab sharded over the ranks with one RCCL all-gather of the volume
+B=64, 256^3), z-slab sharded over the ranks with per-shape RCCL all-gathers of the volume
 (SURVEY.md §8(e)).  Total work is fixed as N grows (``scaling: strong``); ``value`` =
 all queries of the step / max-over-ranks step time.
 
-Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
-Rank 0 prints ONE JSON line.  Extra objects: ``roofline`` (dominant kernel, HIP events on its
-stream), ``cpu_baseline`` (oracle/ref_cpu.py fp32 on this host's cores, bounded sample),
-``ddpm`` (config 3: 1000-step sampling of 8 latents, hipGraph replay, steps/s).
+Launch: ``python bench.py`` (1 GPU), ``torchrun --nproc-per-node N bench.py --gpus N``, or
+``python bench.py --gpus N`` (spawns the N ranks itself through torch.distributed.run, as a
+child process started before anything touches the GPU).  Rank 0 prints ONE JSON line.
+Extra objects: ``roofline`` (dominant kernel, HIP events on its stream), ``cpu_baseline``
+(oracle/ref_cpu.py fp32 on this host's cores, bounded sample), ``ddpm`` (1000-step sampling
+of 8 latents, steps/s, + config 3 end to end), ``config5``, ``train`` (config 2), ``mc``,
+``autodecoder``.
 """
 from __future__ import annotations
 
@@ -16,6 +19,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -55,9 +60,11 @@ def parse():
     ap.add_argument("--no-autodecoder", action="store_true",
                     help="skip C19 (DeepSDF auto-decoder training at 64 shapes x 16384 samples)")
     ap.add_argument("--ad-steps", type=int, default=5)
-    ap.add_argument("--config3", action="store_true",
-                    help="also time sample(8) -> decode 128^3 end to end (adds a decoder "
-                         "launch of another size to the profile)")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip config 3 (sample(8) -> decode 128^3, timed end to end; its "
+                         "decode is a dec_q_kernel launch of another size in a profile)")
+    ap.add_argument("--shapes-per-group", type=int, default=0,
+                    help="multi-GPU decode: shapes per gather group (0: ceil(B/8))")
     return ap.parse_args()
 
 
@@ -69,6 +76,22 @@ def host_cores() -> int:
     if omp and omp.isdigit() and int(omp) > 0:
         n = min(n, int(omp))
     return n
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_fields(cores: int) -> dict:
+    """CPU model, threads used and cores available, for every ``cpu_baseline``."""
+    return {"cores": cores, "threads": torch.get_num_threads(), "cpu_model": cpu_model(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
 
 
 def cpu_baseline_decode(grid: int, budget_s: float):
@@ -89,13 +112,14 @@ def cpu_baseline_decode(grid: int, budget_s: float):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": pts / dt, "unit": "queries/s", "cores": cores, "kind": "port",
+    return {"value": pts / dt, "unit": "queries/s", "kind": "port", **cpu_fields(cores),
             "sample": f"{k} z-slices x {grid}x{grid} of the {grid}^3 grid ({pts} queries), "
                       f"1 shape, fp32 torch-CPU oracle, {dt:.1f}s"}
 
 
 def cpu_baseline_sampling(budget_s: float, B: int):
     from oracle import ref_cpu as R
+    torch.set_num_threads(host_cores())
     p = R.make_denoiser_params(seed=4321, dtype=torch.float32)
     tab = R.ddpm_tables()
     emb = torch.from_numpy(R.timestep_embedding_table(1000, 128))
@@ -111,8 +135,35 @@ def cpu_baseline_sampling(budget_s: float, B: int):
             if time.perf_counter() - t0 >= budget_s:
                 break
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "steps/s", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"{steps} reverse steps, B={B}, fp32 torch-CPU oracle"}
+    return {"value": steps / dt, "unit": "steps/s", "kind": "port",
+            **cpu_fields(host_cores()),
+            "sample": f"{steps} reverse steps, B={B}, fp32 torch-CPU oracle, {dt:.1f}s"}
+
+
+def cpu_baseline_unet(budget_s: float, B: int):
+    """Config 5's sampler on the CPU: the fp32 oracle UNet (oracle/ref_unet.py) reverse steps."""
+    from oracle import ref_cpu as R
+    from oracle import ref_unet as U
+    torch.set_num_threads(host_cores())
+    up = U.make_unet_params(seed=2468, dtype=torch.float32)
+    tab = R.ddpm_tables()
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128))
+    x = torch.randn(B, 1024)
+    noise = torch.randn(1000, B, 1024)
+    t0 = time.perf_counter()
+    steps = 0
+    with torch.inference_mode():
+        for t in range(999, -1, -1):
+            eps = U.unet_forward(up, x, torch.full((B,), t), emb)
+            x = R.ddpm_step(tab, x, eps, noise[t], t)
+            steps += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "steps/s", "kind": "port",
+            **cpu_fields(host_cores()),
+            "sample": f"{steps} reverse steps of the 1D-UNet (D=1024), B={B}, fp32 torch-CPU "
+                      f"oracle, {dt:.1f}s"}
 
 
 def bench_mc(vol, args):
@@ -143,7 +194,7 @@ def bench_mc(vol, args):
         t1 = time.perf_counter()
         M.marching_cubes(vn)
         res["cpu_baseline"] = {"value": 1.0 / (time.perf_counter() - t1), "unit": "meshes/s",
-                               "cores": 1, "kind": "port",
+                               "kind": "port", **cpu_fields(1), "cores": 1,
                                "sample": f"oracle/ref_mc.py (numpy) on the same {N}^3 volume"}
     res["value"] = 1.0 / dt
     res["unit"] = "meshes/s"
@@ -196,19 +247,105 @@ def bench_autodecoder(args, dev):
             A.autodecoder_grads(p, zc, xc, sc)
             n += 1
         sps = n * 4096 / (time.perf_counter() - t1)
-        res["cpu_baseline"] = {"value": sps, "unit": "samples/s", "cores": host_cores(),
-                               "kind": "port", "sample": f"{n} fp32 oracle steps (torch "
-                               "autograd) of 1 shape x 4096 samples"}
+        res["cpu_baseline"] = {"value": sps, "unit": "samples/s", "kind": "port",
+                               **cpu_fields(host_cores()),
+                               "sample": f"{n} fp32 oracle steps (torch autograd) of 1 shape x "
+                                         "4096 samples"}
     return res
+
+
+class SlabTimer:
+    """The decode slab function handed to ``dist.decode_sharded`` (or called directly at one
+    rank): launches ``ldm_decoder_grid_fwd`` for shapes [b0, b1) of the z-slab [k0, k1) and,
+    when ``timed``, brackets the launch with HIP events on the kernel's stream."""
+
+    def __init__(self, desc, beta_fn, N, stream):
+        self.desc, self.beta_fn, self.N, self.stream = desc, beta_fn, N, stream
+        self.timed = False
+        self.events = []          # (start, end, queries of the launch)
+        self.beta = None
+
+    def __call__(self, k0, k1, dst, b0, b1):
+        from ldm_sdf import ops
+        if b0 == 0 or self.beta is None:
+            self.beta = self.beta_fn()     # A2 fold once per step (first group)
+        if self.timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(self.stream)
+        ops.decoder_grid_fwd(self.desc, self.beta[b0:b1], self.N, k0, k1, out=dst)
+        if self.timed:
+            e1.record(self.stream)
+            self.events.append((e0, e1, (b1 - b0) * (k1 - k0) * self.N * self.N))
+
+    def kernel_stats(self):
+        """(average launch ms, average queries per launch) over the timed launches."""
+        if not self.events:
+            return float("nan"), 0
+        ms = [a.elapsed_time(b) for a, b, _ in self.events]
+        return sum(ms) / len(ms), sum(q for _, _, q in self.events) / len(self.events)
+
+
+def run_decode_steps(slab, B: int, N: int, *, steps: int, warmup: int, world: int, group,
+                     device: torch.device, out: torch.Tensor, sync=None,
+                     shapes_per_group=None, on_timed=None) -> float:
+    """The bench's per-rank step loop (shared with the gloo test, tests/test_bench_gloo.py):
+    ``warmup`` untimed steps, then barrier + sync, ``steps`` timed steps, sync + barrier, and
+    the MAX of the per-rank elapsed times (all-reduce).  One step = the (sharded) decode of B
+    shapes on an N^3 grid into ``out``; ``slab(k0, k1, dst, b0, b1)`` computes a slab."""
+    from ldm_sdf.dist import decode_sharded
+    sync = sync or (lambda: None)
+
+    def step():
+        if world == 1:
+            slab(0, N, out, 0, B)
+        else:
+            decode_sharded(slab, B, N, device, group=group, out=out,
+                           shapes_per_group=shapes_per_group)
+
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier(group)
+    sync()
+    if on_timed:
+        on_timed()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier(group)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+        elapsed = float(tt)
+    return elapsed
+
+
+def decoder_traffic(queries_per_launch: float):
+    """HBM bytes per launch for ``roofline.traffic``: the PMC bytes per query measured at
+    B = 64 x 256^3 (profiles/decoder_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, the MI355X
+    guide's gfx950 correction) scaled to this run's queries per launch -- the traffic is
+    linear in the queries (4 B written each; the ~62 MB of weight/aux reads per launch are
+    <1.5 %).  None when the file is absent."""
+    tf = os.path.join(ROOT, "profiles", "decoder_traffic.json")
+    if not os.path.exists(tf):
+        return None, None
+    try:
+        j = json.load(open(tf))
+        per_q = j["hbm_bytes_per_launch"] / j["queries_per_launch"]
+    except (OSError, ValueError, KeyError, ZeroDivisionError):
+        return None, None
+    return per_q * queries_per_launch, j.get("source", tf)
 
 
 def config5(args, rank, world, dev, group, gen):
     """Config 5: 1000-step DDPM sampling of ``--c5-batch`` 1024-d latents with the 1D-UNet
     (bf16 weights, hipGraph) -> fp16 MFMA decode (widen-skip decoder, L=1024) of a 512^3
-    grid, z-slab sharded over the ranks + all-gather.  Decode time = max over ranks."""
+    grid, z-slab sharded over the ranks + all-gathers.  Decode time = max over ranks."""
     import ldm_sdf
-    from ldm_sdf import ops
-    from ldm_sdf.dist import slab_bounds
     nb, N = args.c5_batch, 512
     unet = ldm_sdf.UNet1DDenoiser(D=1024, seed=2468)
     sch = ldm_sdf.DDPMSchedule()
@@ -228,64 +365,66 @@ def config5(args, rank, world, dev, group, gen):
     latents = ldm_sdf.dist.all_gather_rows(lat[:hi - lo].clone(), nb, group=group) \
         if world > 1 else lat[:nb].clone()
     dec = ldm_sdf.SDFDecoder(1024, seed=1235)            # widen-skip (L + 3 >= H)
-    pack = dec.device_pack("fp16", dev)
-    desc = pack["desc"]
-    k0, k1, _ = slab_bounds(rank, world, N)
+    from ldm_sdf import ops
+    desc = dec.device_pack("fp16", dev)["desc"]
     out = torch.empty(nb, N, N, N, device=dev)
     stream = torch.cuda.current_stream(dev)
-    ev = []
-
-    def step(timed):
-        beta = ops.decoder_fold(desc, latents.float().contiguous())
-
-        def slab(a, b, dst):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            ops.decoder_grid_fwd(desc, beta, N, a, b, out=dst)
-            e1.record(stream)
-            if timed:
-                ev.append((e0, e1))
-        if world == 1:
-            slab(0, N, out)
-        else:
-            ldm_sdf.dist.decode_sharded(slab, nb, N, dev, group=group, out=out)
-
-    step(False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t1
-    if world > 1:
-        tt = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt)
-    kms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    ach = FLOPS_PER_QUERY_WIDEN * nb * (k1 - k0) * N * N / (kms * 1e-3) / 1e12
-    H = unet.HT
+    slab = SlabTimer(desc, lambda: ops.decoder_fold(desc, latents.float().contiguous()), N,
+                     stream)
+    el = run_decode_steps(slab, nb, N, steps=1, warmup=1, world=world, group=group,
+                          device=dev, out=out, sync=torch.cuda.synchronize,
+                          on_timed=lambda: setattr(slab, "timed", True))
+    kms, qpl = slab.kernel_stats()
+    ach = FLOPS_PER_QUERY_WIDEN * qpl / (kms * 1e-3) / 1e12
     wbytes = 2 * sum(v.numel() for k, v in unet.params.items()
                      if not (k.startswith("b") or k.endswith((".b", ".b1", ".b2", ".bs"))
                              or k.startswith("Wt") or k.endswith(".p")))
-    return {"workload": f"config5: {nb} x 1000-step 1D-UNet sampling (D=1024, C=(32,64,128), "
-                        f"bf16) -> fp16 decode of a {N}^3 grid (widen-skip, L=1024), "
-                        f"z-slab over {world} rank(s)",
-            "decode_queries_per_s": nb * N ** 3 / el, "decode_s": el,
-            "decode_roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_TFLOPS["fp16"],
-                                "unit": "TFLOP/s", "frac": ach / PEAK_TFLOPS["fp16"],
-                                "flops_per_query": FLOPS_PER_QUERY_WIDEN,
-                                "avg_launch_ms": kms},
-            "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
-            "unet_graph": "hipGraph of 1000 steps x 18 ldm_conv1d launches",
-            "unet_conv_weight_bytes_per_step": wbytes}
+    res = {"workload": f"config5: {nb} x 1000-step 1D-UNet sampling (D=1024, C=(32,64,128), "
+                       f"bf16) -> fp16 decode of a {N}^3 grid (widen-skip, L=1024), "
+                       f"z-slab over {world} rank(s)",
+           "decode_queries_per_s": nb * N ** 3 / el, "decode_s": el,
+           "decode_roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_TFLOPS["fp16"],
+                               "unit": "TFLOP/s", "frac": ach / PEAK_TFLOPS["fp16"],
+                               "flops_per_query": FLOPS_PER_QUERY_WIDEN,
+                               "queries_per_launch": qpl, "avg_launch_ms": kms},
+           "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
+           "unet_graph": "hipGraph of 1000 steps x 18 ldm_conv1d launches",
+           "unet_conv_weight_bytes_per_step": wbytes}
+    if rank == 0 and not args.no_cpu:
+        res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)
+    return res
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: run this same command as N ranks under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) in a CHILD process --
+    nothing here has touched the GPU -- and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+              f"torchrun --nproc-per-node {args.gpus} (or plain python, which spawns them)",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -304,61 +443,23 @@ def main():
     decoder = ldm_sdf.SDFDecoder(256, seed=1234)
     gen = torch.Generator(device=dev).manual_seed(0)
     latents = torch.randn(B, 256, device=dev, generator=gen) * 0.1
-    pack = decoder.device_pack(args.dtype, dev)
-    desc = pack["desc"]
+    desc = decoder.device_pack(args.dtype, dev)["desc"]
     k0, k1, S = slab_bounds(rank, world, N)
-    npts_local = (k1 - k0) * N * N
     out = torch.empty(B, N, N, N, device=dev)
-    kern_ms = []
     stream = torch.cuda.current_stream(dev)
-
-    def step(timed: bool):
-        beta = ops.decoder_fold(desc, latents)
-
-        def slab(a, b, dst):
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                ops.decoder_grid_fwd(desc, beta, N, a, b, out=dst)
-                e1.record(stream)
-                kern_ms.append((e0, e1))
-            else:
-                ops.decoder_grid_fwd(desc, beta, N, a, b, out=dst)
-
-        if world == 1:
-            slab(0, N, out)
-        else:
-            ldm_sdf.dist.decode_sharded(slab, B, N, dev, group=group, out=out)
-
-    for _ in range(args.warmup):
-        step(False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt)
-    kms = sum(a.elapsed_time(b) for a, b in kern_ms) / max(1, len(kern_ms))
+    slab = SlabTimer(desc, lambda: ops.decoder_fold(desc, latents), N, stream)
+    spg = args.shapes_per_group or None
+    elapsed = run_decode_steps(slab, B, N, steps=args.steps, warmup=args.warmup, world=world,
+                               group=group, device=dev, out=out, sync=torch.cuda.synchronize,
+                               shapes_per_group=spg,
+                               on_timed=lambda: setattr(slab, "timed", True))
+    slab.timed = False
+    kms, qpl = slab.kernel_stats()
     total_q = B * N ** 3 * args.steps
     value = total_q / elapsed
-    ach = FLOPS_PER_QUERY * B * npts_local / (kms * 1e-3) / 1e12
+    ach = FLOPS_PER_QUERY * qpl / (kms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    prof_traffic = None
-    tf = os.path.join(ROOT, "profiles", "decoder_traffic.json")
-    if os.path.exists(tf):
-        try:
-            prof_traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
-        except Exception:
-            prof_traffic = None
+    traffic, traffic_src = decoder_traffic(qpl)
 
     res = None
     if rank == 0:
@@ -369,69 +470,22 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (latents N(0,0.1^2) seed 0, He-normal decoder seed 1234)",
             "config": {"workload": f"config4: decode B={B} shapes on a {N}^3 grid, z-slab sharded "
-                                   f"over {world} rank(s) + RCCL all-gather of the volume",
+                                   f"over {world} rank(s) + per-shape RCCL all-gathers of the "
+                                   "volume",
                        "batch": B, "grid": N, "latent_dim": 256, "decoder": "DeepSDF 8x512 skip@4",
                        "parallelism": f"zslab{world}"},
             "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                         "frac": ach / peak, "traffic": prof_traffic,
+                         "frac": ach / peak, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "dec_q_kernel (+qaux_pack, <0.1%)",
                          "flops_per_query": FLOPS_PER_QUERY,
-                         "queries_per_launch": B * npts_local, "avg_launch_ms": kms},
+                         "queries_per_launch": qpl, "avg_launch_ms": kms,
+                         "launches_per_step": len(slab.events) // max(1, args.steps)},
         }
-    if rank == 0 and not args.no_ddpm:
-        den = ldm_sdf.MLPDenoiser(seed=4321)
-        sch = ldm_sdf.DDPMSchedule()
-        nb = args.ddpm_batch
-        sampler = ldm_sdf.Sampler(den, sch, nb, dtype="bf16", device=dev)
-        xT = torch.randn(nb, 256, device=dev, generator=gen)
-        noise = torch.randn(1000, nb, 256, device=dev, generator=gen)
-        sampler.run(xT, noise)            # capture + first replay
-        torch.cuda.synchronize()
-        reps = 3
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            sampler.run(xT, noise)
-        torch.cuda.synchronize()
-        sps = 1000 * reps / (time.perf_counter() - t1)
-        persistent = sampler.loop is not None
-        loop_status = sampler.loop.status() if persistent else None
-        # the per-step path (6 launches per step, hipGraph-replayed) beside it, same inputs
-        sampler_g = ldm_sdf.Sampler(den, sch, nb, dtype="bf16", device=dev, persistent=False)
-        xg = sampler_g.run(xT, noise).clone()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            sampler_g.run(xT, noise)
-        torch.cuda.synchronize()
-        sps_graph = 1000 * reps / (time.perf_counter() - t1)
-        same = bool(torch.equal(sampler.run(xT, noise), xg))
-        e2e = None
-        if args.config3:   # sample -> decode on 128^3 (config 3), end-to-end latency
-            t2 = time.perf_counter()
-            lat = sampler.run(xT, noise)
-            ldm_sdf.decode(decoder, lat, 128, dtype=args.dtype)
-            torch.cuda.synchronize()
-            e2e = time.perf_counter() - t2
-        wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nb * den.D * 4
-        res["ddpm"] = {"metric": "DDPM sample steps/sec", "value": sps, "unit": "steps/s",
-                       "batch": nb, "T": 1000, "shape_steps_per_s": sps * nb,
-                       "path": ("one persistent launch for all 1000 steps "
-                                "(weights in registers, XCD-hierarchical grid barrier per "
-                                "layer)" if persistent
-                                else "hipGraph of 1000 fused steps (6 kernels each)"),
-                       "loop_status": loop_status,
-                       "graph_path": {"steps_per_s": sps_graph,
-                                      "path": "hipGraph of 1000 fused steps (6 kernels each)",
-                                      "bit_identical": same},
-                       "roofline": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
-                                    "peak": 8000.0, "unit": "GB/s",
-                                    "frac": sps * wbytes / 8e12,
-                                    "bytes_per_step": wbytes,
-                                    "note": "SURVEY §8(d) bytes: weights streamed once per "
-                                            "step + x, eps; the persistent loop holds weights "
-                                            "in registers, so it is grid-barrier-latency-bound "
-                                            "(~5 us per layer, DESIGN.md §5)"},
-                       "config3_sample_plus_decode128_s": e2e}
+    if not args.no_ddpm:
+        r = bench_ddpm(args, rank, world, dev, group, gen, decoder)
+        if rank == 0:
+            res["ddpm"] = r
     if rank == 0 and not args.no_mc:
         res["mc"] = bench_mc(out[0], args)
     if not args.no_config5:
@@ -439,34 +493,115 @@ def main():
         if rank == 0:
             res["config5"] = res_c5
     if rank == 0 and not args.no_train:
-        # config 2: DDPM training on 1k synthetic 256-d latents, MLP denoiser, bf16, batch 1000
-        den_t = ldm_sdf.MLPDenoiser(seed=4321)
-        sch_t = ldm_sdf.DDPMSchedule()
-        lat_t = torch.randn(1000, 256, device=dev, generator=gen) * 0.5
-        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16")   # warm-up
-        torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=args.train_steps, batch=1000,
-                           dtype="bf16", state=st)
-        torch.cuda.synchronize()
-        dtt = (time.perf_counter() - t3) / args.train_steps
-        H, D, nb = den_t.H, den_t.D, den_t.n_blocks
-        macs = 1000 * (H * 128 + H * H + H * D + nb * H * 2 * H + D * H)   # forward MACs
-        res["train"] = {"metric": "DDPM training steps/sec (config 2)", "value": 1.0 / dtt,
-                        "unit": "steps/s", "batch": 1000, "ms_per_step": dtt * 1e3,
-                        "tflops_fwd_bwd": 3 * 2 * macs / dtt / 1e12,
-                        "loss_first_last": [st.losses[0], st.losses[-1]]}
+        res["train"] = bench_train(args, dev, gen)
     if rank == 0 and not args.no_autodecoder:
         res["autodecoder"] = bench_autodecoder(args, dev)
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_decode(N, args.cpu_seconds)
         if "ddpm" in res:
-            res["ddpm"]["cpu_baseline"] = cpu_baseline_sampling(min(5.0, args.cpu_seconds), args.ddpm_batch)
+            res["ddpm"]["cpu_baseline"] = cpu_baseline_sampling(min(5.0, args.cpu_seconds),
+                                                                args.ddpm_batch)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_ddpm(args, rank, world, dev, group, gen, decoder):
+    """DDPM sampling, 1000 steps of ``--ddpm-batch`` latents, batch-sharded over the ranks
+    (each rank samples its shard; steps/s = 1000 / max-over-ranks time), through the default
+    ``Sampler`` path (the persistent one-launch loop) with the hipGraph per-step path timed
+    beside it on the same inputs; then config 3 end to end (sample -> decode 128^3)."""
+    import ldm_sdf
+    den = ldm_sdf.MLPDenoiser(seed=4321)
+    sch = ldm_sdf.DDPMSchedule()
+    nb = args.ddpm_batch
+    lo, hi = ldm_sdf.dist.batch_shard(nb, rank, world)
+    nl = max(1, hi - lo)
+    sampler = ldm_sdf.Sampler(den, sch, nl, dtype="bf16", device=dev)
+    xT = torch.randn(nl, 256, device=dev, generator=gen)
+    noise = torch.randn(1000, nl, 256, device=dev, generator=gen)
+    sampler.run(xT, noise)            # first launch (module load) / capture
+    reps = 3
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier(group)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        if world > 1:
+            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+            el = float(tt)
+        return 1000 * reps / el
+
+    # check=False inside the timed region (no per-run sync); the status is read right after
+    sps = timed(lambda: sampler.run(xT, noise, check=False))
+    persistent = sampler.loop is not None
+    loop_status = sampler.loop.status() if persistent else None
+    sampler_g = ldm_sdf.Sampler(den, sch, nl, dtype="bf16", device=dev, persistent=False)
+    xg = sampler_g.run(xT, noise).clone()
+    sps_graph = timed(lambda: sampler_g.run(xT, noise))
+    same = bool(torch.equal(sampler.run(xT, noise), xg))
+    e2e = None
+    if not args.no_config3:      # config 3: sample(8) -> decode 128^3, end to end
+        if world > 1:
+            dist.barrier(group)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        lat = ldm_sdf.sample(den, sch, nb, dtype="bf16", device=dev, group=group,
+                             generator=gen)
+        ldm_sdf.decode(decoder, lat, 128, dtype=args.dtype, group=group)
+        torch.cuda.synchronize()
+        e2e = time.perf_counter() - t2
+    wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nl * den.D * 4
+    return {"metric": "DDPM sample steps/sec", "value": sps, "unit": "steps/s",
+            "batch": nb, "batch_per_rank": nl, "T": 1000, "shape_steps_per_s": sps * nb,
+            "path": ("one persistent launch for all 1000 steps "
+                     "(weights in registers, XCD-hierarchical grid barrier per "
+                     "layer)" if persistent
+                     else "hipGraph of 1000 fused steps (6 kernels each)"),
+            "loop_status": loop_status,
+            "graph_path": {"steps_per_s": sps_graph,
+                           "path": "hipGraph of 1000 fused steps (6 kernels each)",
+                           "bit_identical": same},
+            "roofline": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
+                         "peak": 8000.0, "unit": "GB/s",
+                         "frac": sps * wbytes / 8e12,
+                         "bytes_per_step": wbytes,
+                         "note": "SURVEY §8(d) bytes: weights streamed once per "
+                                 "step + x, eps; the persistent loop holds weights "
+                                 "in registers, so it is grid-barrier-latency-bound "
+                                 "(DESIGN.md §5)"},
+            "config3_sample_plus_decode128_s": e2e,
+            "config3": ("sample(8) (1000 bf16 steps, fresh Sampler: includes its setup) -> "
+                        "decode(128^3, bf16), wall time" if e2e is not None else None)}
+
+
+def bench_train(args, dev, gen):
+    """Config 2: DDPM training on 1k synthetic 256-d latents, MLP denoiser, bf16, batch 1000."""
+    import ldm_sdf
+    den_t = ldm_sdf.MLPDenoiser(seed=4321)
+    sch_t = ldm_sdf.DDPMSchedule()
+    lat_t = torch.randn(1000, 256, device=dev, generator=gen) * 0.5
+    st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16")   # warm-up
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    st = ldm_sdf.train(den_t, sch_t, lat_t, steps=args.train_steps, batch=1000,
+                       dtype="bf16", state=st)
+    torch.cuda.synchronize()
+    dtt = (time.perf_counter() - t3) / args.train_steps
+    H, D, nb = den_t.H, den_t.D, den_t.n_blocks
+    macs = 1000 * (H * 128 + H * H + H * D + nb * H * 2 * H + D * H)   # forward MACs
+    return {"metric": "DDPM training steps/sec (config 2)", "value": 1.0 / dtt,
+            "unit": "steps/s", "batch": 1000, "ms_per_step": dtt * 1e3,
+            "tflops_fwd_bwd": 3 * 2 * macs / dtt / 1e12,
+            "loss_first_last": [st.losses[0], st.losses[-1]]}
 
 
 if __name__ == "__main__":

@@ -31,6 +31,9 @@ namespace ldm {
 namespace {
 
 constexpr unsigned kSpinLimit = 1u << 22;   // x s_sleep(2) ~ 0.3 s per barrier, worst case
+// The limit travels in LoopArgs::spin_limit (default kSpinLimit).  LDM_SAMPLE_LOOP_SPIN_LIMIT
+// lowers it for the timeout test (tests/test_gpu_ddpm.py): a tiny limit makes barriers give up,
+// which must surface as status 1, never as silently wrong latents.
 
 struct LoopArgs {
     const void* w_in;  const float* b_in;     // [H][D]
@@ -47,6 +50,7 @@ struct LoopArgs {
     int B, D, H, t_hi, steps;
     int hier;              // 1: XCD-hierarchical, 2: hierarchical arrival + direct poll,
                            // 0: one flat counter
+    unsigned spin_limit;   // polls before a barrier wait gives up (status 1)
 };
 
 template <typename TW, int NJ>
@@ -165,7 +169,7 @@ __device__ __forceinline__ float row_dot(const float (&w)[NJ][8], const float* x
 // of handed-off bytes are sc1 loads (stage()), so no acquire fence is needed.  Bounded: a
 // timeout raises status[0], which every poller also watches, so every workgroup exits.
 __device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned* status, unsigned target,
-                                          int* ok) {
+                                          int* ok, unsigned limit) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -178,7 +182,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned* status, unsig
                 good = 0;
                 break;
             }
-            if (++spins > kSpinLimit) {
+            if (++spins > limit) {
                 __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 good = 0;
                 break;
@@ -202,13 +206,14 @@ enum SyncLine { L_TOP = 0, L_STATUS = 1, L_START = 2, L_CNT = 3, L_ARR = 11, L_G
 constexpr size_t kSyncBytes = 4096;
 static_assert(L_COUNT * 128 <= (int)kSyncBytes, "sync words overflow");
 
-__device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, unsigned* status) {
+__device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, unsigned* status,
+                                           unsigned limit) {
     unsigned spins = 0;
     while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         if ((spins & 63) == 63 &&
             __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
             return false;
-        if (++spins > kSpinLimit) {
+        if (++spins > limit) {
             __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
@@ -222,7 +227,8 @@ __device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, u
 struct XcdState { unsigned xcc, n_local, n_active; };
 
 __device__ __forceinline__ bool grid_sync_xcd(unsigned* sync, const XcdState& xs_,
-                                              unsigned phase, int* ok, bool direct) {
+                                              unsigned phase, int* ok, bool direct,
+                                              unsigned limit) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -236,12 +242,12 @@ __device__ __forceinline__ bool grid_sync_xcd(unsigned* sync, const XcdState& xs
             __hip_atomic_fetch_add(sync + 32 * L_TOP, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         if (direct) {                                  // everyone polls the chip-wide word
-            good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status);
+            good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status, limit);
         } else if (last) {
-            good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status);
+            good = spin_until(sync + 32 * L_TOP, phase * xs_.n_active, status, limit);
             if (good) __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            good = spin_until(gen, phase, status);
+            good = spin_until(gen, phase, status, limit);
         }
         *ok = good;
     }
@@ -252,15 +258,19 @@ __device__ __forceinline__ bool grid_sync_xcd(unsigned* sync, const XcdState& xs
 
 // Start-up census for grid_sync_xcd: thread 0 of every workgroup learns its XCD, the number of
 // workgroups on it and the number of XCDs holding any.  Returns false on timeout.
-__device__ __forceinline__ bool xcd_census(unsigned* sync, unsigned G, XcdState* st, int* ok) {
+__device__ __forceinline__ bool xcd_census(unsigned* sync, unsigned G, XcdState* st, int* ok,
+                                           unsigned a_spin) {
     if (threadIdx.x == 0) {
         // HW_REG_XCC_ID (hwreg 20), bits [3:0]
         const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
         __hip_atomic_fetch_add(sync + 32 * (L_CNT + xcc), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(sync + 32 * L_START, 1u, __ATOMIC_RELAXED,
+        // release: the L_CNT add above is performed (visible at agent scope) before L_START
+        // counts this workgroup, so a waiter that sees L_START == G reads every final count
+        __hip_atomic_fetch_add(sync + 32 * L_START, 1u, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_AGENT);
-        bool good = spin_until(sync + 32 * L_START, G, sync + 32 * L_STATUS);
+        bool good = spin_until(sync + 32 * L_START, G, sync + 32 * L_STATUS, a_spin);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // once per launch
         unsigned n_act = 0, n_loc = 0;
         for (unsigned x = 0; x < 8; ++x) {
             const unsigned c = __hip_atomic_load(sync + 32 * (L_CNT + x), __ATOMIC_RELAXED,
@@ -300,7 +310,7 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
     const unsigned G = gridDim.x;
     unsigned phase = 0;
     XcdState xst = {0, 0, 0};
-    if (a.hier && !xcd_census(a.ctr, G, &xst, ok)) return;
+    if (a.hier && !xcd_census(a.ctr, G, &xst, ok, a.spin_limit)) return;
 
     for (int s = 0; s < a.steps; ++s) {
         const int t = a.t_hi - s;
@@ -328,8 +338,8 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
             if (writer) publish(a.h + (size_t)b * H + m, acc + bi);
         }
         ++phase;
-        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2)
-                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2, a.spin_limit)
+                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok, a.spin_limit))) return;
         // residual blocks: h <- h + SiLU(W_k h + E_k[t])
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
@@ -343,8 +353,8 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
                 publish(hout + (size_t)b * H + m, xs[b * H + m] + silu(pre));
             }
             ++phase;
-        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2)
-                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2, a.spin_limit)
+                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok, a.spin_limit))) return;
         }
         // out-projection with the A8 update fused
         stage(xs, a.h + (size_t)(NB & 1) * B * H, (B * H) >> 1);
@@ -359,8 +369,8 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
             }
         }
         ++phase;
-        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2)
-                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok))) return;
+        if (!(a.hier ? grid_sync_xcd(a.ctr, xst, phase, ok, a.hier == 2, a.spin_limit)
+                     : grid_sync(a.ctr + 32 * L_TOP, a.status, phase * G, ok, a.spin_limit))) return;
     }
 }
 
@@ -439,6 +449,11 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
     // arrival, every workgroup polls the chip-wide word; "flat": one counter for everything
     a.hier = (bar && bar[0] == 'f') ? 0 : (bar && bar[0] == 'd') ? 2 : 1;
     a.B = B; a.D = w->D; a.H = w->H; a.t_hi = t_hi; a.steps = steps;
+    a.spin_limit = kSpinLimit;
+    if (const char* lim = getenv("LDM_SAMPLE_LOOP_SPIN_LIMIT")) {
+        const long v = strtol(lim, nullptr, 10);
+        if (v >= 1 && v < (long)kSpinLimit) a.spin_limit = (unsigned)v;
+    }
     for (int k = 0; k < 4; ++k)
         LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
     hipStream_t st = (hipStream_t)s;

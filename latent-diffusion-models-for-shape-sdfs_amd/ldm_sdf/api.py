@@ -13,6 +13,7 @@ path in the product (the CPU restatement is oracle/, test infrastructure only).
 """
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -47,8 +48,8 @@ def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
     B = latents.shape[0]
     world, _ = ldist.world_and_rank(group)
 
-    def slab(k0: int, k1: int, dst: torch.Tensor) -> None:
-        ops.decoder_grid_fwd(desc, beta, N, k0, k1, bbox, out=dst)
+    def slab(k0: int, k1: int, dst: torch.Tensor, b0: int = 0, b1: int = B) -> None:
+        ops.decoder_grid_fwd(desc, beta[b0:b1], N, k0, k1, bbox, out=dst)
 
     if world == 1:
         vol = out if out is not None else torch.empty(B, N, N, N, device=latents.device)
@@ -102,6 +103,7 @@ class Sampler:
         # graph-replayed when use_graph.
         make_loop = getattr(denoiser, "make_loop", None)
         self.loop = None
+        self.loop_fallbacks = 0
         if persistent is not False and make_loop is not None:
             self.loop = make_loop(n, dtype, self.device, self.sd["desc"])
         if persistent and self.loop is None:
@@ -117,11 +119,27 @@ class Sampler:
     def result(self) -> torch.Tensor:
         return self.x[self.steps & 1]
 
-    def run(self, x_T: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
+    def run(self, x_T: torch.Tensor, noise: torch.Tensor, *, check: bool = True) -> torch.Tensor:
+        """x_T ``[n, D]``, noise ``[T, n, D]`` -> the sampled latents (a view of the ping-pong
+        buffer; clone it to keep it across runs).
+
+        The persistent loop's grid barriers are bounded: if one gives up (status 1, e.g. when
+        other work on the device kept part of the grid from being resident), the launch has
+        left partially updated latents.  With ``check`` (default) the status word is read back
+        (one stream synchronisation) and such a run is redone on the per-step path, which gives
+        the same numbers bit for bit; ``loop_fallbacks`` counts these.  ``check=False`` keeps
+        the call asynchronous: the caller then reads ``loop.status()`` itself."""
         self.x[0].copy_(x_T)
         self.noise[:noise.shape[0]].copy_(noise)
         if self.loop is not None:
             self.loop(self.x2, self.noise, self.T - 1, self.steps)
+            if not check or self.loop.status() == 0:
+                return self.result
+            self.loop_fallbacks += 1
+            warnings.warn("ldm_sample_loop: a grid barrier timed out (status 1); "
+                          "re-running this sample on the per-step path", RuntimeWarning)
+            self.x[0].copy_(x_T)
+            self._loop()
             return self.result
         if not self.use_graph:
             self._loop()

@@ -2,9 +2,10 @@
 (backend ``nccl`` = RCCL on ROCm, over xGMI).
 
 * Decode shards the grid by z-slab: rank r computes ``k in [r*S, min((r+1)*S, N))`` with
-  ``S = ceil(N/W)`` for every shape into a local ``[B, S, N, N]`` buffer; ONE
-  ``all_gather_into_tensor`` collects ``[W, B, S, N, N]``; because the volume is z-slowest,
-  the gathered slabs are already the volume for B == 1 and need one permute for B > 1.
+  ``S = ceil(N/W)`` for every shape into a local ``[B, S, N, N]`` buffer; per shape, one
+  ``all_gather_into_tensor(out[b], local[b])`` writes the volume in place (z-slowest, so the
+  W slabs in rank order ARE the volume), issued asynchronously group by group so the gathers
+  overlap the next group's compute.
 * Sampling and training shard the batch (data parallel); training all-reduces gradients.
 
 The compute of a slab is injected (``compute_slab``) so the partition / reassembly logic is
@@ -33,40 +34,63 @@ def slab_bounds(rank: int, world: int, N: int) -> Tuple[int, int, int]:
     return k0, k1, S
 
 
-def decode_sharded(compute_slab: Callable[[int, int, torch.Tensor], None], B: int, N: int,
+def shape_groups(B: int, per_group: Optional[int] = None):
+    """Consecutive shape ranges ``[(b0, b1), ...]`` the sharded decode computes and gathers
+    one after another.  Default: ceil(B/8) shapes per group, so up to 8 groups whose gathers
+    overlap the next group's compute."""
+    g = max(1, per_group if per_group else -(-B // 8))
+    return [(b, min(B, b + g)) for b in range(0, B, g)]
+
+
+def decode_sharded(compute_slab: Callable[..., None], B: int, N: int,
                    device: torch.device, group=None,
-                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   out: Optional[torch.Tensor] = None,
+                   shapes_per_group: Optional[int] = None) -> torch.Tensor:
     """Z-slab sharded decode + all-gather of the full volume ``[B, N, N, N]`` on every rank.
 
-    ``compute_slab(k0, k1, dst)`` fills the contiguous ``dst [B, k1-k0, N, N]``.
+    ``compute_slab(k0, k1, dst, b0, b1)`` fills the contiguous ``dst [b1-b0, k1-k0, N, N]``
+    with shapes ``[b0, b1)``.  Per shape ``b`` the volume ``out[b]`` (z slowest) is exactly the
+    W slabs in rank order, so ONE ``all_gather_into_tensor(out[b], local[b])`` assembles it in
+    place: no transpose and no second copy.  Shapes go in groups
+    (``shape_groups``); each group's gathers are issued asynchronously (RCCL runs them on its
+    own stream) before the next group's slabs are computed, so communication overlaps compute.
+    When W does not divide N the last slab is zero-padded to S = ceil(N/W) rows and the
+    gathered ``[W*S, N, N]`` is trimmed into ``out[b]``.
     """
     world, rank = world_and_rank(group)
     k0, k1, S = slab_bounds(rank, world, N)
-    local = torch.empty(B, S, N, N, device=device, dtype=torch.float32)
-    if k1 - k0 == S:
-        compute_slab(k0, k1, local)
-    else:
-        local.zero_()
-        if k1 > k0:
-            part = torch.empty(B, k1 - k0, N, N, device=device, dtype=torch.float32)
-            compute_slab(k0, k1, part)
-            local[:, :k1 - k0].copy_(part)
+    vol = out if out is not None else torch.empty(B, N, N, N, device=device,
+                                                  dtype=torch.float32)
+    if tuple(vol.shape) != (B, N, N, N) or not vol.is_contiguous():
+        raise ValueError("decode_sharded: out must be a contiguous [B, N, N, N] tensor")
     if world == 1:
-        vol = local
-    else:
-        # output as [W*B, S, N, N] (dim-0 concatenation: the form gloo and RCCL both take)
-        gathered = torch.empty(world * B, S, N, N, device=device, dtype=torch.float32)
-        dist.all_gather_into_tensor(gathered, local, group=group)
-        gathered = gathered.view(world, B, S, N, N)
-        if B == 1:
-            vol = gathered.view(1, world * S, N, N)
+        for b0, b1 in shape_groups(B, shapes_per_group):
+            compute_slab(0, N, vol[b0:b1], b0, b1)
+        return vol
+    even = S * world == N
+    local = torch.empty(B, S, N, N, device=device, dtype=torch.float32)
+    pending, staged = [], []
+    for b0, b1 in shape_groups(B, shapes_per_group):
+        if k1 - k0 == S:
+            compute_slab(k0, k1, local[b0:b1], b0, b1)
         else:
-            vol = gathered.permute(1, 0, 2, 3, 4).reshape(B, world * S, N, N)
-    vol = vol[:, :N]
-    if out is not None:
-        out.copy_(vol)
-        return out
-    return vol if vol.is_contiguous() else vol.contiguous()
+            local[b0:b1].zero_()
+            if k1 > k0:
+                part = torch.empty(b1 - b0, k1 - k0, N, N, device=device, dtype=torch.float32)
+                compute_slab(k0, k1, part, b0, b1)
+                local[b0:b1, :k1 - k0].copy_(part)
+        for b in range(b0, b1):
+            dst = vol[b] if even else torch.empty(world * S, N, N, device=device,
+                                                  dtype=torch.float32)
+            pending.append(dist.all_gather_into_tensor(dst, local[b], group=group,
+                                                       async_op=True))
+            if not even:
+                staged.append((b, dst))
+    for w in pending:
+        w.wait()
+    for b, dst in staged:
+        vol[b].copy_(dst[:N])
+    return vol
 
 
 def batch_shard(n: int, rank: int, world: int) -> Tuple[int, int]:

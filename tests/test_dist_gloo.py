@@ -26,7 +26,12 @@ def _worker(rank, world, port, fn_name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, globals()[fn_name](rank, world)))
+        if ":" in fn_name:               # "module:function" from another test file
+            import importlib
+            mod, fn = fn_name.split(":")
+            q.put((rank, getattr(importlib.import_module(mod), fn)(rank, world)))
+        else:
+            q.put((rank, globals()[fn_name](rank, world)))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, repr(e)))
     finally:
@@ -51,9 +56,9 @@ def _volume_exact(rank, world):
     B, N = 3, 11
     seen = []
 
-    def slab(k0, k1, dst):
+    def slab(k0, k1, dst, b0, b1):
         seen.append((k0, k1))
-        b = torch.arange(B).view(B, 1, 1, 1).float()
+        b = torch.arange(b0, b1).view(-1, 1, 1, 1).float()
         k = torch.arange(k0, k1).view(1, -1, 1, 1).float()
         j = torch.arange(N).view(1, 1, N, 1).float()
         i = torch.arange(N).view(1, 1, 1, N).float()
@@ -75,8 +80,8 @@ def _volume_oracle(rank, world):
     z = torch.randn(2, 16, generator=torch.Generator().manual_seed(0), dtype=torch.float64)
     N = 8
 
-    def slab(k0, k1, dst):
-        dst.copy_(R.decode_grid(p, z, N, k0, k1).float())
+    def slab(k0, k1, dst, b0, b1):
+        dst.copy_(R.decode_grid(p, z[b0:b1], N, k0, k1).float())
 
     vol = decode_sharded(slab, 2, N, torch.device("cpu"))
     full = R.decode_grid(p, z, N).float()
@@ -134,8 +139,8 @@ def test_zslab_reassembly_exact(world):
         ok, seen = res[r]
         assert ok is True, res[r]
     # N=11 over 3 ranks: slabs of 4 (last rank 3)
-    if world == 3:
-        assert res[2][1] == [(8, 11)]
+    if world == 3:          # B = 3 shapes go in 3 groups of 1 (shape_groups)
+        assert res[2][1] == [(8, 11)] * 3
 
 
 def test_zslab_oracle_matches_single_rank():

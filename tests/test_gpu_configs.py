@@ -1,0 +1,135 @@
+"""The BASELINE.json configs at their own sizes, on the MI355X, against the oracle.
+
+* config 2 -- the bf16 DDPM training step at batch 1000 on 1k latents (`BASELINE.json:8`);
+* config 3 -- 1000-step bf16 sampling of 8 latents -> bf16 decode of a 128^3 grid
+  (`BASELINE.json:9`);
+* config 5 -- fp16 decode of a 512^3 grid with the widen-skip decoder, L = 1024
+  (`BASELINE.json:11`; the UNet sampling half is pinned in test_gpu_unet.py).
+
+Config 4 (64 x 256^3 over 8 GPUs) is the bench's own step; its single-GPU numerics are the
+decoder tests', and its reassembly is covered by the gloo tests (test_dist_gloo.py).
+Full volumes are checked on random point subsets (the fp64 oracle on 134 M points would take
+hours); tolerances are SURVEY.md §8(c)'s.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+TOL = {"fp32": 2e-6, "fp16": 2e-3, "bf16": 1e-2}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ldm_sdf
+    ldm_sdf.load_library()
+    return torch.device("cuda", 0)
+
+
+def _denoiser():
+    from ldm_sdf import MLPDenoiser
+    from oracle import ref_cpu as R
+    p = R.make_denoiser_params(seed=4321)
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"], params[f"bblk{k}"] = p.Wblk[k], p.bblk[k]
+    return MLPDenoiser(params=params), p
+
+
+def test_config2_train_step_bf16_batch1000(dev):
+    """Config 2's step: 1000 latents, batch 1000, bf16 weights + matrix-core GEMMs, vs the fp64
+    oracle's autograd on the same (x0, t, eps): loss within 1e-3 relative, every gradient
+    (whole tensor) at cosine >= 0.999 and norm within 2 %."""
+    import ldm_sdf
+    from oracle import ref_cpu as R
+    model, p = _denoiser()
+    model.to_device(dev)
+    g = torch.Generator().manual_seed(2024)
+    x0 = torch.randn(1000, 256, generator=g) * 0.5
+    t = torch.randint(0, 1000, (1000,), generator=g, dtype=torch.int32)
+    eps = torch.randn(1000, 256, generator=g)
+    loss, grads = ldm_sdf.train_step(model, ldm_sdf.DDPMSchedule(), x0.to(dev), t.to(dev),
+                                     eps.to(dev), dtype="bf16")
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    want_loss, want = R.train_step_grads(p, R.ddpm_tables(), emb, x0.double(), eps.double(),
+                                         t.long())
+    assert abs(float(loss) - float(want_loss)) / float(want_loss) < 1e-3
+    for k, v in grads.items():
+        got = v.cpu().double().flatten()
+        w = want[k].flatten()
+        cos = float(got @ w / (got.norm() * w.norm() + 1e-30))
+        rel = abs(float(got.norm()) - float(w.norm())) / float(w.norm())
+        print(f"config2 grad {k}: cos {cos:.6f} norm rel {rel:.2e}")
+        assert cos >= 0.999, (k, cos)
+        assert rel <= 2e-2, (k, rel)
+
+
+def test_config3_sample8_then_decode128(dev):
+    """Config 3 end to end: sample(8) (1000 bf16 steps, the default persistent loop) ->
+    decode(128^3, bf16).  The latents are checked against the fp64 oracle on the bf16-rounded
+    weights (relative 2e-5, see test_gpu_ddpm.py), and the volume on 600 random points per
+    shape against the fp64 oracle decoder fed those same latents.  The untrained synthetic
+    denoiser drives the latents to ~1e8, where every SDF saturates at +-1, so the volume is
+    also checked for latents brought to the decoder's operating range (each shape's sampled
+    code rescaled to RMS 0.1, the synthetic-latent scale of SURVEY.md §8(d))."""
+    import ldm_sdf
+    from oracle import ref_cpu as R
+    from tests.test_gpu_ddpm import _bf16_rounded_params, _oracle_sample
+    model, p = _denoiser()
+    gen = torch.Generator().manual_seed(33)
+    xT = torch.randn(8, 256, generator=gen)
+    noise = torch.randn(1000, 8, 256, generator=gen)
+    lat = ldm_sdf.sample(model, ldm_sdf.DDPMSchedule(), 8, dtype="bf16", x_T=xT, noise=noise,
+                         device=dev)
+    want_lat = _oracle_sample(_bf16_rounded_params(p), xT, noise, 1000)
+    rel = float((lat.cpu().double() - want_lat).abs().max()) / float(want_lat.abs().max())
+    assert rel <= 2e-5, rel
+    pd = R.make_decoder_params(seed=1234)
+    dec = ldm_sdf.SDFDecoder(256, weights=pd.weights, biases=pd.biases)
+    N = 128
+    grid = torch.from_numpy(R.grid_coords_np(N)).double()
+    scaled = lat / lat.pow(2).mean(dim=1, keepdim=True).sqrt() * 0.1
+    for z in (lat, scaled):
+        vol = ldm_sdf.decode(dec, z, N, dtype="bf16")
+        assert vol.shape == (8, N, N, N) and bool(torch.isfinite(vol).all())
+        idx = torch.randint(0, N ** 3, (8, 600), generator=gen)
+        got = vol.reshape(8, -1)[torch.arange(8)[:, None], idx.to(dev)].cpu().double()
+        zc = z.cpu().double()
+        for b in range(8):
+            want = R.decoder_forward(pd, zc[b:b + 1], grid[idx[b]])[0]
+            err = float((got[b] - want).abs().max())
+            assert err <= TOL["bf16"], (b, err)
+
+
+def test_config5_decode_512_fp16_widen_skip(dev):
+    """Config 5's decode: 1 latent (L = 1024, widen-skip decoder), fp16 matrix cores, the full
+    512^3 grid (134 M queries, the size the bench runs), 2000 random points vs the fp64 oracle
+    at the fp16 tolerance, plus the grid's 8 corners and a full z-slice's finiteness."""
+    import ldm_sdf
+    from oracle import ref_cpu as R
+    p = R.make_decoder_params(L=1024, widen_skip=True, seed=1235)
+    dec = ldm_sdf.SDFDecoder(1024, weights=p.weights, biases=p.biases)
+    assert dec.widen_skip and dec.skip_width == 512
+    g = torch.Generator().manual_seed(55)
+    z = torch.randn(1, 1024, generator=g) * 0.1
+    N = 512
+    vol = ldm_sdf.decode(dec, z.to(dev), N, dtype="fp16")
+    assert vol.shape == (1, N, N, N)
+    assert bool(torch.isfinite(vol[0, 0]).all()) and bool(torch.isfinite(vol[0, -1]).all())
+    idx = torch.randint(0, N ** 3, (2000,), generator=g)
+    corners = torch.tensor([k * N * N + j * N + i for k in (0, N - 1) for j in (0, N - 1)
+                            for i in (0, N - 1)])
+    idx = torch.cat([idx, corners])
+    got = vol.reshape(-1)[idx.to(dev)].cpu().double()
+    line = (np.arange(N, dtype=np.float32) * R.grid_voxel_size(N)).astype(np.float32) \
+        + np.float32(-1.0)                                  # A1's rule, without the 1.6 GB grid
+    ii = idx.numpy()
+    xyz = torch.from_numpy(np.stack([line[ii % N], line[(ii // N) % N], line[ii // (N * N)]],
+                                    axis=1).astype(np.float32)).double()
+    want = R.decoder_forward(p, z.double(), xyz)[0]
+    err = float((got - want).abs().max())
+    print(f"config5 512^3 fp16: max abs err {err:.3e} on {idx.numel()} points")
+    assert err <= TOL["fp16"], err
