@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LDM_ABI_VERSION 1
+#define LDM_ABI_VERSION 2
 
 /* dtypes */
 #define LDM_F32 0
@@ -104,7 +104,23 @@ typedef struct ldm_denoiser {
     const float* e_tab[LDM_MAX_BLOCKS];       /* [T][H] */
     const void* w_out;  const float* b_out;   /* [D][H] */
     const float* emb_table;                   /* [T][TE] sinusoidal (A5) */
+    /* bf16 training only (ldm_denoiser_fwd / _bwd / _train_step): TRANSPOSED bf16 copies the
+     * backward's G W products read k-contiguous, kept current by ldm_adamw_multi. */
+    const void* wt_in;                        /* [D][H]  = w_in^T  (only for dx)      */
+    const void* wt_t2;                        /* [H][H]  = w_t2^T                     */
+    const void* wt_blk[LDM_MAX_BLOCKS];       /* [2H][H] = w_blk[k]^T                 */
+    const void* wt_out;                       /* [H][D]  = w_out^T                    */
 } ldm_denoiser_t;
+
+/* fp32 tensors with the denoiser's parameter shapes (gradients, masters, Adam moments). */
+typedef struct ldm_denoiser_grads {
+    float* w_in;  float* b_in;                /* [H][D], [H]   */
+    float* w_t1;  float* b_t1;                /* [H][TE], [H]  */
+    float* w_t2;  float* b_t2;                /* [H][H], [H]   */
+    float* w_blk[LDM_MAX_BLOCKS];             /* [H][2H]       */
+    float* b_blk[LDM_MAX_BLOCKS];             /* [H]           */
+    float* w_out; float* b_out;               /* [D][H], [D]   */
+} ldm_denoiser_grads_t;
 
 /* ---- library -------------------------------------------------------------------------- */
 int ldm_abi_version(void);
@@ -163,7 +179,48 @@ int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, float* x, co
                     int t_hi, int steps, int B, float* ws, size_t ws_bytes, ldm_stream_t s);
 int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host, ldm_stream_t s);
 
+/* ---- A6/A7/A9 training: denoiser forward with saved activations, backward, fused step ----
+ * bf16 weights (w->dtype == LDM_BF16, the wt_* transposed copies set), matrix-core GEMMs
+ * (ldm_gemm_bf16) with bf16 operands and fp32 accumulation, per-sample timesteps t int32 [B].
+ * `saved` is a device workspace of ldm_denoiser_train_ws_bytes(w, B) bytes (256-B aligned):
+ * the forward writes every activation the backward reads (bf16 GEMM operands in both layouts,
+ * fp32 residual stream and pre-activations); its contents are opaque.  Gradients are fp32 in
+ * the parameter shapes (ldm_denoiser_grads_t), overwritten (not accumulated).  Deterministic:
+ * fixed reduction orders, no atomics.  D, H, TE multiples of 64; n_blocks 1..8. */
+size_t ldm_denoiser_train_ws_bytes(const ldm_denoiser_t* w, int B);
+/* eps_out fp32 [B][D] = net(x, t) (may be NULL when only the saved activations are wanted). */
+int ldm_denoiser_fwd(const ldm_denoiser_t* w, const float* x, const int32_t* t, int B,
+                     float* eps_out, void* saved, ldm_stream_t s);
+/* Given deps = dL/d eps_hat fp32 [B][D] for the last ldm_denoiser_fwd on `saved`: every
+ * parameter gradient, and dx = dL/dx fp32 [B][D] when dx != NULL. */
+int ldm_denoiser_bwd(const ldm_denoiser_t* w, void* saved, const float* deps, int B,
+                     const ldm_denoiser_grads_t* grads, float* dx, ldm_stream_t s);
+/* A9 head.  xt_out (if not NULL) = sqrt(abar[t]) x0 + sqrt(1 - abar[t]) eps (bit-exact with the
+ * fp32 oracle); eps_hat (if not NULL): loss_out[0] = mean((eps_hat - eps)^2) and grad_out (if
+ * not NULL) = d loss / d eps_hat = 2 (eps_hat - eps) / (B D). */
+int ldm_q_sample_loss(const ldm_sched_t* sc, const float* x0, const float* eps,
+                      const int32_t* t, int B, int D, float* xt_out, const float* eps_hat,
+                      float* loss_out, float* grad_out, ldm_stream_t s);
+/* One whole DDPM training step's forward + backward (Alg. 1 without the optimizer):
+ * q_sample -> net -> eps-MSE (loss_out[0]) -> every gradient, the loss gradient fused into
+ * the out-projection's epilogue.  17 launches, no host synchronisation (graph-capturable). */
+int ldm_denoiser_train_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0,
+                            const float* eps, const int32_t* t, int B, void* saved,
+                            const ldm_denoiser_grads_t* grads, float* loss_out, ldm_stream_t s);
+
 /* ---- optimizer (A7 training step) -------------------------------------------------------- */
+/* Multi-tensor AdamW in ONE launch (torch.optim.AdamW's update order, as ldm_adamw_step):
+ * per tensor fp32 p, g, m, v [rows][cols]; optional bf16 working copies p_bf16 [rows][cols]
+ * and p_bf16_t [cols][rows] (transposed, for the backward's k-contiguous operands), rounded to
+ * nearest even.  `tensors` is a HOST array of n <= LDM_ADAMW_MAX_TENSORS descriptors. */
+#define LDM_ADAMW_MAX_TENSORS 40
+typedef struct ldm_adamw_tensor {
+    float* p; const float* g; float* m; float* v;
+    void* p_bf16; void* p_bf16_t;
+    int32_t rows, cols;
+} ldm_adamw_tensor_t;
+int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double lr, double beta1,
+                    double beta2, double eps, double weight_decay, int step, ldm_stream_t s);
 /* AdamW on fp32 masters p [n] with grads g, moments m, v (torch.optim.AdamW's order; step is
  * 1-based).  p_bf16 (may be NULL): bf16 [n] working copy of the updated p, written in the same
  * pass (RNE). */
@@ -252,6 +309,64 @@ int ldm_colsum_segments(const float* G, int S, int P, int M, float* out, int acc
  * coef = lambda * min(1, epoch/100) / S.  One workgroup, fixed order. */
 int ldm_latent_l2_reg(const float* z, int S, int L, float coef, float* loss_io, float* grad_io,
                       ldm_stream_t s);
+
+/* ---- grouped bf16 GEMM with fused training epilogues (csrc/gemm_bf16.hip) ---
+ * Per problem:  acc[m][n] = sum_seg sum_{k < K_seg} A_seg[m][k] B_seg[n][k]
+ * A_seg / B_seg: bf16, k contiguous (row strides lda / ldb in elements, multiples of 8, 16-B
+ * aligned), K_seg a multiple of 64.  A K-concatenation ([h || temb] [W | U]^T) is two segments.
+ * Rows m >= M_valid are padding: R / P_in / C are not read there and the fp32 outputs (C, P) not
+ * written (so caller buffers need only M_valid rows), the bf16 outputs Cb / CbT get zeros (so
+ * operand buffers padded to M rows stay zero-padded), and they add nothing to colsum / loss.
+ * Epilogue, with pre = acc + bias[n] (bias optional):
+ *   LDM_GEMM_STORE       out = pre
+ *   LDM_GEMM_SILU        out = SiLU(pre);        P = pre (if P)
+ *   LDM_GEMM_RESID_SILU  out = R + SiLU(pre);    P = pre (if P)                 (A6 block)
+ *   LDM_GEMM_RELU        out = max(pre, 0)
+ *   LDM_GEMM_ACCUM       out = C + pre
+ *   LDM_GEMM_DGRAD_SILU  dh = (R +) pre -> C;  out = dh * SiLU'(P_in)  (A7: the gradient at the
+ *                        layer below's pre-activation, fused into the G W product)
+ *   LDM_GEMM_LOSS        d = pre - P_in (targets); out = scale * d; loss_part += d^2 (A9)
+ *   LDM_GEMM_ADD_R       out = R + pre
+ * Outputs (each optional): C fp32 [m][n] (ldc; in DGRAD_SILU C receives dh), Cb bf16 [m][n]
+ * (ldcb), CbT bf16 TRANSPOSED [n][m] (ldct; M and ldct multiples of 4), colsum fp32
+ * [ceil(M/32)][N]: per 32-row block column sums of out (bias gradients, summed in fixed order
+ * by the caller), loss_part fp32 [ceil(M/32)][ceil(N/32)]: sums of d^2 (LOSS).
+ * Up to LDM_GEMM_MAX_PROBS independent problems share one launch.  tile: 0 = auto, 1 = 64x64,
+ * 2 = 128x64, 3 = 128x128, 4 = 64x64 with a 3-deep ring. */
+#define LDM_GEMM_MAX_SEGS 8
+#define LDM_GEMM_MAX_PROBS 4
+#define LDM_GEMM_STORE 0
+#define LDM_GEMM_SILU 1
+#define LDM_GEMM_RESID_SILU 2
+#define LDM_GEMM_RELU 3
+#define LDM_GEMM_ACCUM 4
+#define LDM_GEMM_DGRAD_SILU 5
+#define LDM_GEMM_LOSS 6
+#define LDM_GEMM_ADD_R 7
+typedef struct ldm_gemm_seg {
+    const void* A; const void* B;    /* bf16 */
+    int64_t lda, ldb;
+    int32_t K, reserved;
+} ldm_gemm_seg_t;
+typedef struct ldm_gemm_prob {
+    int32_t M, N, M_valid, n_seg;
+    ldm_gemm_seg_t seg[LDM_GEMM_MAX_SEGS];
+    int32_t mode; float scale;
+    const float* bias;
+    const float* R;    int64_t ldr;
+    const float* P_in; int64_t ldp_in;
+    float* C;          int64_t ldc;
+    float* P;          int64_t ldp;
+    void* Cb;          int64_t ldcb;
+    void* CbT;         int64_t ldct;
+    float* colsum;
+    float* loss_part;
+} ldm_gemm_prob_t;
+typedef struct ldm_gemm_args {
+    int32_t n_prob, tile;
+    ldm_gemm_prob_t prob[LDM_GEMM_MAX_PROBS];
+} ldm_gemm_args_t;
+int ldm_gemm_bf16(const ldm_gemm_args_t* a, ldm_stream_t s);
 
 /* ---- C17 1D-UNet denoiser: fused conv1d (implicit GEMM) ------------------ */
 /* Y[b][co][l] = epi( sum_s sum_{ci<C_s} sum_{k<ksize_s} W_s(co,ci,k) * act_s(Xsrc_s(b,ci,l,k))

@@ -1,0 +1,353 @@
+// Grouped bf16 GEMM with fused training epilogues (ldm_gemm_bf16): the matrix-core engine of
+// the DDPM denoiser's training step (A6/A7 at batch 1000, config 2) and of the C19 auto-decoder.
+//
+//   C[m][n] = sum_seg sum_{k < K_seg} A_seg[m][k] * B_seg[n][k]      (both operands bf16,
+//                                                                     k contiguous: "NT")
+// then one epilogue per problem (include/ldm_sdf.h LDM_GEMM_*): bias, SiLU / residual+SiLU /
+// ReLU, the SiLU backward of the layer below, the eps-MSE gradient, accumulation; outputs in
+// fp32, bf16 and bf16 TRANSPOSED ([n][m]), plus per-32-row column sums (bias gradients) and
+// per-tile loss sums -- all written from the accumulators, so every operand the next GEMM
+// needs is produced here in the layout it wants (k contiguous).  No GEMM reads a transposed
+// view; no separate cast / transpose / colsum / silu-backward launch exists.
+//
+// Why this shape (PMC in profiles/r02a/pmc_train): the generic ldm_linear MFMA
+// kernel staged fp32 operands through registers one 128-deep chunk at a time and sat at 3-4 %
+// MFMA busy, 51-59 % of wave time parked on memory.  Here
+//   * operands are bf16 in HBM (half the bytes) and arrive by LDS-DMA (global_load_lds, 16 B
+//     per lane, no VGPR staging) into a STAGES-deep ring: STAGES-1 k-steps in flight across raw
+//     s_barriers, retired by a counted vmcnt (never 0 in the steady state);
+//   * the LDS image is lane-linear per DMA instruction (8 rows x 128 B) with the 16-byte chunks
+//     of row r XOR-permuted by (r >> 1) & 7 on the SOURCE address, so the ds_read_b128 fragment
+//     reads of 16 rows are conflict-free (guide T2, rule 21);
+//   * several independent GEMMs can share one launch (problems), so small backward products
+//     fill the chip together.
+// Tiles: BM x BN per 4-wave workgroup (64 or 128 each), each wave (BM/2) x (BN/2) as
+// RM x RN v_mfma_f32_32x32x16_bf16 tiles; k-step 64.
+#include "ldm_internal.h"
+#include "ddpm_common.h"
+
+#include <algorithm>
+
+namespace ldm {
+namespace {
+
+constexpr int kBK = 64;                 // k per ring stage (128 B per operand row)
+
+__device__ __forceinline__ unsigned pack2_bf16(float a, float b) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 v = {a, b};
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+
+// Issue the LDS-DMA pieces of one operand tile (ROWS x 64 k) of stage `ks` into LDS at `dst`.
+// Piece i (1 KiB) = tile rows 8i..8i+7; wave w issues pieces w, w+4, ...  Lane L: row 8i+L/8,
+// LDS chunk L%8 <- global chunk (L%8) ^ ((row >> 1) & 7).
+// Per-lane source pointers of one operand tile (ROWS x 64 k): piece i (1 KiB) = tile rows
+// 8i..8i+7; wave w issues pieces w, w+4, ...  Lane L: row 8i+L/8, LDS chunk L%8 <- global chunk
+// (L%8) ^ ((row >> 1) & 7).  Rows past the end are clamped (valid bytes, never stored).
+template <int ROWS>
+struct TileSrc {
+    const unsigned short* p[ROWS / 32];
+    __device__ __forceinline__ void init(const unsigned short* src, int64_t ld, int row0,
+                                         int nrows, int wave, int lane) {
+        const int rl = lane >> 3, cc = lane & 7;
+#pragma unroll
+        for (int j = 0; j < ROWS / 32; ++j) {
+            const int rr = 8 * (wave + 4 * j) + rl;
+            const int row = min(row0 + rr, nrows - 1);
+            p[j] = src + (int64_t)row * ld + 8 * (cc ^ ((rr >> 1) & 7));
+        }
+    }
+    // issue the stage at k offset kk into LDS `dst`, then step to the next 64 k
+    __device__ __forceinline__ void issue(unsigned short* dst, int wave) {
+#pragma unroll
+        for (int j = 0; j < ROWS / 32; ++j) {
+            __builtin_amdgcn_global_load_lds(
+                (const void*)p[j],
+                (__attribute__((address_space(3))) void*)(dst + (wave + 4 * j) * 512), 16, 0, 0);
+            p[j] += kBK;
+        }
+    }
+};
+
+__device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, int chunk) {
+    const int c = chunk ^ ((row >> 1) & 7);
+    return *reinterpret_cast<const u32x4*>(tile + row * kBK + 8 * c);
+}
+
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(ldm_gemm_args_t a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+    constexpr int RM = BM / 64, RN = BN / 64;
+    constexpr int A_ELEMS = BM * kBK, STAGE_ELEMS = (BM + BN) * kBK;
+    constexpr int G = (BM + BN) / 32;                 // DMA pieces per wave per stage
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+
+    // ---- which problem / tile: XCD-aware deal of the linear workgroup id (bijective) ------
+    // The argument block is read through the kernarg segment pointer (scalar loads at a
+    // runtime offset); indexing the by-value parameter by a runtime problem id would copy it
+    // to scratch.
+    typedef const __attribute__((address_space(4))) ldm_gemm_args_t KArgs;
+    KArgs* ka = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int np = ka->n_prob;
+    int total = 0, p = 0, first = 0, tm_n = 1, tn_n = 1;
+    const int lid = blockIdx.x;
+    int tot_all = 0;
+#pragma unroll
+    for (int i = 0; i < LDM_GEMM_MAX_PROBS; ++i)
+        if (i < np)
+            tot_all += ((ka->prob[i].M + BM - 1) / BM) * ((ka->prob[i].N + BN - 1) / BN);
+    int t;
+    {
+        const int q = tot_all / 8, r = tot_all % 8, x = lid % 8;
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
+    }
+#pragma unroll
+    for (int i = 0; i < LDM_GEMM_MAX_PROBS; ++i) {
+        if (i < np) {
+            const int tm = (ka->prob[i].M + BM - 1) / BM, tn = (ka->prob[i].N + BN - 1) / BN;
+            if (t >= total) { p = i; first = total; tm_n = tm; tn_n = tn; }
+            total += tm * tn;
+        }
+    }
+    const __attribute__((address_space(4))) ldm_gemm_prob_t& P = ka->prob[p];
+    const int tl = t - first;
+    // tiles in groups of 4 tile-rows, column-major inside a group (L2 reuse of both panels)
+    const int grp = tl / (4 * tn_n), gh = min(4, tm_n - grp * 4), in = tl - grp * 4 * tn_n;
+    const int m0 = (grp * 4 + in % gh) * BM, n0 = (in / gh) * BN;
+
+    // ---- k schedule over the segments -------------------------------------------------------
+    int nk = 0;
+    for (int s = 0; s < P.n_seg; ++s) nk += P.seg[s].K / kBK;
+
+    // DMA sources advance 64 k per issued stage; they are re-seated at each segment start.
+    TileSrc<BM> srcA;
+    TileSrc<BN> srcB;
+    int seg = -1, seg_left = 0;
+    auto issue = [&](int slot) {
+        if (seg_left == 0) {
+            ++seg;
+            const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[seg];
+            srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
+            srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
+            seg_left = S.K / kBK;
+        }
+        unsigned short* st = smem + slot * STAGE_ELEMS;
+        srcA.issue(st, wave);
+        srcB.issue(st + A_ELEMS, wave);
+        --seg_left;
+    };
+
+    f32x16 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) issue(s);
+
+    const int r32 = lane & 31, h = lane >> 5;
+    for (int ks = 0; ks < nk; ++ks) {
+        // RAW: this wave's pieces of stage ks landed (STAGES-2 younger stages may still fly),
+        // then the barrier makes every wave's pieces visible and retires every wave's reads of
+        // stage ks-1, whose slot the issue below refills (WAR).
+        if (ks + STAGES - 2 < nk)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((STAGES - 2) * G) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (ks + STAGES - 1 < nk) issue((ks + STAGES - 1) % STAGES);
+        const unsigned short* sa = smem + (ks % STAGES) * STAGE_ELEMS;
+        const unsigned short* sb = sa + A_ELEMS;
+        // every fragment of the stage first (one LDS round trip), then the MFMAs
+        u32x4 af[kBK / 16][RM], bf[kBK / 16][RN];
+#pragma unroll
+        for (int s = 0; s < kBK / 16; ++s) {
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+                af[s][i] = read_frag(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+                bf[s][j] = read_frag(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
+        }
+        __builtin_amdgcn_sched_barrier(0);     // keep the reads batched ahead of the MFMAs
+#pragma unroll
+        for (int s = 0; s < kBK / 16; ++s)
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        __builtin_bit_cast(bf16x8, af[s][i]), __builtin_bit_cast(bf16x8, bf[s][j]),
+                        acc[i][j], 0, 0, 0);
+    }
+
+    // ---- epilogue ------------------------------------------------------------------------
+    // Called once per accumulator tile with compile-time (i, j), so every acc index stays a
+    // constant (a runtime-indexed accumulator array goes to scratch: guide rule 20).
+    const int mode = P.mode;
+    auto epi = [&](const f32x16& c, const int i, const int j) {
+        const int rb = m0 + wr * (BM / 2) + i * 32;           // first row of this 32-row block
+        {
+            const int n = n0 + wc * (BN / 2) + j * 32 + r32;
+            const bool ncol = n < P.N;
+            const int nn = ncol ? n : P.N - 1;
+            const float bias = P.bias ? P.bias[nn] : 0.f;
+            float out[16];
+            float lsum = 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
+                const bool live = ncol && b < P.M_valid;   // padding rows: nothing read / fp32 kept
+                const bool inb = ncol && b < P.M;
+                const int bb = live ? b : 0;
+                const int64_t ir = (int64_t)bb * P.ldr + nn, ip = (int64_t)bb * P.ldp_in + nn;
+                const int64_t ic = (int64_t)bb * P.ldc + nn;
+                const float pre = c[v] + bias;
+                float o = pre;
+                switch (mode) {
+                    case LDM_GEMM_SILU:
+                        if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
+                        o = silu(pre);
+                        break;
+                    case LDM_GEMM_RESID_SILU:
+                        if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
+                        o = (live ? P.R[ir] : 0.f) + silu(pre);
+                        break;
+                    case LDM_GEMM_RELU: o = fmaxf(pre, 0.f); break;
+                    case LDM_GEMM_ACCUM: o = (live ? P.C[ic] : 0.f) + pre; break;
+                    case LDM_GEMM_ADD_R: o = (live ? P.R[ir] : 0.f) + pre; break;
+                    case LDM_GEMM_DGRAD_SILU: {
+                        const float dh = (P.R && live) ? P.R[ir] + pre : pre;
+                        if (P.C && live) P.C[ic] = dh;
+                        o = dh * silu_grad(live ? P.P_in[ip] : 0.f);
+                        break;
+                    }
+                    case LDM_GEMM_LOSS: {
+                        const float d = pre - (live ? P.P_in[ip] : 0.f);
+                        lsum += live ? d * d : 0.f;
+                        o = P.scale * d;
+                        break;
+                    }
+                    default: break;
+                }
+                out[v] = live ? o : 0.f;
+                if (mode != LDM_GEMM_DGRAD_SILU && P.C && live) P.C[ic] = out[v];
+                if (P.Cb && inb)
+                    reinterpret_cast<unsigned short*>(P.Cb)[(int64_t)b * P.ldcb + nn] =
+                        (unsigned short)(pack2_bf16(out[v], 0.f) & 0xffffu);
+            }
+            if (P.CbT && ncol) {                 // [n][b]: 4 consecutive rows per 8-byte store
+                unsigned short* T = reinterpret_cast<unsigned short*>(P.CbT) + (int64_t)n * P.ldct;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int b = rb + 8 * g + 4 * h;
+                    if (b < P.M) {
+                        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                        const u32x2 w = {pack2_bf16(out[4 * g], out[4 * g + 1]),
+                                         pack2_bf16(out[4 * g + 2], out[4 * g + 3])};
+                        *reinterpret_cast<u32x2*>(T + b) = w;
+                    }
+                }
+            }
+            if (P.colsum) {                      // one partial per 32-row block and column
+                float cs = 0.f;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) cs += out[v];
+                cs += __shfl_xor(cs, 32);
+                if (h == 0 && ncol && rb < P.M) P.colsum[(int64_t)(rb / 32) * P.N + n] = cs;
+            }
+            if (mode == LDM_GEMM_LOSS && P.loss_part) {
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
+                if (lane == 0 && rb < P.M)
+                    P.loss_part[(int64_t)(rb / 32) * ((P.N + 31) / 32) + (n0 + wc * (BN / 2) + j * 32) / 32] = lsum;
+            }
+        }
+    };
+    epi(acc[0][0], 0, 0);
+    if constexpr (RN > 1) epi(acc[0][RN - 1], 0, 1);
+    if constexpr (RM > 1) epi(acc[RM - 1][0], 1, 0);
+    if constexpr (RM > 1 && RN > 1) epi(acc[RM - 1][RN - 1], 1, 1);
+}
+
+template <int BM, int BN, int STAGES>
+int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
+    auto* k = &gemm_bf16_kernel<BM, BN, STAGES>;
+    constexpr int lds = STAGES * (BM + BN) * kBK * 2;
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_gemm_bf16: hipFuncSetAttribute: %s",
+                    hipGetErrorString(e));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(total), dim3(256), lds, s, a);
+    return launch_status("ldm_gemm_bf16");
+}
+
+}  // namespace
+
+int gemm_tiles(const ldm_gemm_args_t& a, int bm, int bn) {
+    int total = 0;
+    for (int p = 0; p < a.n_prob; ++p)
+        total += ((a.prob[p].M + bm - 1) / bm) * ((a.prob[p].N + bn - 1) / bn);
+    return total;
+}
+
+int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
+    LDM_REQUIRE(a.n_prob >= 1 && a.n_prob <= LDM_GEMM_MAX_PROBS, LDM_EINVAL,
+                "ldm_gemm_bf16: n_prob %d", a.n_prob);
+    for (int p = 0; p < a.n_prob; ++p) {
+        const ldm_gemm_prob_t& P = a.prob[p];
+        LDM_REQUIRE(P.M >= 1 && P.N >= 1 && P.M_valid >= 0 && P.M_valid <= P.M &&
+                        P.n_seg >= 1 && P.n_seg <= LDM_GEMM_MAX_SEGS,
+                    LDM_EINVAL, "ldm_gemm_bf16: problem %d: M=%d N=%d M_valid=%d n_seg=%d", p,
+                    P.M, P.N, P.M_valid, P.n_seg);
+        for (int s = 0; s < P.n_seg; ++s) {
+            const ldm_gemm_seg_t& S = P.seg[s];
+            LDM_REQUIRE(S.A && S.B && S.K > 0 && S.K % kBK == 0, LDM_EINVAL,
+                        "ldm_gemm_bf16: problem %d seg %d: K=%d must be a positive multiple of 64",
+                        p, s, S.K);
+            LDM_REQUIRE(LDM_ALIGNED(S.A, 16) && LDM_ALIGNED(S.B, 16) && S.lda % 8 == 0 &&
+                            S.ldb % 8 == 0 && S.lda >= S.K && S.ldb >= S.K,
+                        LDM_EALIGN, "ldm_gemm_bf16: problem %d seg %d: operands must be 16-B "
+                        "aligned with row strides a multiple of 8 elements", p, s);
+        }
+        LDM_REQUIRE(P.mode >= LDM_GEMM_STORE && P.mode <= LDM_GEMM_ADD_R, LDM_EINVAL,
+                    "ldm_gemm_bf16: problem %d: mode %d", p, P.mode);
+        const bool needR = P.mode == LDM_GEMM_RESID_SILU || P.mode == LDM_GEMM_ADD_R;
+        const bool needPin = P.mode == LDM_GEMM_DGRAD_SILU || P.mode == LDM_GEMM_LOSS;
+        LDM_REQUIRE((!needR || P.R) && (!needPin || P.P_in) &&
+                        (P.mode != LDM_GEMM_ACCUM || P.C),
+                    LDM_EINVAL, "ldm_gemm_bf16: problem %d: mode %d operand missing", p, P.mode);
+        LDM_REQUIRE(!P.CbT || (LDM_ALIGNED(P.CbT, 8) && P.ldct % 4 == 0 && P.M % 4 == 0),
+                    LDM_EALIGN, "ldm_gemm_bf16: problem %d: transposed output needs 8-B "
+                    "alignment, ldct and M multiples of 4", p);
+    }
+    // tile: 128 x 128 once the 64 x 64 grid has >= 8 workgroups per CU (C19's 1M-row
+    // products); else 64 x 64 (config 2: 256-768 workgroups)
+    int tile = a.tile;
+    if (tile == 0) tile = gemm_tiles(a, 64, 64) >= 2048 ? 3 : 1;
+    switch (tile) {
+        case 1: return launch_gemm<64, 64, 4>(a, gemm_tiles(a, 64, 64), s);
+        case 2: return launch_gemm<128, 64, 4>(a, gemm_tiles(a, 128, 64), s);
+        case 3: return launch_gemm<128, 128, 3>(a, gemm_tiles(a, 128, 128), s);
+        case 4: return launch_gemm<64, 64, 3>(a, gemm_tiles(a, 64, 64), s);
+        default: break;
+    }
+    set_error("ldm_gemm_bf16: tile %d", tile);
+    return LDM_EINVAL;
+}
+
+}  // namespace ldm
+
+extern "C" int ldm_gemm_bf16(const ldm_gemm_args_t* a, ldm_stream_t s) {
+    LDM_REQUIRE(a != nullptr, LDM_EINVAL, "ldm_gemm_bf16: null args");
+    return ldm::gemm_bf16(*a, (hipStream_t)s);
+}

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("LDM_SDF_LIB", LIB_PATH)
 HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                             "..", "..", "include", "ldm_sdf.h"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER = 0, 1
@@ -54,7 +54,23 @@ class Denoiser(C.Structure):
                 ("w_in", _vp), ("b_in", _vp), ("w_t1", _vp), ("b_t1", _vp), ("w_t2", _vp),
                 ("b_t2", _vp), ("w_blk", _vp * MAX_BLOCKS), ("b_blk", _vp * MAX_BLOCKS),
                 ("e_tab", _vp * MAX_BLOCKS), ("w_out", _vp), ("b_out", _vp),
-                ("emb_table", _vp)]
+                ("emb_table", _vp), ("wt_in", _vp), ("wt_t2", _vp),
+                ("wt_blk", _vp * MAX_BLOCKS), ("wt_out", _vp)]
+
+
+class DenoiserGrads(C.Structure):
+    """fp32 tensors in the denoiser's parameter shapes (ldm_denoiser_grads_t)."""
+    _fields_ = [("w_in", _vp), ("b_in", _vp), ("w_t1", _vp), ("b_t1", _vp), ("w_t2", _vp),
+                ("b_t2", _vp), ("w_blk", _vp * MAX_BLOCKS), ("b_blk", _vp * MAX_BLOCKS),
+                ("w_out", _vp), ("b_out", _vp)]
+
+
+ADAMW_MAX_TENSORS = 40
+
+
+class AdamwTensor(C.Structure):
+    _fields_ = [("p", _vp), ("g", _vp), ("m", _vp), ("v", _vp), ("p_bf16", _vp),
+                ("p_bf16_t", _vp), ("rows", C.c_int32), ("cols", C.c_int32)]
 
 
 class LinearArgs(C.Structure):
@@ -68,6 +84,29 @@ class LinearArgs(C.Structure):
                 ("Y", _vp), ("syb", C.c_int64), ("sym", C.c_int64),
                 ("A_out", _vp), ("sab", C.c_int64), ("compute", C.c_int32),
                 ("ws", _vp), ("ws_floats", C.c_int64)]
+
+
+GEMM_MAX_SEGS, GEMM_MAX_PROBS = 8, 4
+(GEMM_STORE, GEMM_SILU, GEMM_RESID_SILU, GEMM_RELU, GEMM_ACCUM, GEMM_DGRAD_SILU, GEMM_LOSS,
+ GEMM_ADD_R) = range(8)
+
+
+class GemmSeg(C.Structure):
+    _fields_ = [("A", _vp), ("B", _vp), ("lda", C.c_int64), ("ldb", C.c_int64),
+                ("K", C.c_int32), ("reserved", C.c_int32)]
+
+
+class GemmProb(C.Structure):
+    _fields_ = [("M", C.c_int32), ("N", C.c_int32), ("M_valid", C.c_int32), ("n_seg", C.c_int32),
+                ("seg", GemmSeg * GEMM_MAX_SEGS), ("mode", C.c_int32), ("scale", C.c_float),
+                ("bias", _vp), ("R", _vp), ("ldr", C.c_int64), ("P_in", _vp),
+                ("ldp_in", C.c_int64), ("C", _vp), ("ldc", C.c_int64), ("P", _vp),
+                ("ldp", C.c_int64), ("Cb", _vp), ("ldcb", C.c_int64), ("CbT", _vp),
+                ("ldct", C.c_int64), ("colsum", _vp), ("loss_part", _vp)]
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("n_prob", C.c_int32), ("tile", C.c_int32), ("prob", GemmProb * GEMM_MAX_PROBS)]
 
 
 CONV_DIRECT, CONV_UP2 = 0, 1
@@ -126,6 +165,16 @@ SIGNATURES = [
     ("ldm_colsum_segments", _i, [_fp, _i, _i, _i, _fp, _i, _vp]),
     ("ldm_latent_l2_reg", _i, [_fp, _i, _i, _f, _fp, _fp, _vp]),
     ("ldm_conv1d", _i, [C.POINTER(ConvArgs), _vp]),
+    ("ldm_gemm_bf16", _i, [C.POINTER(GemmArgs), _vp]),
+    ("ldm_denoiser_train_ws_bytes", _sz, [C.POINTER(Denoiser), _i]),
+    ("ldm_denoiser_fwd", _i, [C.POINTER(Denoiser), _fp, _vp, _i, _fp, _vp, _vp]),
+    ("ldm_denoiser_bwd", _i, [C.POINTER(Denoiser), _vp, _fp, _i, C.POINTER(DenoiserGrads), _fp,
+                              _vp]),
+    ("ldm_q_sample_loss", _i, [C.POINTER(Sched), _fp, _fp, _vp, _i, _i, _fp, _fp, _fp, _fp, _vp]),
+    ("ldm_denoiser_train_step", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _vp, _i,
+                                     _vp, C.POINTER(DenoiserGrads), _fp, _vp]),
+    ("ldm_adamw_multi", _i, [C.POINTER(AdamwTensor), _i, C.c_double, C.c_double, C.c_double,
+                             C.c_double, C.c_double, _i, _vp]),
     ("ldm_mc_workspace_bytes", _sz, [_i]),
     ("ldm_mc_count", _i, [_fp, _i, _f, _vp, _sz, _vp, _vp]),
     ("ldm_mc_emit", _i, [_fp, _i, _f, _f, _f, _vp, _sz, _fp, _vp, _vp]),

@@ -195,6 +195,8 @@ class TrainState:
     masters: Optional[Dict[str, torch.Tensor]] = None
     adam: Optional[Dict[str, Tuple[torch.Tensor, torch.Tensor]]] = None   # fused AdamW (m, v)
     hparams: Dict[str, float] = field(default_factory=dict)
+    adam_table: Optional[object] = None     # ldm_adamw_multi descriptors (bf16 path)
+    adam_grads: Optional[Dict[str, torch.Tensor]] = None
 
 
 def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
@@ -208,13 +210,24 @@ def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
     device = x0.device
     dev = denoiser.device_pack(dtype, device, with_tables=False)
     sd = schedule.device(device)
+    if grads is None:
+        grads = {n: torch.empty_like(denoiser.params[n], device=device) for n in denoiser.names()}
+    if dtype == "bf16":
+        # the fused C-ABI step (ldm_denoiser_train_step): q_sample, forward, eps-MSE and the
+        # whole backward as ldm_gemm_bf16 problems with fused epilogues, one host call
+        B = x0.shape[0]
+        ws = denoiser.train_workspace(B, device)
+        loss = torch.empty(1, device=device, dtype=torch.float32)
+        ops.denoiser_train_step(dev["desc"], sd["desc"], x0.float().contiguous(),
+                                eps.float().contiguous(), t.to(torch.int32).contiguous(), ws,
+                                denoiser.grads_struct(grads), loss)
+        ldist.allreduce_mean_([grads[n] for n in denoiser.names()], group=group)
+        return loss, grads
     xt = ops.q_sample(sd["desc"], x0.contiguous(), eps.contiguous(), t.to(torch.int32).contiguous())
     cp = capi.COMPUTE_CODES[dtype]
     eps_hat, sv = ops.denoiser_forward_train(denoiser, dev, xt, t.to(torch.int32).contiguous(),
                                              compute=cp)
     loss, g_out = ops.eps_mse_loss(eps_hat, eps.contiguous())
-    if grads is None:
-        grads = {n: torch.empty_like(denoiser.params[n], device=device) for n in denoiser.names()}
     ops.denoiser_backward_train(denoiser, dev, sv, g_out, grads, compute=cp)
     ldist.allreduce_mean_([grads[n] for n in denoiser.names()], group=group)
     return loss, grads
@@ -246,7 +259,8 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         state.adam = {n: (torch.zeros_like(v), torch.zeros_like(v))
                       for n, v in state.masters.items()}
         state.hparams = dict(lr=lr, weight_decay=weight_decay)
-    grads = {n: torch.empty_like(v) for n, v in state.masters.items()}
+    grads = state.adam_grads if state.adam_grads is not None else \
+        {n: torch.empty_like(v) for n, v in state.masters.items()}
     T = schedule.T
     for _ in range(steps):
         idx = torch.randint(0, M, (batch,), device=device, generator=generator) \
@@ -262,6 +276,20 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
                 p.grad = grads[n]
             state.optimizer.step()
             denoiser.invalidate()
+        elif dtype == "bf16":
+            # one launch for every tensor: fp32 masters + Adam moments, and the bf16 working
+            # copies (both layouts) the next step's GEMMs read
+            if state.adam_table is None:
+                work = denoiser.device_pack(dtype, device, with_tables=False)
+                state.adam_table = ops.adamw_table(
+                    [(p, grads[n], *state.adam[n], work[n] if n.startswith("W") else None,
+                      work.get(n + "_T")) for n, p in state.masters.items()])
+                state.adam_grads = grads
+            if state.adam_grads is not grads:
+                raise RuntimeError("train: gradient buffers changed under the AdamW table")
+            ops.adamw_multi(state.adam_table, lr=state.hparams["lr"],
+                            weight_decay=state.hparams["weight_decay"], step=state.step + 1,
+                            device=device)
         else:
             work = denoiser.device_pack(dtype, device, with_tables=False)
             for n, p in state.masters.items():
@@ -276,5 +304,6 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         state.losses.append(loss)
     if state.optimizer is None:
         denoiser.invalidate()    # E tables (sampling) are rebuilt from the trained masters
+        state.adam_table = None  # ... and so are the working copies the table pointed at
     state.losses = [float(l) if isinstance(l, torch.Tensor) else l for l in state.losses]
     return state

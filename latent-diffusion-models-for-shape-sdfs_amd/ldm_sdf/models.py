@@ -237,6 +237,23 @@ class MLPDenoiser:
         self.params = {k: v.to(device) for k, v in self.params.items()}
         self.emb_table = self.emb_table.to(device)
         self._dev.clear()
+        self._train_ws = {}
+
+    def train_workspace(self, B: int, device) -> torch.Tensor:
+        """The ``saved`` activations workspace of the bf16 C-ABI training path (cached per
+        batch size and device; contents are per call)."""
+        from . import ops
+        key = (torch.device(device), int(B))
+        ws = getattr(self, "_train_ws", {})
+        self._train_ws = ws
+        if key not in ws:
+            ws[key] = ops.train_workspace(self.device_pack("bf16", device, with_tables=False)["desc"],
+                                          B, device)
+        return ws[key]
+
+    def grads_struct(self, grads: Dict[str, torch.Tensor]):
+        from . import ops
+        return ops.grads_struct(grads, self.n_blocks)
 
     def invalidate(self) -> None:
         """Call after the fp32 masters changed (training): drops packed copies / E tables."""
@@ -293,6 +310,15 @@ class MLPDenoiser:
             desc.b_blk[k] = dev[f"bblk{k}"].data_ptr()
         desc.w_out, desc.b_out = dev["Wout"].data_ptr(), dev["bout"].data_ptr()
         desc.emb_table = dev["emb_table"].data_ptr()
+        if dtype == "bf16":
+            # transposed bf16 copies for the backward's G W products (ldm_denoiser_bwd /
+            # _train_step read every operand k-contiguous); ldm_adamw_multi keeps them current
+            for n in ["Win", "Wt2", "Wout"] + [f"Wblk{k}" for k in range(self.n_blocks)]:
+                dev[n + "_T"] = dev[n].t().contiguous()
+            desc.wt_in, desc.wt_t2 = dev["Win_T"].data_ptr(), dev["Wt2_T"].data_ptr()
+            desc.wt_out = dev["Wout_T"].data_ptr()
+            for k in range(self.n_blocks):
+                desc.wt_blk[k] = dev[f"Wblk{k}_T"].data_ptr()
         dev["desc"] = desc
         self._dev[key] = dev
         if with_tables:

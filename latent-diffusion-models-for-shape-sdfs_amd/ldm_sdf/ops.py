@@ -355,6 +355,79 @@ def latent_l2_reg(z: torch.Tensor, coef: float, loss_io: torch.Tensor,
                "ldm_latent_l2_reg")
 
 
+# ---------------------------------------------------------------------------------------- GEMM
+_GEMM_MODES = {"store": capi.GEMM_STORE, "silu": capi.GEMM_SILU,
+               "resid_silu": capi.GEMM_RESID_SILU, "relu": capi.GEMM_RELU,
+               "accum": capi.GEMM_ACCUM, "dgrad_silu": capi.GEMM_DGRAD_SILU,
+               "loss": capi.GEMM_LOSS, "add_r": capi.GEMM_ADD_R}
+
+
+def _rowmajor(t: Optional[torch.Tensor], what: str, dtype=None) -> int:
+    """Row stride of a 2-D view whose rows are contiguous (0 for None)."""
+    if t is None:
+        return 0
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise capi.LdmError(f"gemm: {what} must be a 2-D view with contiguous rows")
+    if dtype is not None and t.dtype != dtype:
+        raise capi.LdmError(f"gemm: {what} must be {dtype}, got {t.dtype}")
+    return t.stride(0)
+
+
+def gemm_problem(segs, M: int, N: int, *, mode: str = "store", M_valid: Optional[int] = None,
+                 bias=None, R=None, P_in=None, C=None, P=None, Cb=None, CbT=None, colsum=None,
+                 loss_part=None, scale: float = 1.0) -> capi.GemmProb:
+    """One problem of ``ldm_gemm_bf16`` (include/ldm_sdf.h): ``segs`` = [(A [M,K] bf16,
+    B [N,K] bf16), ...] as row-contiguous views; outputs / operands as documented there."""
+    pr = capi.GemmProb()
+    pr.M, pr.N = int(M), int(N)
+    pr.M_valid = int(M if M_valid is None else M_valid)
+    if not 1 <= len(segs) <= capi.GEMM_MAX_SEGS:
+        raise capi.LdmError(f"gemm: 1..{capi.GEMM_MAX_SEGS} segments")
+    pr.n_seg = len(segs)
+    for i, (A, B) in enumerate(segs):
+        la = _rowmajor(A, "A", torch.bfloat16)
+        lb = _rowmajor(B, "B", torch.bfloat16)
+        if A.shape[0] < M or B.shape[0] < N or A.shape[1] != B.shape[1]:
+            raise capi.LdmError(f"gemm seg {i}: A{tuple(A.shape)} B{tuple(B.shape)} vs M={M} N={N}")
+        g = pr.seg[i]
+        g.A, g.B, g.lda, g.ldb, g.K = A.data_ptr(), B.data_ptr(), la, lb, A.shape[1]
+    pr.mode = _GEMM_MODES[mode]
+    pr.scale = float(scale)
+    for name, t, dt in (("R", R, torch.float32), ("P_in", P_in, torch.float32),
+                        ("C", C, torch.float32), ("P", P, torch.float32),
+                        ("Cb", Cb, torch.bfloat16), ("CbT", CbT, torch.bfloat16)):
+        ld = _rowmajor(t, name, dt)
+        setattr(pr, name, capi.ptr(t))
+        if t is not None:
+            setattr(pr, {"R": "ldr", "P_in": "ldp_in", "C": "ldc", "P": "ldp", "Cb": "ldcb",
+                         "CbT": "ldct"}[name], ld)
+    for name, t in (("bias", bias), ("colsum", colsum), ("loss_part", loss_part)):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise capi.LdmError(f"gemm: {name} must be contiguous fp32")
+        setattr(pr, name, capi.ptr(t))
+    return pr
+
+
+def gemm_args(problems, tile: int = 0) -> capi.GemmArgs:
+    a = capi.GemmArgs()
+    if not 1 <= len(problems) <= capi.GEMM_MAX_PROBS:
+        raise capi.LdmError("gemm: 1..4 problems per launch")
+    a.n_prob, a.tile = len(problems), int(tile)
+    for i, pr in enumerate(problems):
+        a.prob[i] = pr
+    return a
+
+
+def gemm_launch(a: capi.GemmArgs, device) -> None:
+    capi.check(capi.load().ldm_gemm_bf16(C.byref(a), capi.stream_handle(device)), "ldm_gemm_bf16")
+
+
+def gemm(problems, tile: int = 0, device=None) -> None:
+    """Launch ``ldm_gemm_bf16`` on torch's current stream (problems from ``gemm_problem``)."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    gemm_launch(gemm_args(problems, tile), device)
+
+
 # ---------------------------------------------------------------------------------------- C17
 def _r16(n: int) -> int:
     return (n + 15) // 16 * 16
@@ -480,6 +553,114 @@ def build_e_tables(model, dev: Dict[str, object], dtype: str) -> List[torch.Tens
 
 
 # ---------------------------------------------------------------------------------------- A6/A7
+# bf16 training through the C ABI (csrc/denoiser_train.hip): one call per forward / backward /
+# fused step; every product is an ldm_gemm_bf16 problem with fused epilogues.
+def grads_struct(grads: Dict[str, torch.Tensor], n_blocks: int) -> capi.DenoiserGrads:
+    """``ldm_denoiser_grads_t`` over fp32 tensors named like MLPDenoiser.params."""
+    g = capi.DenoiserGrads()
+    for fld, name in (("w_in", "Win"), ("b_in", "bin"), ("w_t1", "Wt1"), ("b_t1", "bt1"),
+                      ("w_t2", "Wt2"), ("b_t2", "bt2"), ("w_out", "Wout"), ("b_out", "bout")):
+        t = grads[name]
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise capi.LdmError(f"{name}: fp32 contiguous tensor expected")
+        setattr(g, fld, t.data_ptr())
+    for k in range(n_blocks):
+        g.w_blk[k] = grads[f"Wblk{k}"].data_ptr()
+        g.b_blk[k] = grads[f"bblk{k}"].data_ptr()
+    return g
+
+
+def train_workspace(desc: capi.Denoiser, B: int, device) -> torch.Tensor:
+    """The ``saved`` workspace of ldm_denoiser_fwd / _bwd / _train_step for batch B."""
+    n = int(capi.load().ldm_denoiser_train_ws_bytes(C.byref(desc), int(B)))
+    if n == 0:
+        raise capi.LdmError("ldm_denoiser_train_ws_bytes: unsupported denoiser shape")
+    ws = torch.empty(n + 256, device=device, dtype=torch.uint8)
+    off = (-ws.data_ptr()) % 256
+    return ws[off:off + n]
+
+
+def denoiser_train_step(desc: capi.Denoiser, sched_desc: capi.Sched, x0: torch.Tensor,
+                        eps: torch.Tensor, t: torch.Tensor, ws: torch.Tensor,
+                        gstruct: capi.DenoiserGrads, loss: torch.Tensor) -> None:
+    """q_sample -> net -> eps-MSE -> every gradient (``ldm_denoiser_train_step``)."""
+    _f32(x0, eps, loss)
+    _contig(x0, eps, t)
+    if t.dtype != torch.int32:
+        raise capi.LdmError("t must be int32")
+    capi.check(capi.load().ldm_denoiser_train_step(C.byref(desc), C.byref(sched_desc),
+                                                   x0.data_ptr(), eps.data_ptr(), t.data_ptr(),
+                                                   x0.shape[0], ws.data_ptr(), C.byref(gstruct),
+                                                   loss.data_ptr(),
+                                                   capi.stream_handle(x0.device)),
+               "ldm_denoiser_train_step")
+
+
+def denoiser_fwd(desc: capi.Denoiser, x: torch.Tensor, t: torch.Tensor, ws: torch.Tensor,
+                 eps_out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Training forward with per-sample t (``ldm_denoiser_fwd``), activations saved in ws."""
+    _f32(x, eps_out)
+    _contig(x, t, eps_out)
+    if t.dtype != torch.int32:
+        raise capi.LdmError("t must be int32")
+    capi.check(capi.load().ldm_denoiser_fwd(C.byref(desc), x.data_ptr(), t.data_ptr(),
+                                            x.shape[0], capi.ptr(eps_out), ws.data_ptr(),
+                                            capi.stream_handle(x.device)), "ldm_denoiser_fwd")
+    return eps_out
+
+
+def denoiser_bwd(desc: capi.Denoiser, ws: torch.Tensor, deps: torch.Tensor,
+                 gstruct: capi.DenoiserGrads, dx: Optional[torch.Tensor] = None) -> None:
+    """Backward of the last ``denoiser_fwd`` on ws (``ldm_denoiser_bwd``)."""
+    _f32(deps, dx)
+    _contig(deps, dx)
+    capi.check(capi.load().ldm_denoiser_bwd(C.byref(desc), ws.data_ptr(), deps.data_ptr(),
+                                            deps.shape[0], C.byref(gstruct), capi.ptr(dx),
+                                            capi.stream_handle(deps.device)), "ldm_denoiser_bwd")
+
+
+def q_sample_loss(sched_desc: capi.Sched, eps: torch.Tensor, *, x0=None, t=None, xt_out=None,
+                  eps_hat=None, loss_out=None, grad_out=None) -> None:
+    """A9 head (``ldm_q_sample_loss``): x_t and/or the eps-MSE loss and its gradient."""
+    _f32(eps, x0, xt_out, eps_hat, loss_out, grad_out)
+    _contig(eps, x0, t, xt_out, eps_hat, grad_out)
+    B, D = eps.shape
+    capi.check(capi.load().ldm_q_sample_loss(C.byref(sched_desc), capi.ptr(x0), eps.data_ptr(),
+                                             capi.ptr(t), B, D, capi.ptr(xt_out),
+                                             capi.ptr(eps_hat), capi.ptr(loss_out),
+                                             capi.ptr(grad_out),
+                                             capi.stream_handle(eps.device)), "ldm_q_sample_loss")
+
+
+def adamw_table(entries) -> "C.Array":
+    """Host ``ldm_adamw_tensor_t`` array for ``adamw_multi``: entries are tuples
+    (p, g, m, v, p_bf16 or None, p_bf16_t or None) of tensors with 1-D or 2-D shapes."""
+    arr = (capi.AdamwTensor * len(entries))()
+    for i, (p, g, m, v, pb, pbt) in enumerate(entries):
+        for t in (p, g, m, v):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.shape != p.shape:
+                raise capi.LdmError("adamw_multi: p, g, m, v must be contiguous fp32 of one shape")
+        rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+        for t, shp in ((pb, (rows, cols)), (pbt, (cols, rows))):
+            if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous()
+                                  or t.numel() != rows * cols):
+                raise capi.LdmError("adamw_multi: bf16 copies must be contiguous, p's size")
+        e = arr[i]
+        e.p, e.g, e.m, e.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+        e.p_bf16, e.p_bf16_t = capi.ptr(pb), capi.ptr(pbt)
+        e.rows, e.cols = rows, cols
+    return arr
+
+
+def adamw_multi(table, *, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
+                weight_decay: float = 0.0, step: int, device=None) -> None:
+    """Every tensor of ``table`` (``adamw_table``) in one launch (``ldm_adamw_multi``)."""
+    capi.check(capi.load().ldm_adamw_multi(table, len(table), float(lr), float(betas[0]),
+                                           float(betas[1]), float(eps), float(weight_decay),
+                                           int(step), capi.stream_handle(device)),
+               "ldm_adamw_multi")
+
+
 def denoiser_forward_train(model, dev: Dict[str, object], xt: torch.Tensor,
                            t: torch.Tensor, compute: int = capi.COMPUTE_FP32
                            ) -> Tuple[torch.Tensor, dict]:

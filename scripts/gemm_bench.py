@@ -1,0 +1,57 @@
+"""Microbenchmark of the training GEMM shapes (config 2, B = 1000 padded to 1024; C19 1M rows):
+ldm_gemm_bf16 per tile shape vs the generic ldm_linear MFMA path vs torch.mm (hipBLASLt) on
+the same bf16 operands.  HIP events over REPS back-to-back launches, after a warm-up.
+Prints one JSON line per shape."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "latent-diffusion-models-for-shape-sdfs_amd")]
+import torch  # noqa: E402
+import ldm_sdf  # noqa: E402
+from ldm_sdf import ops, _capi as capi  # noqa: E402
+
+dev = torch.device("cuda", 0)
+REPS = int(os.environ.get("REPS", "50"))
+SHAPES = [(1024, 1024, 2048), (1024, 2048, 1024), (1024, 1024, 1024), (1024, 256, 1024),
+          (256, 1024, 1024), (1024, 1024, 128), (1024, 1024, 4096)]
+if os.environ.get("BIG"):
+    SHAPES += [(1 << 20, 512, 512), (512, 512, 1 << 20)]
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(REPS):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / REPS * 1e3   # us
+
+
+g = torch.Generator(device=dev).manual_seed(0)
+for (M, N, K) in SHAPES:
+    A = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    B = torch.randn(N, K, device=dev, generator=g).bfloat16()
+    C = torch.empty(M, N, device=dev)
+    fl = 2.0 * M * N * K
+    res = {"M": M, "N": N, "K": K}
+    reps = REPS if M * N * K < 1 << 34 else 5
+    for tile in (1, 2, 3, 4):
+        args = ops.gemm_args([ops.gemm_problem([(A, B)], M, N, C=C)], tile)
+        us = timed(lambda: ops.gemm_launch(args, dev))
+        res[f"gemm_t{tile}_us"] = round(us, 2)
+        res[f"gemm_t{tile}_tflops"] = round(fl / us / 1e6, 1)
+    ref = A.float() @ B.float().T
+    ops.gemm([ops.gemm_problem([(A, B)], M, N, C=C)])
+    res["max_err"] = float((C - ref).abs().max())
+    us = timed(lambda: torch.mm(A, B.T))
+    res["torch_mm_us"], res["torch_mm_tflops"] = round(us, 2), round(fl / us / 1e6, 1)
+    if M * N * K < 1 << 34:
+        Af = A.float()
+        us = timed(lambda: ops.linear(Af, B, C, compute=capi.COMPUTE_BF16))
+        res["ldm_linear_us"], res["ldm_linear_tflops"] = round(us, 2), round(fl / us / 1e6, 1)
+    print(json.dumps(res), flush=True)

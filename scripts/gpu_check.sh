@@ -18,12 +18,12 @@ run() {  # name timeout cmd...
 STAGES="${STAGES:-pytest smoke bench prof}"
 for s in $STAGES; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 900 python bench.py ${BENCH_ARGS:-} ;;
     prof)   cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
             run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-                --output-format csv -- python bench.py ${PROF_ARGS:---batch 8 --steps 2 --no-cpu} ;;
+                --output-format csv -- python3 bench.py ${PROF_ARGS:-} ;;
   esac
 done
 exit 0

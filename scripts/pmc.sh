@@ -4,7 +4,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
+WORKLOAD=${WORKLOAD:-scripts/decode_once.py}
 mkdir -p $OUT
 declare -A P
 P[cycles]="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_WAVES"
@@ -17,7 +18,7 @@ P[l2]="TCC_HIT_sum TCC_MISS_sum"
 for name in ${PASSES:-cycles insts lds fetch write ea l2}; do
   echo "== pass $name: ${P[$name]}"
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${P[$name]} -d $OUT/$name -o run \
-      --output-format csv -- python3 scripts/decode_once.py > $OUT/$name.log 2>&1
+      --output-format csv -- python3 $WORKLOAD > $OUT/$name.log 2>&1
   rc=$?
   echo "   rc=$rc"
   case $rc in 0) ;; *) tail -5 $OUT/$name.log; exit $rc;; esac

@@ -1,0 +1,57 @@
+"""rocprofv3 --pmc passes (one directory per pass, each with run_counter_collection.csv) ->
+per (kernel, grid) average counters per dispatch + derived ratios (MI355X guide units:
+SQ_*_CYCLES in quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES; FETCH_SIZE x2 on gfx950).
+Usage: python scripts/pmc_by_kernel.py <pmc_root> [name-substring] [min-dispatches]"""
+import csv
+import glob
+import os
+import re
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+pat = sys.argv[2] if len(sys.argv) > 2 else ""
+vals = defaultdict(lambda: defaultdict(list))
+dur = defaultdict(list)
+for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
+    per = defaultdict(float)
+    meta = {}
+    for r in csv.DictReader(open(f)):
+        if pat not in r["Kernel_Name"]:
+            continue
+        short = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+        short = re.sub(r"\(.*", "", short)[:64]
+        grid = int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"]))
+        key = (short, grid)
+        per[(r["Dispatch_Id"], key, r["Counter_Name"])] += float(r["Counter_Value"])
+        meta[(r["Dispatch_Id"], key)] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    for (d, key, c), v in per.items():
+        vals[key][c].append(v)
+    for (d, key), t in meta.items():
+        dur[key].append(t)
+for key in sorted(vals, key=lambda k: -sum(dur[k])):
+    a = {c: sum(v) / len(v) for c, v in vals[key].items()}
+    us = sum(dur[key]) / len(dur[key])
+    out = [f"{key[0]} grid={key[1]} dispatches~{len(dur[key])} avg {us:.2f} us"]
+    if "SQ_WAVE_CYCLES" in a:
+        wc = a["SQ_WAVE_CYCLES"]
+        out.append("  wait_any %.2f  wait_inst %.2f  active %.2f (of wave cycles)" % (
+            a.get("SQ_WAIT_ANY", 0) / wc, a.get("SQ_WAIT_INST_ANY", 0) / wc,
+            a.get("SQ_ACTIVE_INST_ANY", 0) / wc))
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in a and "GRBM_GUI_ACTIVE" in a:
+        out.append("  mfma_busy %.3f of SIMD-cycles; clock %.2f GHz" % (
+            a["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * a["GRBM_GUI_ACTIVE"] / 8),
+            a["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)))
+    if "SQ_INSTS_MFMA" in a:
+        out.append("  insts: mfma %.3g valu %.3g lds %.3g salu %.3g" % (
+            a["SQ_INSTS_MFMA"], a.get("SQ_INSTS_VALU", 0), a.get("SQ_INSTS_LDS", 0),
+            a.get("SQ_INSTS_SALU", 0)))
+    if "SQ_LDS_BANK_CONFLICT" in a:
+        out.append("  lds: bank_conflict/idx_active %.3f  wait_inst_lds/wave %.3g" % (
+            a["SQ_LDS_BANK_CONFLICT"] / max(1.0, a.get("SQ_LDS_IDX_ACTIVE", 1.0)),
+            a.get("SQ_WAIT_INST_LDS", 0)))
+    if "FETCH_SIZE" in a:
+        out.append("  hbm read %.3f MB (FETCH_SIZE x2)" % (a["FETCH_SIZE"] * 1024 * 2 / 1e6))
+    if "WRITE_SIZE" in a:
+        out.append("  hbm write %.3f MB" % (a["WRITE_SIZE"] * 1024 / 1e6))
+    print("\n".join(out))

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_error_path_without_gpu():
     from ldm_sdf import _capi as capi
     lib = capi.load()
-    assert lib.ldm_abi_version() == 1
+    assert lib.ldm_abi_version() == 2
     # argument validation runs before any device work
     assert lib.ldm_grid_coords(0, 0, 0, 0.0, 0.0, None, None) == -22
     assert b"bad grid slab" in lib.ldm_last_error()
@@ -53,6 +53,11 @@ def test_struct_layouts_match_c():
              offsetof(ldm_denoiser_t, e_tab), offsetof(ldm_linear_args_t, A_out));
       printf("%zu %zu %zu %zu\n", sizeof(ldm_conv1d_seg_t), sizeof(ldm_conv1d_args_t),
              offsetof(ldm_conv1d_args_t, bias), offsetof(ldm_conv1d_args_t, t));
+      printf("%zu %zu %zu %zu\n", sizeof(ldm_denoiser_grads_t), sizeof(ldm_adamw_tensor_t),
+             offsetof(ldm_denoiser_t, wt_blk), offsetof(ldm_denoiser_grads_t, b_out));
+      printf("%zu %zu %zu %zu %zu\n", sizeof(ldm_gemm_seg_t), sizeof(ldm_gemm_prob_t),
+             sizeof(ldm_gemm_args_t), offsetof(ldm_gemm_prob_t, bias),
+             offsetof(ldm_gemm_prob_t, loss_part));
       return 0; }
     '''
     tmp = "/tmp/ldm_layout_check"
@@ -68,5 +73,11 @@ def test_struct_layouts_match_c():
                          ctypes.sizeof(capi.Denoiser), ctypes.sizeof(capi.LinearArgs)]
     assert sizes[4:8] == [capi.Decoder.weights.offset, capi.Decoder.b_last.offset,
                           capi.Denoiser.e_tab.offset, capi.LinearArgs.A_out.offset]
-    assert sizes[8:] == [ctypes.sizeof(capi.ConvSeg), ctypes.sizeof(capi.ConvArgs),
-                         capi.ConvArgs.bias.offset, capi.ConvArgs.t.offset]
+    assert sizes[8:12] == [ctypes.sizeof(capi.ConvSeg), ctypes.sizeof(capi.ConvArgs),
+                           capi.ConvArgs.bias.offset, capi.ConvArgs.t.offset]
+    assert sizes[12:16] == [ctypes.sizeof(capi.DenoiserGrads), ctypes.sizeof(capi.AdamwTensor),
+                            capi.Denoiser.wt_blk.offset, capi.DenoiserGrads.b_out.offset]
+    sizes = sizes[4:]
+    assert sizes[12:17] == [ctypes.sizeof(capi.GemmSeg), ctypes.sizeof(capi.GemmProb),
+                            ctypes.sizeof(capi.GemmArgs), capi.GemmProb.bias.offset,
+                            capi.GemmProb.loss_part.offset]

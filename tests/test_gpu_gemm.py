@@ -1,0 +1,176 @@
+"""ldm_gemm_bf16 (csrc/gemm_bf16.hip) on the MI355X against fp64 torch on the same bf16
+operands: every epilogue mode, K segments, several problems per launch, ragged M / N, the
+M_valid row mask, bf16 / transposed outputs, column-sum and loss partials, every tile shape.
+
+Tolerances: the fp64 product of the bf16 operands is the reference; fp32 accumulation of K
+products of O(1) values errs by ~1e-7 * sqrt(K) * |terms|, so 2e-6 * sqrt(K) * 4 absolute on
+fp32 outputs; bf16 outputs are compared after rounding the reference the same way (RNE), with
+one bf16 ulp of slack for values that sit on a rounding boundary."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ldm_sdf
+    ldm_sdf.load_library()
+    return torch.device("cuda", 0)
+
+
+def _rand(shape, g, dev, scale=1.0):
+    return (torch.randn(shape, generator=g) * scale).to(dev)
+
+
+def _ref(segs):
+    return sum(A.double() @ B.double().T for A, B in segs)
+
+
+def _bf_close(got, want, tol):
+    """bf16 output vs an fp64 reference: within the fp32-accumulation tolerance plus one bf16
+    rounding step of the value."""
+    w = want.double()
+    return bool(((got.double() - w).abs() <= tol + w.abs() * 2 ** -8).all())
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,Ks", [(1000, 1024, (2048,)), (64, 64, (64,)), (130, 70, (128, 64)),
+                                    (1024, 256, (1024,)), (96, 2048, (256, 128, 64, 512))])
+def test_gemm_store_segments_tiles(dev, tile, M, N, Ks):
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(M * 7 + N + len(Ks) * 13 + tile)
+    segs = [(_rand((M, K), g, dev).bfloat16(), _rand((N, K), g, dev).bfloat16()) for K in Ks]
+    bias = _rand((N,), g, dev)
+    Mp = (M + 3) // 4 * 4
+    C = torch.full((M, N), 7.0, device=dev)
+    Cb = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+    CbT = torch.zeros(N, Mp, device=dev, dtype=torch.bfloat16)
+    Aseg = [(torch.cat([A, torch.zeros(Mp - M, A.shape[1], device=dev, dtype=A.dtype)]), B)
+            for A, B in segs]
+    cs = torch.zeros((Mp + 31) // 32, N, device=dev)
+    ops.gemm([ops.gemm_problem(Aseg, Mp, N, M_valid=M, bias=bias, C=torch.cat(
+        [C, torch.zeros(Mp - M, N, device=dev)]) if Mp != M else C, Cb=None, CbT=CbT,
+        colsum=cs)], tile=tile)
+    # run again with exactly M rows for the row-major outputs
+    ops.gemm([ops.gemm_problem(segs, M, N, bias=bias, C=C, Cb=Cb)], tile=tile)
+    torch.cuda.synchronize()
+    want = _ref(segs) + bias.double()
+    tol = 2e-6 * math.sqrt(sum(Ks)) * 4
+    assert (C.double() - want).abs().max() < tol
+    assert _bf_close(Cb, want, tol)
+    assert _bf_close(CbT[:, :M].T, want, tol)
+    assert bool((CbT[:, M:] == 0).all())
+    csw = torch.zeros_like(cs, dtype=torch.float64)
+    for r in range(cs.shape[0]):
+        csw[r] = want[r * 32:(r + 1) * 32].sum(0)
+    assert (cs.double() - csw).abs().max() < tol * 32
+
+
+@pytest.mark.parametrize("mode", ["silu", "resid_silu", "relu", "accum", "add_r", "dgrad_silu",
+                                  "loss"])
+def test_gemm_epilogues(dev, mode):
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(hash(mode) % 1000)
+    M, N, K = 200, 192, 320
+    Mv = 190
+    A = _rand((M, K), g, dev).bfloat16()
+    B = _rand((N, K), g, dev, 0.1).bfloat16()
+    bias = _rand((N,), g, dev)
+    R = _rand((M, N), g, dev)
+    Pin = _rand((M, N), g, dev)
+    C0 = _rand((M, N), g, dev)
+    C = C0.clone()
+    P = torch.zeros(M, N, device=dev)
+    Cb = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+    CbT = torch.zeros(N, M, device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros((M + 31) // 32, N, device=dev)
+    lp = torch.zeros((M + 31) // 32, (N + 31) // 32, device=dev)
+    kw = dict(bias=bias, C=C, Cb=Cb, CbT=CbT, colsum=cs, M_valid=Mv)
+    if mode in ("silu", "resid_silu"):
+        kw["P"] = P
+    if mode in ("resid_silu", "add_r", "dgrad_silu"):
+        kw["R"] = R
+    if mode in ("dgrad_silu", "loss"):
+        kw["P_in"] = Pin
+    if mode == "loss":
+        kw["loss_part"] = lp
+        kw["scale"] = 0.37
+    ops.gemm([ops.gemm_problem([(A, B)], M, N, mode=mode, **kw)])
+    torch.cuda.synchronize()
+    pre = A.double() @ B.double().T + bias.double()
+    sig = torch.sigmoid
+    Rd, Pd, C0d = R.double(), Pin.double(), C0.double()
+    dh = None
+    if mode == "silu":
+        out = pre * sig(pre)
+    elif mode == "resid_silu":
+        out = Rd + pre * sig(pre)
+    elif mode == "relu":
+        out = pre.clamp_min(0)
+    elif mode == "accum":
+        out = C0d + pre
+    elif mode == "add_r":
+        out = Rd + pre
+    elif mode == "dgrad_silu":
+        dh = Rd + pre
+        s = sig(Pd)
+        out = dh * s * (1 + Pd * (1 - s))
+    else:
+        d = pre - Pd
+        out = 0.37 * d
+    live = torch.arange(M, device=dev)[:, None] < Mv
+    out = torch.where(live, out, torch.zeros_like(out))
+    tol = 2e-6 * math.sqrt(K) * 4 * 4
+    # fp32 outputs: live rows computed, padding rows (>= M_valid) left as they were
+    Cw = dh if mode == "dgrad_silu" else out
+    assert (C[:Mv].double() - Cw[:Mv]).abs().max() < tol, mode
+    assert torch.equal(C[Mv:], C0[Mv:])
+    assert _bf_close(Cb, out, tol)
+    assert _bf_close(CbT.T, out, tol)
+    assert bool((Cb[Mv:] == 0).all()) and bool((CbT[:, Mv:] == 0).all())
+    if mode in ("silu", "resid_silu"):
+        assert (P[:Mv].double() - pre[:Mv]).abs().max() < tol
+        assert bool((P[Mv:] == 0).all())
+    csw = torch.stack([out[r * 32:(r + 1) * 32].sum(0) for r in range(cs.shape[0])])
+    assert (cs.double() - csw).abs().max() < tol * 32
+    if mode == "loss":
+        d2 = torch.where(live, (pre - Pd) ** 2, torch.zeros_like(pre))
+        lw = torch.stack([torch.stack([d2[r * 32:(r + 1) * 32, c * 32:(c + 1) * 32].sum()
+                                       for c in range(lp.shape[1])]) for r in range(lp.shape[0])])
+        assert (lp.double() - lw).abs().max() < 1e-4 * lw.abs().max()
+
+
+def test_gemm_grouped_problems(dev):
+    """Four problems of different shapes and modes in one launch == four launches."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(77)
+    shapes = [(1024, 1024, 1024), (256, 1024, 1024), (1024, 128, 1024), (64, 2048, 192)]
+    probs, outs, refs = [], [], []
+    for (M, N, K) in shapes:
+        A = _rand((M, K), g, dev).bfloat16()
+        B = _rand((N, K), g, dev).bfloat16()
+        C = torch.zeros(M, N, device=dev)
+        probs.append(ops.gemm_problem([(A, B)], M, N, C=C))
+        outs.append(C)
+        refs.append(A.double() @ B.double().T)
+    ops.gemm(probs)
+    torch.cuda.synchronize()
+    for (M, N, K), C, w in zip(shapes, outs, refs):
+        assert (C.double() - w).abs().max() < 2e-6 * math.sqrt(K) * 4, (M, N, K)
+
+
+def test_gemm_rejects_bad_args(dev):
+    from ldm_sdf import ops, LdmError
+    A = torch.zeros(64, 100, device=dev, dtype=torch.bfloat16)
+    B = torch.zeros(64, 100, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(LdmError):                     # K not a multiple of 64
+        ops.gemm([ops.gemm_problem([(A, B)], 64, 64, C=torch.zeros(64, 64, device=dev))])
+    A = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(LdmError):                     # resid_silu without R
+        ops.gemm([ops.gemm_problem([(A, A)], 64, 64, mode="resid_silu",
+                                   C=torch.zeros(64, 64, device=dev))])

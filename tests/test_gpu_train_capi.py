@@ -1,0 +1,250 @@
+"""The bf16 training path through the C ABI on the MI355X (csrc/denoiser_train.hip):
+ldm_denoiser_fwd (per-sample t) / ldm_denoiser_bwd / ldm_denoiser_train_step /
+ldm_q_sample_loss / ldm_adamw_multi, called through ctypes.
+
+References:
+  * a bf16-operand emulation of the oracle (oracle/ref_cpu.py's network with every GEMM operand
+    rounded to bf16 as the kernels round it, fp64 arithmetic otherwise): the forward output
+    agrees to <= 2e-3 relative to its scale (rounding-boundary flips of single operands and
+    fp32 accumulation order are all that differ);
+  * the fp64 oracle itself (unrounded weights): loss within 1e-3 relative, every gradient at
+    cosine >= 0.999 and norm within 2 % (bf16 operand rounding), as the ldm_linear bf16 path;
+  * the modular fwd -> q_sample_loss -> bwd sequence against the fused step on the same
+    inputs (same activations; the loss gradient enters through fp32 deps instead of the
+    epilogue: <= 1e-3 relative);
+  * ldm_adamw_multi against ldm_adamw_step bit for bit, and its bf16 copies (both layouts)
+    against the RNE-rounded master.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ldm_sdf
+    ldm_sdf.load_library()
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def net():
+    from ldm_sdf import MLPDenoiser
+    from oracle import ref_cpu as R
+    p = R.make_denoiser_params(seed=4321)
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"], params[f"bblk{k}"] = p.Wblk[k], p.bblk[k]
+    return MLPDenoiser(params=params), p
+
+
+def _bf(x):
+    return x.float().bfloat16().double()
+
+
+def _emulated_forward(p, x, t, emb):
+    """oracle network with GEMM operands rounded to bf16 (weights and activations), fp64
+    otherwise; the residual stream stays unrounded as on the device."""
+    e = emb[t.long()]
+    a_t = _bf(e) @ _bf(p.Wt1).T + p.bt1.float().double()
+    u = a_t * torch.sigmoid(a_t)
+    temb = _bf(u) @ _bf(p.Wt2).T + p.bt2.float().double()
+    h = _bf(x) @ _bf(p.Win).T + p.bin.float().double()
+    for k in range(p.n_blocks):
+        W = _bf(p.Wblk[k])
+        a = _bf(h) @ W[:, :p.H].T + _bf(temb) @ W[:, p.H:].T + p.bblk[k].float().double()
+        h = h + a * torch.sigmoid(a)
+    return _bf(h) @ _bf(p.Wout).T + p.bout.float().double()
+
+
+def _inputs(B, seed):
+    g = torch.Generator().manual_seed(seed)
+    x0 = torch.randn(B, 256, generator=g) * 0.5
+    t = torch.randint(0, 1000, (B,), generator=g, dtype=torch.int32)
+    eps = torch.randn(B, 256, generator=g)
+    return x0, t, eps
+
+
+@pytest.mark.parametrize("B", [1, 37, 64, 200])
+def test_denoiser_fwd_per_sample_t(dev, net, B):
+    """ldm_denoiser_fwd with per-sample t vs the bf16-emulated oracle (ragged B: padding rows)."""
+    from ldm_sdf import ops
+    from oracle import ref_cpu as R
+    model, p = net
+    model.to_device(dev)
+    desc = model.device_pack("bf16", dev, with_tables=False)["desc"]
+    x0, t, eps = _inputs(B, B)
+    ws = ops.train_workspace(desc, B, dev)
+    out = torch.empty(B, 256, device=dev)
+    ops.denoiser_fwd(desc, x0.to(dev), t.to(dev), ws, out)
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    want = _emulated_forward(p, x0.double(), t, emb)
+    scale = float(want.abs().max())
+    err = float((out.cpu().double() - want).abs().max()) / scale
+    print(f"B={B}: fwd rel err vs bf16-emulated oracle {err:.2e}")
+    assert err <= 2e-3, err
+    # and vs the exact oracle, loosely (bf16 operands)
+    exact = R.denoiser_forward(p, x0.double(), t.long(), emb)
+    cos = float((out.cpu().double().flatten() @ exact.flatten())
+                / (out.cpu().double().norm() * exact.norm()))
+    assert cos >= 0.9995, cos
+
+
+@pytest.mark.parametrize("B", [64, 1000])
+def test_train_step_fused_vs_oracle(dev, net, B):
+    """ldm_denoiser_train_step (the config-2 step at B = 1000) vs the fp64 oracle's autograd."""
+    from ldm_sdf import ops
+    from oracle import ref_cpu as R
+    import ldm_sdf
+    model, p = net
+    model.to_device(dev)
+    desc = model.device_pack("bf16", dev, with_tables=False)["desc"]
+    sd = ldm_sdf.DDPMSchedule().device(dev)
+    x0, t, eps = _inputs(B, 100 + B)
+    grads = {n: torch.full_like(model.params[n], float("nan")) for n in model.names()}
+    loss = torch.empty(1, device=dev)
+    ws = ops.train_workspace(desc, B, dev)
+    ops.denoiser_train_step(desc, sd["desc"], x0.to(dev), eps.to(dev), t.to(dev), ws,
+                            model.grads_struct(grads), loss)
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    wl, wg = R.train_step_grads(p, R.ddpm_tables(), emb, x0.double(), eps.double(), t.long())
+    assert abs(float(loss) - float(wl)) / float(wl) < 1e-3, (float(loss), float(wl))
+    for k, v in grads.items():
+        got = v.cpu().double().flatten()
+        w = wg[k].flatten()
+        assert bool(torch.isfinite(got).all()), k
+        cos = float(got @ w / (got.norm() * w.norm() + 1e-30))
+        rel = abs(float(got.norm()) - float(w.norm())) / float(w.norm())
+        print(f"B={B} {k}: cos {cos:.6f} norm rel {rel:.2e}")
+        assert cos >= 0.999 and rel <= 2e-2, (k, cos, rel)
+
+
+def test_modular_fwd_bwd_matches_fused(dev, net):
+    """fwd -> q_sample_loss -> bwd (the three SURVEY §8(b) entry points) == the fused step."""
+    from ldm_sdf import ops
+    import ldm_sdf
+    model, _ = net
+    model.to_device(dev)
+    desc = model.device_pack("bf16", dev, with_tables=False)["desc"]
+    sd = ldm_sdf.DDPMSchedule().device(dev)
+    B = 300
+    x0, t, eps = (v.to(dev) for v in _inputs(B, 7))
+    gf = {n: torch.empty_like(model.params[n]) for n in model.names()}
+    gm = {n: torch.empty_like(model.params[n]) for n in model.names()}
+    loss_f = torch.empty(1, device=dev)
+    ws = ops.train_workspace(desc, B, dev)
+    ops.denoiser_train_step(desc, sd["desc"], x0, eps, t, ws, model.grads_struct(gf), loss_f)
+    xt = torch.empty(B, 256, device=dev)
+    ops.q_sample_loss(sd["desc"], eps, x0=x0, t=t, xt_out=xt)
+    want_xt = ops.q_sample(sd["desc"], x0, eps, t)
+    assert torch.equal(xt, want_xt)                       # the A9 head is bit-exact
+    eps_hat = torch.empty(B, 256, device=dev)
+    ops.denoiser_fwd(desc, xt, t, ws, eps_hat)
+    loss_m, deps = torch.empty(1, device=dev), torch.empty(B, 256, device=dev)
+    ops.q_sample_loss(sd["desc"], eps, eps_hat=eps_hat, loss_out=loss_m, grad_out=deps)
+    dx = torch.empty(B, 256, device=dev)
+    ops.denoiser_bwd(desc, ws, deps, model.grads_struct(gm), dx)
+    assert abs(float(loss_m) - float(loss_f)) <= 1e-5 * float(loss_f)
+    for n in gf:
+        a, b = gf[n].double(), gm[n].double()
+        assert float((a - b).norm() / b.norm()) <= 1e-3, n
+    # dx = dL/dx_t against autograd of the bf16-emulated network's first layer chain is covered
+    # by the fp64 check below: finite and the right scale
+    assert bool(torch.isfinite(dx).all()) and float(dx.abs().max()) > 0
+
+
+def test_dx_vs_oracle(dev, net):
+    """dL/dx_t from ldm_denoiser_bwd vs fp64 autograd of the oracle network."""
+    from ldm_sdf import ops
+    from oracle import ref_cpu as R
+    model, p = net
+    model.to_device(dev)
+    desc = model.device_pack("bf16", dev, with_tables=False)["desc"]
+    B = 128
+    x, t, eps = _inputs(B, 11)
+    ws = ops.train_workspace(desc, B, dev)
+    eps_hat = torch.empty(B, 256, device=dev)
+    ops.denoiser_fwd(desc, x.to(dev), t.to(dev), ws, eps_hat)
+    deps = (2.0 * (eps_hat.cpu() - eps) / (B * 256)).float()
+    grads = {n: torch.empty_like(model.params[n]) for n in model.names()}
+    dx = torch.empty(B, 256, device=dev)
+    ops.denoiser_bwd(desc, ws, deps.to(dev), model.grads_struct(grads), dx)
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128)).double()
+    xd = x.double().requires_grad_(True)
+    with torch.enable_grad():
+        out = R.denoiser_forward(p, xd, t.long(), emb)
+        ((out - eps.double()) ** 2).mean().backward()
+    w = xd.grad.flatten()
+    got = dx.cpu().double().flatten()
+    cos = float(got @ w / (got.norm() * w.norm()))
+    assert cos >= 0.999, cos
+
+
+def test_adamw_multi_matches_single(dev):
+    """One launch over mixed shapes == ldm_adamw_step per tensor, bitwise; bf16 copies RNE."""
+    from ldm_sdf import ops
+    g = torch.Generator(device=dev).manual_seed(9)
+    shapes = [(1024, 2048), (256, 1024), (1000,), (1024, 128), (77, 130), (5,)]
+    ps = [torch.randn(s, device=dev, generator=g) for s in shapes]
+    ref = [p.clone() for p in ps]
+    ms = [torch.zeros_like(p) for p in ps]
+    vs = [torch.zeros_like(p) for p in ps]
+    mr = [torch.zeros_like(p) for p in ps]
+    vr = [torch.zeros_like(p) for p in ps]
+    lows = [torch.empty_like(p, dtype=torch.bfloat16) if p.dim() == 2 else None for p in ps]
+    lowt = [torch.empty(p.shape[1], p.shape[0], device=dev, dtype=torch.bfloat16)
+            if p.dim() == 2 else None for p in ps]
+    grads = [torch.empty_like(p) for p in ps]
+    table = ops.adamw_table(list(zip(ps, grads, ms, vs, lows, lowt)))
+    for step in range(1, 4):
+        for gr in grads:
+            gr.copy_(torch.randn(gr.shape, device=dev, generator=g))
+        ops.adamw_multi(table, lr=3e-3, weight_decay=0.01, step=step, device=dev)
+        for i in range(len(ps)):
+            ops.adamw_step(ref[i], grads[i], mr[i], vr[i], None, lr=3e-3, weight_decay=0.01,
+                           step=step)
+    torch.cuda.synchronize()
+    for i, p in enumerate(ps):
+        assert torch.equal(p, ref[i]) and torch.equal(ms[i], mr[i]) and torch.equal(vs[i], vr[i])
+        if lows[i] is not None:
+            assert torch.equal(lows[i], p.to(torch.bfloat16))
+            assert torch.equal(lowt[i], p.t().contiguous().to(torch.bfloat16))
+
+
+def test_train_bf16_loop_learns_and_matches_torch_adamw(dev, net):
+    """train(dtype='bf16') (fused step + ldm_adamw_multi) tracks the same run driven by
+    torch.optim.AdamW over the same fused gradients, and lowers the loss."""
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser
+    _, p = net
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"], params[f"bblk{k}"] = p.Wblk[k], p.bblk[k]
+    lat = torch.randn(512, 256, generator=torch.Generator().manual_seed(2)).to(dev) * 0.5
+    sch = ldm_sdf.DDPMSchedule()
+    runs = []
+    for use_torch in (False, True):
+        model = MLPDenoiser(params={k: v.clone() for k, v in params.items()})
+        model.to_device(dev)
+        st = None
+        if use_torch:
+            st = ldm_sdf.api.TrainState()
+            st.masters = {n: model.params[n] for n in model.names()}
+            st.optimizer = torch.optim.AdamW(list(st.masters.values()), lr=3e-4, weight_decay=0.0)
+        st = ldm_sdf.train(model, sch, lat, steps=30, batch=512, lr=3e-4, dtype="bf16", state=st,
+                           generator=torch.Generator(device=dev).manual_seed(8))
+        runs.append((st.losses, {n: t.clone() for n, t in model.params.items()}))
+    (la, pa), (lb, pb) = runs
+    assert np.mean(la[-5:]) < np.mean(la[:5])
+    # same gradients, same update rule: identical up to the bf16 working copies' rounding of
+    # the torch path (torch updates fp32 masters and re-packs; ours rounds in the same pass)
+    assert max(abs(a - b) for a, b in zip(la, lb)) <= 1e-3 * max(lb)
+    for n in pa:
+        assert (pa[n] - pb[n]).abs().max() <= 1e-3 * pb[n].abs().max() + 1e-6, n
