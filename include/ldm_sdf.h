@@ -332,7 +332,8 @@ int ldm_latent_l2_reg(const float* z, int S, int L, float coef, float* loss_io, 
  * [ceil(M/32)][N]: per 32-row block column sums of out (bias gradients, summed in fixed order
  * by the caller), loss_part fp32 [ceil(M/32)][ceil(N/32)]: sums of d^2 (LOSS).
  * Up to LDM_GEMM_MAX_PROBS independent problems share one launch.  tile: 0 = auto, 1 = 64x64,
- * 2 = 128x64, 3 = 128x128, 4 = 64x64 with a 3-deep ring. */
+ * 2 = 128x64, 3 = 128x128, 4 = 64x64 with a 3-deep ring; 5 / 6 / 7 = 64x64 / 128x128 / 128x64
+ * with 8 waves in two k-groups (csrc/gemm_bf16.hip). */
 #define LDM_GEMM_MAX_SEGS 8
 #define LDM_GEMM_MAX_PROBS 4
 #define LDM_GEMM_STORE 0

@@ -760,11 +760,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float eps, float step_size, float bc2_sqrt) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float gi = g[i];
-    const float mi = m[i] + omb1 * (gi - m[i]);
-    const float vi = v[i] * b2 + omb2 * gi * gi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pi = p[i] * decay - step_size * (mi / denom);
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_update(pi, g[i], mi, vi, decay, omb1, b2, omb2, eps, step_size, bc2_sqrt);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;

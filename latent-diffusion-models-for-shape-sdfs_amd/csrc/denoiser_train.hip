@@ -152,8 +152,19 @@ __global__ __launch_bounds__(256) void colsum_jobs_kernel(SumJobs jobs) {
     const __attribute__((address_space(4))) SumJob& J = kj->j[jb];
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= J.len) return;
+    // 8 loads in flight per round, summed in row order (deterministic)
+    const float* src = J.src + c;
+    const int64_t ld = J.ld;
     float s = 0.f;
-    for (int r = 0; r < J.rows; ++r) s += J.src[(int64_t)r * J.ld + c];
+    int r = 0;
+    for (; r + 8 <= J.rows; r += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(r + u) * ld];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < J.rows; ++r) s += src[(int64_t)r * ld];
     J.dst[c] = J.scale * s;
 }
 
@@ -478,33 +489,65 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(AdamJobs jobs) {
     const int cq = (tid & 15) * 4;
     const float decay = kj->decay, omb1 = kj->omb1, b2 = kj->b2, omb2 = kj->omb2;
     const float eps = kj->eps, step_size = kj->step_size, bc2_sqrt = kj->bc2_sqrt;
+    float* __restrict__ P = T.p;
+    const float* __restrict__ Gp = T.g;
+    float* __restrict__ M = T.m;
+    float* __restrict__ V = T.v;
+    // every load of the thread's 4 rows x 4 columns first (16-byte vectors when the row is
+    // aligned and whole), then the updates, then the stores: one memory round trip
+    const bool vec = (cols & 3) == 0 && c0 + cq + 4 <= cols;
+    f32x4 p4[4], g4[4], m4[4], v4[4];
+    int64_t off[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = min(r0 + (tid >> 4) + 16 * i, rows - 1);
+        off[i] = (int64_t)r * cols + c0 + cq;
+        if (vec) {
+            p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
+            g4[i] = *reinterpret_cast<const f32x4*>(Gp + off[i]);
+            m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
+            v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t x = c0 + cq + e < cols ? off[i] + e : off[i];
+                p4[i][e] = P[x]; g4[i][e] = Gp[x]; m4[i][e] = M[x]; v4[i][e] = V[x];
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int rl = (tid >> 4) + 16 * i;
-        const int r = r0 + rl;
-        unsigned short q[4] = {0, 0, 0, 0};
-        if (r < rows) {
+        const bool rin = r0 + rl < rows;
+        unsigned short q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float pi = p4[i][e], mi = m4[i][e], vi = v4[i][e];
+            adamw_update(pi, g4[i][e], mi, vi, decay, omb1, b2, omb2, eps, step_size, bc2_sqrt);
+            p4[i][e] = pi; m4[i][e] = mi; v4[i][e] = vi;
+            const unsigned u = __builtin_bit_cast(unsigned, pi);
+            q[e] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+            sT[cq + e][rl] = rin ? q[e] : (unsigned short)0;
+        }
+        if (!rin) continue;
+        if (vec) {
+            *reinterpret_cast<f32x4*>(P + off[i]) = p4[i];
+            *reinterpret_cast<f32x4*>(M + off[i]) = m4[i];
+            *reinterpret_cast<f32x4*>(V + off[i]) = v4[i];
+            if (T.p_bf16) {
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 w = {(unsigned)q[0] | ((unsigned)q[1] << 16),
+                                 (unsigned)q[2] | ((unsigned)q[3] << 16)};
+                *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(T.p_bf16) + off[i]) = w;
+            }
+        } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int c = c0 + cq + e;
-                if (c < cols) {
-                    const int64_t x = (int64_t)r * cols + c;
-                    const float gi = T.g[x];
-                    const float mi = T.m[x] + omb1 * (gi - T.m[x]);
-                    const float vi = T.v[x] * b2 + omb2 * gi * gi;
-                    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-                    const float pi = T.p[x] * decay - step_size * (mi / denom);
-                    T.p[x] = pi;
-                    T.m[x] = mi;
-                    T.v[x] = vi;
-                    const unsigned u = __builtin_bit_cast(unsigned, pi);
-                    q[e] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-                    if (T.p_bf16) reinterpret_cast<unsigned short*>(T.p_bf16)[x] = q[e];
-                }
+                if (c0 + cq + e >= cols) continue;
+                P[off[i] + e] = p4[i][e]; M[off[i] + e] = m4[i][e]; V[off[i] + e] = v4[i][e];
+                if (T.p_bf16) reinterpret_cast<unsigned short*>(T.p_bf16)[off[i] + e] = q[e];
             }
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sT[cq + e][rl] = q[e];
     }
     if (!T.p_bf16_t) return;
     __syncthreads();
@@ -513,10 +556,21 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(AdamJobs jobs) {
     const int c = c0 + cl;
     if (c >= cols) return;
     unsigned short* dst = reinterpret_cast<unsigned short*>(T.p_bf16_t) + (int64_t)c * rows;
+    if ((rows & 7) == 0 && r0 + rb + 16 <= rows) {
+        u32x4 w0, w1;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const int r = r0 + rb + e;
-        if (r < rows) dst[r] = sT[cl][rb + e];
+        for (int e = 0; e < 4; ++e) {
+            w0[e] = (unsigned)sT[cl][rb + 2 * e] | ((unsigned)sT[cl][rb + 2 * e + 1] << 16);
+            w1[e] = (unsigned)sT[cl][rb + 8 + 2 * e] | ((unsigned)sT[cl][rb + 9 + 2 * e] << 16);
+        }
+        *reinterpret_cast<u32x4*>(dst + r0 + rb) = w0;
+        *reinterpret_cast<u32x4*>(dst + r0 + rb + 8) = w1;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int r = r0 + rb + e;
+            if (r < rows) dst[r] = sT[cl][rb + e];
+        }
     }
 }
 }  // namespace

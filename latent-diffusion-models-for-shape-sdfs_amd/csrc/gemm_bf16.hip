@@ -39,34 +39,39 @@ __device__ __forceinline__ unsigned pack2_bf16(float a, float b) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
 }
 
-// Issue the LDS-DMA pieces of one operand tile (ROWS x 64 k) of stage `ks` into LDS at `dst`.
-// Piece i (1 KiB) = tile rows 8i..8i+7; wave w issues pieces w, w+4, ...  Lane L: row 8i+L/8,
-// LDS chunk L%8 <- global chunk (L%8) ^ ((row >> 1) & 7).
 // Per-lane source pointers of one operand tile (ROWS x 64 k): piece i (1 KiB) = tile rows
-// 8i..8i+7; wave w issues pieces w, w+4, ...  Lane L: row 8i+L/8, LDS chunk L%8 <- global chunk
-// (L%8) ^ ((row >> 1) & 7).  Rows past the end are clamped (valid bytes, never stored).
-template <int ROWS>
+// 8i..8i+7; the NW waves of the workgroup issue pieces w, w + NW, ...  Lane L: row 8i+L/8, LDS
+// chunk L%8 <- global chunk (L%8) ^ ((row >> 1) & 7).  Rows past the end are clamped (valid
+// bytes, never stored).
+template <int ROWS, int NW>
 struct TileSrc {
-    const unsigned short* p[ROWS / 32];
+    static constexpr int NP = ROWS / (8 * NW);          // pieces per wave
+    static_assert(NP >= 1 && ROWS % (8 * NW) == 0, "tile rows vs issuing waves");
+    // Scalar base + 32-bit per-lane byte offsets: the DMA issues in the saddr form (one SGPR
+    // pair, no 64-bit vector address math per piece), and the k step is a scalar add.
+    const char* base;                                    // wave-uniform
+    uint32_t voff[NP];
     __device__ __forceinline__ void init(const unsigned short* src, int64_t ld, int row0,
                                          int nrows, int wave, int lane) {
         const int rl = lane >> 3, cc = lane & 7;
+        base = reinterpret_cast<const char*>(src);
 #pragma unroll
-        for (int j = 0; j < ROWS / 32; ++j) {
-            const int rr = 8 * (wave + 4 * j) + rl;
+        for (int j = 0; j < NP; ++j) {
+            const int rr = 8 * (wave + NW * j) + rl;
             const int row = min(row0 + rr, nrows - 1);
-            p[j] = src + (int64_t)row * ld + 8 * (cc ^ ((rr >> 1) & 7));
+            voff[j] = (uint32_t)(((int64_t)row * ld + 8 * (cc ^ ((rr >> 1) & 7))) * 2);
         }
     }
-    // issue the stage at k offset kk into LDS `dst`, then step to the next 64 k
-    __device__ __forceinline__ void issue(unsigned short* dst, int wave) {
+    // issue the next 64-k stage into LDS `dst` and step on; `again`: re-issue the previous
+    // stage instead (a dummy that keeps every wave's vmcnt arithmetic uniform)
+    __device__ __forceinline__ void issue(unsigned short* dst, int wave, bool again) {
+        const char* b = again ? base - 2 * kBK : base;
 #pragma unroll
-        for (int j = 0; j < ROWS / 32; ++j) {
+        for (int j = 0; j < NP; ++j)
             __builtin_amdgcn_global_load_lds(
-                (const void*)p[j],
-                (__attribute__((address_space(3))) void*)(dst + (wave + 4 * j) * 512), 16, 0, 0);
-            p[j] += kBK;
-        }
+                (const void*)(b + voff[j]),
+                (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 512), 16, 0, 0);
+        if (!again) base += 2 * kBK;
     }
 };
 
@@ -75,14 +80,22 @@ __device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, 
     return *reinterpret_cast<const u32x4*>(tile + row * kBK + 8 * c);
 }
 
-template <int BM, int BN, int STAGES>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(ldm_gemm_args_t a) {
+// KG = 1: 4 waves, 2 x 2 over the output tile, every wave walks every k-step.
+// KG = 2: 8 waves = two k-groups of 4; group g computes the k-steps of parity g (two waves per
+// SIMD working on different stages, so one's LDS reads overlap the other's MFMAs) and the two
+// partial tiles are summed through LDS before the epilogue.  The ring holds STAGES / KG
+// "super-stages" of KG consecutive k-steps.
+template <int BM, int BN, int STAGES, int KG>
+__global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(ldm_gemm_args_t a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-    constexpr int RM = BM / 64, RN = BN / 64;
+    constexpr int RM = BM / 64, RN = BN / 64, NW = 4 * KG;
     constexpr int A_ELEMS = BM * kBK, STAGE_ELEMS = (BM + BN) * kBK;
-    constexpr int G = (BM + BN) / 32;                 // DMA pieces per wave per stage
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wr = wave >> 1, wc = wave & 1;
+    constexpr int G = (BM + BN) / (8 * NW);           // DMA pieces per wave per stage
+    constexpr int SS = STAGES / KG;                   // super-stages in the ring
+    static_assert(STAGES % KG == 0 && SS >= 2, "ring of whole super-stages");
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int grp = wave >> 2, w4 = wave & 3;
+    const int wr = w4 >> 1, wc = w4 & 1;
 
     // ---- which problem / tile: XCD-aware deal of the linear workgroup id (bijective) ------
     // The argument block is read through the kernarg segment pointer (scalar loads at a
@@ -114,29 +127,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(ldm_gemm_args_t a) {
     const __attribute__((address_space(4))) ldm_gemm_prob_t& P = ka->prob[p];
     const int tl = t - first;
     // tiles in groups of 4 tile-rows, column-major inside a group (L2 reuse of both panels)
-    const int grp = tl / (4 * tn_n), gh = min(4, tm_n - grp * 4), in = tl - grp * 4 * tn_n;
-    const int m0 = (grp * 4 + in % gh) * BM, n0 = (in / gh) * BN;
+    const int tg = tl / (4 * tn_n), gh = min(4, tm_n - tg * 4), in = tl - tg * 4 * tn_n;
+    const int m0 = (tg * 4 + in % gh) * BM, n0 = (in / gh) * BN;
 
     // ---- k schedule over the segments -------------------------------------------------------
     int nk = 0;
     for (int s = 0; s < P.n_seg; ++s) nk += P.seg[s].K / kBK;
 
     // DMA sources advance 64 k per issued stage; they are re-seated at each segment start.
-    TileSrc<BM> srcA;
-    TileSrc<BN> srcB;
+    TileSrc<BM, NW> srcA;
+    TileSrc<BN, NW> srcB;
     int seg = -1, seg_left = 0;
-    auto issue = [&](int slot) {
-        if (seg_left == 0) {
+    auto issue = [&](int q) {                 // stage q (q >= nk: dummy re-issue)
+        const bool again = q >= nk;
+        if (!again && seg_left == 0) {
             ++seg;
             const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[seg];
             srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
             srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
             seg_left = S.K / kBK;
         }
-        unsigned short* st = smem + slot * STAGE_ELEMS;
-        srcA.issue(st, wave);
-        srcB.issue(st + A_ELEMS, wave);
-        --seg_left;
+        unsigned short* st = smem + (q % STAGES) * STAGE_ELEMS;
+        srcA.issue(st, wave, again);
+        srcB.issue(st + A_ELEMS, wave, again);
+        if (!again) --seg_left;
     };
 
     f32x16 acc[RM][RN];
@@ -147,43 +161,83 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(ldm_gemm_args_t a) {
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
+    const int nks = (nk + KG - 1) / KG;                 // super-steps
+    for (int ss = 0; ss < SS - 1; ++ss)
+        if (ss < nks)
 #pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) issue(s);
+            for (int u = 0; u < KG; ++u) issue(ss * KG + u);
 
     const int r32 = lane & 31, h = lane >> 5;
-    for (int ks = 0; ks < nk; ++ks) {
-        // RAW: this wave's pieces of stage ks landed (STAGES-2 younger stages may still fly),
+    for (int it = 0; it < nks; ++it) {
+        // RAW: this wave's pieces of super-stage it landed (SS-2 younger ones may still fly),
         // then the barrier makes every wave's pieces visible and retires every wave's reads of
-        // stage ks-1, whose slot the issue below refills (WAR).
-        if (ks + STAGES - 2 < nk)
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((STAGES - 2) * G) : "memory");
+        // super-stage it-1, whose slots the issue below refills (WAR).
+        if (it + SS - 2 < nks)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((SS - 2) * KG * G) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (ks + STAGES - 1 < nk) issue((ks + STAGES - 1) % STAGES);
-        const unsigned short* sa = smem + (ks % STAGES) * STAGE_ELEMS;
-        const unsigned short* sb = sa + A_ELEMS;
-        // every fragment of the stage first (one LDS round trip), then the MFMAs
-        u32x4 af[kBK / 16][RM], bf[kBK / 16][RN];
+        if (it + SS - 1 < nks)
 #pragma unroll
-        for (int s = 0; s < kBK / 16; ++s) {
+            for (int u = 0; u < KG; ++u) issue((it + SS - 1) * KG + u);
+        const int q = it * KG + grp;
+        if (KG == 1 || q < nk) {
+            const unsigned short* sa = smem + (q % STAGES) * STAGE_ELEMS;
+            const unsigned short* sb = sa + A_ELEMS;
+            // every fragment of the stage first (one LDS round trip), then the MFMAs
+            u32x4 af[kBK / 16][RM], bf[kBK / 16][RN];
 #pragma unroll
-            for (int i = 0; i < RM; ++i)
-                af[s][i] = read_frag(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
+            for (int s = 0; s < kBK / 16; ++s) {
 #pragma unroll
-            for (int j = 0; j < RN; ++j)
-                bf[s][j] = read_frag(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
-        }
-        __builtin_amdgcn_sched_barrier(0);     // keep the reads batched ahead of the MFMAs
-#pragma unroll
-        for (int s = 0; s < kBK / 16; ++s)
-#pragma unroll
-            for (int i = 0; i < RM; ++i)
+                for (int i = 0; i < RM; ++i)
+                    af[s][i] = read_frag(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
 #pragma unroll
                 for (int j = 0; j < RN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                        __builtin_bit_cast(bf16x8, af[s][i]), __builtin_bit_cast(bf16x8, bf[s][j]),
-                        acc[i][j], 0, 0, 0);
+                    bf[s][j] = read_frag(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
+            }
+            __builtin_amdgcn_sched_barrier(0);     // keep the reads batched ahead of the MFMAs
+#pragma unroll
+            for (int s = 0; s < kBK / 16; ++s)
+#pragma unroll
+                for (int i = 0; i < RM; ++i)
+#pragma unroll
+                    for (int j = 0; j < RN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            __builtin_bit_cast(bf16x8, af[s][i]),
+                            __builtin_bit_cast(bf16x8, bf[s][j]), acc[i][j], 0, 0, 0);
+        }
+    }
+
+    // ---- k-groups: sum the two partial tiles through LDS ---------------------------------
+    // RM == 2: group g keeps accumulator row-block i = g and receives the other group's;
+    // RM == 1: group 0 receives everything and runs the whole epilogue.
+    if constexpr (KG == 2) {
+        __syncthreads();                                // every DMA landed, every read done
+        float* red = reinterpret_cast<float*>(smem);    // [4 waves][RN][16][64] per block
+        constexpr int BLK = 4 * RN * 16 * 64;
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+            const int owner = RM == 2 ? i : 0;
+            if (grp != owner) {
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        red[i * BLK + ((w4 * RN + j) * 16 + v) * 64 + lane] = acc[i][j][v];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+            const int owner = RM == 2 ? i : 0;
+            if (grp == owner) {
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        acc[i][j][v] += red[i * BLK + ((w4 * RN + j) * 16 + v) * 64 + lane];
+            }
+        }
+        if (RM == 1 && grp != 0) return;
     }
 
     // ---- epilogue ------------------------------------------------------------------------
@@ -269,15 +323,23 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(ldm_gemm_args_t a) {
             }
         }
     };
-    epi(acc[0][0], 0, 0);
-    if constexpr (RN > 1) epi(acc[0][RN - 1], 0, 1);
-    if constexpr (RM > 1) epi(acc[RM - 1][0], 1, 0);
-    if constexpr (RM > 1 && RN > 1) epi(acc[RM - 1][RN - 1], 1, 1);
+    const bool do0 = KG == 1 || RM == 1 || grp == 0;
+    const bool do1 = KG == 1 || grp == 1;
+    if (do0) {
+        epi(acc[0][0], 0, 0);
+        if constexpr (RN > 1) epi(acc[0][RN - 1], 0, 1);
+    }
+    if constexpr (RM > 1) {
+        if (do1) {
+            epi(acc[RM - 1][0], 1, 0);
+            if constexpr (RN > 1) epi(acc[RM - 1][RN - 1], 1, 1);
+        }
+    }
 }
 
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, int KG = 1>
 int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
-    auto* k = &gemm_bf16_kernel<BM, BN, STAGES>;
+    auto* k = &gemm_bf16_kernel<BM, BN, STAGES, KG>;
     constexpr int lds = STAGES * (BM + BN) * kBK * 2;
     static bool attr = false;
     if (!attr) {
@@ -287,7 +349,7 @@ int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
                     hipGetErrorString(e));
         attr = true;
     }
-    hipLaunchKernelGGL(k, dim3(total), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k, dim3(total), dim3(256 * KG), lds, s, a);
     return launch_status("ldm_gemm_bf16");
 }
 
@@ -339,6 +401,11 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
         case 2: return launch_gemm<128, 64, 4>(a, gemm_tiles(a, 128, 64), s);
         case 3: return launch_gemm<128, 128, 3>(a, gemm_tiles(a, 128, 128), s);
         case 4: return launch_gemm<64, 64, 3>(a, gemm_tiles(a, 64, 64), s);
+        case 5: return launch_gemm<64, 64, 6, 2>(a, gemm_tiles(a, 64, 64), s);
+        case 6: return launch_gemm<128, 128, 4, 2>(a, gemm_tiles(a, 128, 128), s);
+        case 7: return launch_gemm<128, 64, 6, 2>(a, gemm_tiles(a, 128, 64), s);
+        case 8: return launch_gemm<64, 64, 8>(a, gemm_tiles(a, 64, 64), s);
+        case 9: return launch_gemm<128, 64, 5>(a, gemm_tiles(a, 128, 64), s);
         default: break;
     }
     set_error("ldm_gemm_bf16: tile %d", tile);

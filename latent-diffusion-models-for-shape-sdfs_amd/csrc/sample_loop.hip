@@ -23,6 +23,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 #ifndef LDM_LOOP_SLEEP
 #define LDM_LOOP_SLEEP 1     // s_sleep units (64 clocks) between polls of the XCD barrier
 #endif
@@ -92,20 +94,21 @@ typedef unsigned long long u64;
 #define LDM_STAGE_IN_FLIGHT 16
 #endif
 constexpr int kStageInFlight = LDM_STAGE_IN_FLIGHT;   // 8-B loads per thread per round
+template <int NT = 256>
 __device__ __forceinline__ void stage(float* xs, const float* X, int n2) {
-    constexpr int U = kStageInFlight;
+    constexpr int U = kStageInFlight * 256 / NT;
     const u64* X2 = reinterpret_cast<const u64*>(X);
-    for (int base = 0; base < n2; base += 256 * U) {
+    for (int base = 0; base < n2; base += NT * U) {
         u64 t[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int i = base + u * 256 + (int)threadIdx.x;
+            const int i = base + u * NT + (int)threadIdx.x;
             t[u] = __hip_atomic_load(X2 + (i < n2 ? i : 0), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int i = base + u * 256 + (int)threadIdx.x;
+            const int i = base + u * NT + (int)threadIdx.x;
             if (i < n2) reinterpret_cast<u64*>(xs)[i] = t[u];
         }
     }
@@ -374,6 +377,282 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// XCD-replica loop (bf16 weights).  Each of the 8 XCDs holds a FULL copy of the network in its
+// G/8 workgroups' registers (bf16 pairs, ~300 VGPRs per lane) and samples the shapes
+// b == xcd (mod 8) on its own, so a layer boundary is a barrier of the G/8 workgroups of one
+// XCD instead of the whole chip (no chip-wide hop).  Wave gw (0..127) of a
+// replica owns rows gw*8 .. gw*8+7 of the in-projection and of every block, and D/128 rows of
+// the out-projection.  Per row the arithmetic is the per-step kernels' exactly: the same
+// k-to-lane map and fma order, and a reduce-scatter over (row, shape) pairs whose butterfly
+// visits the lanes in the same order as the batch reduce-scatter (floating-point addition is
+// commutative, so each sum is the same bits) -- the loop stays bit-identical to the graph path.
+// Placement: workgroups learn their XCD from HW_REG_XCC_ID; if an XCD holds other than G/8 of
+// them the launch reports status 2 and returns before any compute (the host then uses the
+// chip-wide loop), so correctness never rests on the dispatch order.
+enum ReplicaLine { R_START = 0, R_STATUS = 1, R_CNT = 2, R_ARR = 10, R_GEN = 18, R_COUNT = 26 };
+static_assert(R_COUNT * 128 <= (int)kSyncBytes, "replica sync words overflow");
+
+template <int NR, int NJ>
+__device__ __forceinline__ void load_rows_bf16(u32x4 (&w)[NR][NJ], const void* W, int row0,
+                                               int ldw, int K, int lane) {
+    const int nch = K >> 3;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = lane + 64 * j;
+            const bool on = c < nch;
+            const u32x4 u = *reinterpret_cast<const u32x4*>(
+                reinterpret_cast<const unsigned short*>(W) + (size_t)(row0 + r) * ldw +
+                (on ? c : 0) * 8);
+            w[r][j] = on ? u : u32x4{0u, 0u, 0u, 0u};
+        }
+}
+
+// vals[r * MBX + b] = this lane's partial dot product of row r with shape b (row_dot's chain);
+// rows NW..NR-1 have no weights and stay 0 (padding of the reduce-scatter).  wget(r, j) returns
+// the lane's 8 bf16 weights (u32x4) of row r, chunk j -- registers or LDS.
+template <int NR, int NW, int NJ, int MBX, typename WGet>
+__device__ __forceinline__ void rows_partial(float (&vals)[NR * MBX], WGet wget, const float* xs,
+                                             int K, int lane) {
+    const int nch = K >> 3;
+#pragma unroll
+    for (int q = 0; q < NR * MBX; ++q) vals[q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        const int cc = c < nch ? c : 0;
+#pragma unroll
+        for (int b = 0; b < MBX; ++b) {
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(xs + b * K + cc * 8);
+            const f32x4 x1 = *reinterpret_cast<const f32x4*>(xs + b * K + cc * 8 + 4);
+#pragma unroll
+            for (int r = 0; r < NW; ++r) {
+                u32x4 u4 = wget(r, j);
+                // opaque to the optimiser: the bf16 -> fp32 unpack then stays here instead of
+                // being hoisted out of the step loop as 2x the registers (which spilled)
+                asm volatile("" : "+v"(u4));
+                float wf[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const unsigned u = u4[i];
+                    wf[2 * i] = __builtin_bit_cast(float, u << 16);
+                    wf[2 * i + 1] = __builtin_bit_cast(float, u & 0xffff0000u);
+                }
+                float t = vals[r * MBX + b];
+                t = fmaf(wf[0], x0[0], t); t = fmaf(wf[1], x0[1], t);
+                t = fmaf(wf[2], x0[2], t); t = fmaf(wf[3], x0[3], t);
+                t = fmaf(wf[4], x1[0], t); t = fmaf(wf[5], x1[1], t);
+                t = fmaf(wf[6], x1[2], t); t = fmaf(wf[7], x1[3], t);
+                vals[r * MBX + b] = t;
+            }
+        }
+    }
+}
+
+// row_dot's reduce-scatter over NV values: lane group q = lane >> (6 - log2 NV) ends with
+// vals[0] = the full sum of value q.
+template <int NV>
+__device__ __forceinline__ float reduce_scatter(float (&acc)[NV], int lane) {
+    static_assert(NV == 2 || NV == 4 || NV == 8 || NV == 16, "power-of-two value count");
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {
+        const int o = 32 >> lv;
+        const int n = NV >> lv;
+        const bool upper = (lane & o) != 0;
+        if (n > 1) {
+            const int half = n >> 1;
+#pragma unroll
+            for (int i = 0; i < half; ++i) {
+                const float send = upper ? acc[i] : acc[i + half];
+                const float keep = upper ? acc[i + half] : acc[i];
+                acc[i] = keep + __shfl_xor(send, o);
+            }
+        } else {
+            acc[0] += __shfl_xor(acc[0], o);
+        }
+    }
+    return acc[0];
+}
+
+// XCD-local barrier of the nloc workgroups of replica xcc (every storing wave drained its sc1
+// stores; one lane adds; the last arriver of the phase publishes the generation word).
+__device__ __forceinline__ bool replica_sync(unsigned* sync, unsigned xcc, unsigned nloc,
+                                            unsigned phase, int* ok, unsigned limit) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* status = sync + 32 * R_STATUS;
+        unsigned* gen = sync + 32 * (R_GEN + xcc);
+        const unsigned t = __hip_atomic_fetch_add(sync + 32 * (R_ARR + xcc), 1u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool good = true;
+        if (t + 1 == phase * nloc)
+            __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            good = spin_until(gen, phase, status, limit);
+        *ok = good;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    return *ok != 0;
+}
+
+constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per wave
+
+template <int D_, int MBX>
+__global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs a) {
+    constexpr int H = 1024, NB = 4, NWV = kRepWaves, R = H / (32 * NWV), RO = D_ / (32 * NWV);
+    constexpr int NJD = (D_ + 511) / 512, NJH = 2;
+    constexpr int NV = R * MBX, LB = NV >= 16 ? 4 : NV >= 8 ? 3 : NV >= 4 ? 2 : 1;
+    constexpr int NT = 64 * NWV;
+    static_assert(RO * MBX <= NV, "out-projection values fit the reduce-scatter");
+    // LDS: [4] flags | xs [MBX][H] | in-proj weights [4 waves][R][NJD][64 lanes] u32x4 |
+    //      out-proj weights [4 waves][RO][NJH][64] u32x4.  The 4 residual blocks' weights (256
+    //      VGPRs of bf16 pairs) live in registers; the two projections' in LDS (registers
+    //      would spill).
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    int* ok = reinterpret_cast<int*>(smem);
+    float* xs = smem + 4;
+    u32x4* lwi = reinterpret_cast<u32x4*>(smem + 4 + MBX * H);
+    u32x4* lwo = lwi + NWV * R * NJD * 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned* sync = a.ctr;
+    const unsigned G = gridDim.x;
+
+    // ---- census: XCD id, local rank, equal split check -----------------------------------
+    __shared__ unsigned s_xcc, s_rank, s_nloc;
+    if (threadIdx.x == 0) {
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
+        const unsigned rank = __hip_atomic_fetch_add(sync + 32 * (R_CNT + xcc), 1u,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(sync + 32 * R_START, 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        bool good = spin_until(sync + 32 * R_START, G, sync + 32 * R_STATUS, a.spin_limit);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        bool even = true;
+        for (unsigned x = 0; x < 8; ++x)
+            even = even && __hip_atomic_load(sync + 32 * (R_CNT + x), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) == G / 8;
+        if (good && !even)          // placement other than G/8 per XCD: leave it to the host
+            __hip_atomic_store(sync + 32 * R_STATUS, 2u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        s_xcc = xcc; s_rank = rank; s_nloc = G / 8;
+        *ok = good && even;
+    }
+    __syncthreads();
+    if (!*ok) return;
+    const unsigned xcc = s_xcc, nloc = s_nloc;
+    const int B = a.B, D = D_;
+    const int nsh = (B > (int)xcc) + (B > (int)xcc + 8);     // shapes of this replica
+    if (nsh == 0) return;                                     // idle replica (B < 8)
+    const int gw = (int)s_rank * NWV + wave;                  // 0 .. 32 NWV - 1
+    const int row0 = gw * R, orow0 = gw * RO;
+
+    u32x4 wb[NB][R][NJH];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) load_rows_bf16<R, NJH>(wb[k], a.w_blk[k], row0, 2 * H, H, lane);
+    {
+        u32x4 wi[R][NJD], wo[RO][NJH];
+        load_rows_bf16<R, NJD>(wi, a.w_in, row0, D, D, lane);
+        load_rows_bf16<RO, NJH>(wo, a.w_out, orow0, H, H, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < NJD; ++j) lwi[((wave * R + r) * NJD + j) * 64 + lane] = wi[r][j];
+#pragma unroll
+        for (int r = 0; r < RO; ++r)
+#pragma unroll
+            for (int j = 0; j < NJH; ++j) lwo[((wave * RO + r) * NJH + j) * 64 + lane] = wo[r][j];
+    }
+    auto get_in = [&](int r, int j) { return lwi[((wave * R + r) * NJD + j) * 64 + lane]; };
+    auto get_out = [&](int r, int j) { return lwo[((wave * RO + r) * NJH + j) * 64 + lane]; };
+
+    const int q = lane >> (6 - LB);                     // value index this lane finishes
+    const bool qlead = (lane & ((1 << (6 - LB)) - 1)) == 0;
+    const int qr = q / MBX, qb = q % MBX;                 // (row, shape) of value q
+    const int sb = (int)xcc + 8 * qb;                    // global shape index
+    const bool wr_h = qlead && qb < nsh;                 // writes an H-wide row
+    const bool wr_o = wr_h && qr < RO;                   // writes an out-projection row
+    const int mh = row0 + qr, mo = orow0 + (qr < RO ? qr : 0);
+    const float bi = a.b_in[mh];
+    const float bo = a.b_out[mo];
+    float* hrep = a.h + (size_t)xcc * 2 * MBX * H;       // [2][MBX][H] per replica
+    unsigned phase = 0;
+
+    for (int s = 0; s < a.steps; ++s) {
+        const int t = a.t_hi - s;
+        const float* xin = a.x + (size_t)(s & 1) * B * D;
+        float* xout = a.x + (size_t)((s & 1) ^ 1) * B * D;
+        const int sq = qb < nsh ? sb : (int)xcc;
+        float ep[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) ep[k] = a.e_tab[k][(size_t)t * H + mh];
+        const float zp = a.noise[(size_t)t * B * D + (size_t)sq * D + mo];
+        const float xp = __builtin_bit_cast(float, __hip_atomic_load(
+            reinterpret_cast<const unsigned*>(xin + (size_t)sq * D + mo), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
+        const float c1 = a.c1[t], c2 = a.c2[t], sg = a.sg[t];
+        // in-projection over this replica's shapes
+#pragma unroll
+        for (int b = 0; b < MBX; ++b)
+            stage<NT>(xs + b * D, xin + (size_t)((int)xcc + 8 * (b < nsh ? b : 0)) * D, D >> 1);
+        __syncthreads();
+        {
+            float v[NV];
+            rows_partial<R, R, NJD, MBX>(v, get_in, xs, D, lane);
+            const float acc = reduce_scatter<NV>(v, lane);
+            if (wr_h) publish(hrep + (size_t)qb * H + mh, acc + bi);
+        }
+        ++phase;
+        if (!replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit)) return;
+        // the four blocks as four compile-time copies (a runtime block index into wb would
+        // put the register-resident weights in scratch)
+        bool alive = true;
+        auto block = [&](auto KC) {
+            constexpr int k = decltype(KC)::value;
+            if (!alive) return;
+            const float* hin = hrep + (size_t)(k & 1) * MBX * H;
+            float* hout = hrep + (size_t)((k + 1) & 1) * MBX * H;
+            stage<NT>(xs, hin, (MBX * H) >> 1);
+            __syncthreads();
+            float v[NV];
+            rows_partial<R, R, NJH, MBX>(v, [&](int r, int j) { return wb[k][r][j]; }, xs, H,
+                                         lane);
+            const float acc = reduce_scatter<NV>(v, lane);
+            if (wr_h) {
+                const float pre = acc + ep[k];
+                publish(hout + (size_t)qb * H + mh, xs[qb * H + mh] + silu(pre));
+            }
+            ++phase;
+            alive = replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit);
+        };
+        static_assert(NB == 4, "four residual blocks");
+        block(std::integral_constant<int, 0>{});
+        block(std::integral_constant<int, 1>{});
+        block(std::integral_constant<int, 2>{});
+        block(std::integral_constant<int, 3>{});
+        if (!alive) return;
+        stage<NT>(xs, hrep + (size_t)(NB & 1) * MBX * H, (MBX * H) >> 1);
+        __syncthreads();
+        {
+            float v[NV];
+            // out-projection: RO rows, zero-padded to the R-row reduce-scatter
+            rows_partial<R, RO, NJH, MBX>(v, get_out, xs, H, lane);
+            const float acc = reduce_scatter<NV>(v, lane);
+            if (wr_o) {
+                const float pre = acc + bo;
+                const bool noise = t > 0;
+                publish(xout + (size_t)sb * D + mo,
+                        ddpm_update(xp, pre, noise ? zp : 0.f, c1, c2, sg, noise));
+            }
+        }
+        ++phase;
+        if (!replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit)) return;
+    }
+}
+
 // Residency: every workgroup of the grid must be resident at once (the grid barriers wait for
 // all of them).  Checked against the occupancy query x CU count before each plain launch; a
 // cooperative launch would make the same check at +15-19 us per call (MI355X guide,
@@ -398,6 +677,50 @@ bool loop_resident_any(int dtype, int B, int D, int H) {
     return B <= 8 ? loop_resident<float, 8>(B, D, H) : loop_resident<float, 16>(B, D, H);
 }
 
+// The replica loop needs exactly H/4 = 256 workgroups resident, G/8 per XCD (checked in the
+// kernel: status 2 otherwise).  Once a launch has reported status 2 on this process, later
+// launches take the chip-wide loop.
+bool g_replica_off = false;
+
+size_t replica_lds(int D, int MBX) {
+    const int H = 1024, W = kRepWaves, R = H / (32 * W), RO = D / (32 * W);
+    const int NJD = (D + 511) / 512, NJH = 2;
+    return 16 + (size_t)MBX * H * 4 + (size_t)W * (R * NJD + RO * NJH) * 64 * 16;
+}
+
+template <int D_, int MBX>
+bool replica_resident() {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    const size_t lds = replica_lds(D_, MBX);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, (const void*)sample_replica_kernel<D_, MBX>, 64 * kRepWaves, lds) != hipSuccess)
+        return false;
+    return per_cu >= 1 && (long)per_cu * cus >= 256;
+}
+
+bool replica_ok(const ldm_denoiser_t* w, int B) {
+    if (g_replica_off || w->dtype != LDM_BF16 || w->H != 1024 || w->n_blocks != 4) return false;
+    if (w->D == 256) return B <= 8 ? replica_resident<256, 1>() : replica_resident<256, 2>();
+    if (w->D == 512) return B <= 8 ? replica_resident<512, 1>() : replica_resident<512, 2>();
+    return false;
+}
+
+int launch_replica(const LoopArgs& a, hipStream_t s) {
+    const size_t lds = replica_lds(a.D, a.B <= 8 ? 1 : 2);
+    const dim3 grid(a.H / 4), blk(64 * kRepWaves);
+    if (a.D == 256) {
+        if (a.B <= 8) hipLaunchKernelGGL((sample_replica_kernel<256, 1>), grid, blk, lds, s, a);
+        else hipLaunchKernelGGL((sample_replica_kernel<256, 2>), grid, blk, lds, s, a);
+    } else {
+        if (a.B <= 8) hipLaunchKernelGGL((sample_replica_kernel<512, 1>), grid, blk, lds, s, a);
+        else hipLaunchKernelGGL((sample_replica_kernel<512, 2>), grid, blk, lds, s, a);
+    }
+    return launch_status("sample_loop (replica)");
+}
+
 template <typename TW, int MB>
 int launch_loop(const LoopArgs& a, hipStream_t s) {
     const size_t lds = 16 + (size_t)a.B * (a.H > a.D ? a.H : a.D) * sizeof(float);
@@ -410,8 +733,13 @@ int launch_loop(const LoopArgs& a, hipStream_t s) {
 
 using namespace ldm;
 
+// ws = [activations: 32 H floats (chip-wide loop: [2][B][H], B <= 16; replica loop:
+// [8 XCDs][2][MBX <= 2][H])] [sync words: kSyncBytes]
+static size_t act_floats(int H) { return (size_t)32 * H; }
+
 extern "C" size_t ldm_sample_loop_ws_bytes(int B, int H) {
-    return (size_t)2 * B * H * sizeof(float) + kSyncBytes;
+    (void)B;
+    return act_floats(H) * sizeof(float) + kSyncBytes;
 }
 
 extern "C" int ldm_sample_loop_supported(const ldm_denoiser_t* w, int B) {
@@ -442,11 +770,14 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
     a.c1 = sc->c1; a.c2 = sc->c2; a.sg = sc->sigma;
     a.x = x; a.noise = noise;
     a.h = ws;
-    a.ctr = reinterpret_cast<unsigned*>(ws + (size_t)2 * B * w->H);
+    a.ctr = reinterpret_cast<unsigned*>(ws + act_floats(w->H));
     a.status = a.ctr + 32 * L_STATUS;
     const char* bar = getenv("LDM_SAMPLE_LOOP_BARRIER");
-    // default / "xcd": XCD-hierarchical with per-XCD generation words; "direct": hierarchical
-    // arrival, every workgroup polls the chip-wide word; "flat": one counter for everything
+    // default / "replica": one network copy per XCD, XCD-local barriers (bf16 weights; else
+    // "xcd"); "xcd": chip-wide loop, XCD-hierarchical barrier with per-XCD generation words;
+    // "direct": hierarchical arrival, every workgroup polls the chip-wide word; "flat": one
+    // counter for everything
+    const bool replica = (!bar || bar[0] == 'r') && replica_ok(w, B);
     a.hier = (bar && bar[0] == 'f') ? 0 : (bar && bar[0] == 'd') ? 2 : 1;
     a.B = B; a.D = w->D; a.H = w->H; a.t_hi = t_hi; a.steps = steps;
     a.spin_limit = kSpinLimit;
@@ -458,6 +789,7 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
         LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
     hipStream_t st = (hipStream_t)s;
     if (hipMemsetAsync(a.ctr, 0, kSyncBytes, st) != hipSuccess) return launch_status("sample_loop memset");
+    if (replica) return launch_replica(a, st);
     if (w->dtype == LDM_BF16)
         return B <= 8 ? launch_loop<unsigned short, 8>(a, st) : launch_loop<unsigned short, 16>(a, st);
     return B <= 8 ? launch_loop<float, 8>(a, st) : launch_loop<float, 16>(a, st);
@@ -465,9 +797,11 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
 
 extern "C" int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host,
                                       ldm_stream_t s) {
-    const unsigned* st = reinterpret_cast<const unsigned*>(ws + (size_t)2 * B * H) + 32 * L_STATUS;
+    (void)B;
+    const unsigned* st = reinterpret_cast<const unsigned*>(ws + act_floats(H)) + 32 * L_STATUS;
     hipError_t e = hipMemcpyAsync(status_host, st, sizeof(unsigned), hipMemcpyDeviceToHost,
                                   (hipStream_t)s);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
+    if (e == hipSuccess && *status_host == 2) g_replica_off = true;   // placement: chip-wide loop
     return e == hipSuccess ? 0 : (int)e;
 }

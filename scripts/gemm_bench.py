@@ -18,6 +18,11 @@ SHAPES = [(1024, 1024, 2048), (1024, 2048, 1024), (1024, 1024, 1024), (1024, 256
           (256, 1024, 1024), (1024, 1024, 128), (1024, 1024, 4096)]
 if os.environ.get("BIG"):
     SHAPES += [(1 << 20, 512, 512), (512, 512, 1 << 20)]
+if os.environ.get("SHAPE"):          # e.g. SHAPE=1024,1024,2048 (profiling one shape)
+    SHAPES = [tuple(int(v) for v in os.environ["SHAPE"].split(","))]
+TILES = tuple(int(v) for v in os.environ.get("TILES", "1,3,4,5,6,8,9").split(","))
+NO_REF = bool(os.environ.get("NO_REF"))
+OUT = os.environ.get("OUT", "c")     # epilogue outputs: none | c | cb | cbt | all
 
 
 def timed(fn):
@@ -40,11 +45,20 @@ for (M, N, K) in SHAPES:
     fl = 2.0 * M * N * K
     res = {"M": M, "N": N, "K": K}
     reps = REPS if M * N * K < 1 << 34 else 5
-    for tile in (1, 2, 3, 4):
-        args = ops.gemm_args([ops.gemm_problem([(A, B)], M, N, C=C)], tile)
+    Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    CbT = torch.empty(N, M, device=dev, dtype=torch.bfloat16)
+    cs = torch.empty((M + 31) // 32, N, device=dev)
+    outs = {"none": dict(colsum=cs), "c": dict(C=C), "cb": dict(Cb=Cb), "cbt": dict(CbT=CbT),
+            "all": dict(C=C, Cb=Cb, CbT=CbT, colsum=cs)}[OUT]
+    res["out"] = OUT
+    for tile in TILES:
+        args = ops.gemm_args([ops.gemm_problem([(A, B)], M, N, **outs)], tile)
         us = timed(lambda: ops.gemm_launch(args, dev))
         res[f"gemm_t{tile}_us"] = round(us, 2)
         res[f"gemm_t{tile}_tflops"] = round(fl / us / 1e6, 1)
+    if NO_REF:
+        print(json.dumps(res), flush=True)
+        continue
     ref = A.float() @ B.float().T
     ops.gemm([ops.gemm_problem([(A, B)], M, N, C=C)])
     res["max_err"] = float((C - ref).abs().max())

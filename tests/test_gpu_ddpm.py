@@ -159,13 +159,17 @@ def test_sampling_graph_equals_eager_bf16(dev, den):
 
 
 @pytest.mark.parametrize("dtype,n,steps,barrier",
-                         [("bf16", 8, 1000, "xcd"), ("bf16", 1, 40, "xcd"), ("bf16", 5, 40, "xcd"),
+                         [("bf16", 8, 1000, "replica"), ("bf16", 1, 40, "replica"),
+                          ("bf16", 5, 40, "replica"), ("bf16", 9, 40, "replica"),
+                          ("bf16", 13, 40, "replica"), ("bf16", 16, 200, "replica"),
+                          ("bf16", 8, 1000, "xcd"), ("bf16", 1, 40, "xcd"), ("bf16", 5, 40, "xcd"),
                           ("bf16", 16, 40, "xcd"), ("fp32", 8, 40, "xcd"), ("fp32", 13, 40, "xcd"),
                           ("bf16", 8, 200, "flat"), ("fp32", 3, 40, "flat")])
 def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps, barrier, monkeypatch):
     """The one-launch loop (ldm_sample_loop) is bit-identical to the per-step launches: same
-    k-to-lane mapping, fma order, shuffle reduce and epilogues; every barrier completed.  Both
-    grid barriers (XCD-hierarchical default, flat counter) are covered."""
+    k-to-lane mapping, fma order, shuffle reduce and epilogues; every barrier completed.  Every
+    form is covered: the XCD-replica loop (bf16 default), the chip-wide loop with the
+    XCD-hierarchical barrier (fp32 default) and with the flat counter."""
     import ldm_sdf
     monkeypatch.setenv("LDM_SAMPLE_LOOP_BARRIER", barrier)
     model, _ = den

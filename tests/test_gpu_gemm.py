@@ -38,7 +38,7 @@ def _bf_close(got, want, tol):
     return bool(((got.double() - w).abs() <= tol + w.abs() * 2 ** -8).all())
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,Ks", [(1000, 1024, (2048,)), (64, 64, (64,)), (130, 70, (128, 64)),
                                     (1024, 256, (1024,)), (96, 2048, (256, 128, 64, 512))])
 def test_gemm_store_segments_tiles(dev, tile, M, N, Ks):
@@ -150,11 +150,12 @@ def test_gemm_grouped_problems(dev):
     from ldm_sdf import ops
     g = torch.Generator().manual_seed(77)
     shapes = [(1024, 1024, 1024), (256, 1024, 1024), (1024, 128, 1024), (64, 2048, 192)]
-    probs, outs, refs = [], [], []
+    probs, outs, refs, keep = [], [], [], []
     for (M, N, K) in shapes:
         A = _rand((M, K), g, dev).bfloat16()
         B = _rand((N, K), g, dev).bfloat16()
         C = torch.zeros(M, N, device=dev)
+        keep += [A, B]                  # the problem holds raw pointers: keep the operands alive
         probs.append(ops.gemm_problem([(A, B)], M, N, C=C))
         outs.append(C)
         refs.append(A.double() @ B.double().T)
