@@ -27,6 +27,7 @@
 #include "ddpm_common.h"
 
 #include <algorithm>
+#include <string.h>
 
 namespace ldm {
 namespace {
@@ -75,6 +76,16 @@ struct TileSrc {
     }
 };
 
+// The launch's argument block: the caller's problems plus the tile bookkeeping the host
+// resolves once (first tile and tile counts per problem, k-steps), so a workgroup finds its
+// problem with one batch of scalar loads instead of a dependent chain.
+struct GemmKArgs {
+    int n_prob, total;
+    int first[LDM_GEMM_MAX_PROBS];      // first tile of each problem (INT_MAX when unused)
+    int tiles_m[LDM_GEMM_MAX_PROBS], tiles_n[LDM_GEMM_MAX_PROBS], nk[LDM_GEMM_MAX_PROBS];
+    ldm_gemm_prob_t prob[LDM_GEMM_MAX_PROBS];
+};
+
 __device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, int chunk) {
     const int c = chunk ^ ((row >> 1) & 7);
     return *reinterpret_cast<const u32x4*>(tile + row * kBK + 8 * c);
@@ -86,7 +97,7 @@ __device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, 
 // partial tiles are summed through LDS before the epilogue.  The ring holds STAGES / KG
 // "super-stages" of KG consecutive k-steps.
 template <int BM, int BN, int STAGES, int KG>
-__global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(ldm_gemm_args_t a) {
+__global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     constexpr int RM = BM / 64, RN = BN / 64, NW = 4 * KG;
     constexpr int A_ELEMS = BM * kBK, STAGE_ELEMS = (BM + BN) * kBK;
@@ -101,38 +112,21 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(ldm_gemm_args_t a) 
     // The argument block is read through the kernarg segment pointer (scalar loads at a
     // runtime offset); indexing the by-value parameter by a runtime problem id would copy it
     // to scratch.
-    typedef const __attribute__((address_space(4))) ldm_gemm_args_t KArgs;
+    typedef const __attribute__((address_space(4))) GemmKArgs KArgs;
     KArgs* ka = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    const int np = ka->n_prob;
-    int total = 0, p = 0, first = 0, tm_n = 1, tn_n = 1;
-    const int lid = blockIdx.x;
-    int tot_all = 0;
-#pragma unroll
-    for (int i = 0; i < LDM_GEMM_MAX_PROBS; ++i)
-        if (i < np)
-            tot_all += ((ka->prob[i].M + BM - 1) / BM) * ((ka->prob[i].N + BN - 1) / BN);
+    const int lid = blockIdx.x, tot_all = ka->total;
     int t;
     {
         const int q = tot_all / 8, r = tot_all % 8, x = lid % 8;
         t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
     }
-#pragma unroll
-    for (int i = 0; i < LDM_GEMM_MAX_PROBS; ++i) {
-        if (i < np) {
-            const int tm = (ka->prob[i].M + BM - 1) / BM, tn = (ka->prob[i].N + BN - 1) / BN;
-            if (t >= total) { p = i; first = total; tm_n = tm; tn_n = tn; }
-            total += tm * tn;
-        }
-    }
+    const int p = (t >= ka->first[1]) + (t >= ka->first[2]) + (t >= ka->first[3]);
     const __attribute__((address_space(4))) ldm_gemm_prob_t& P = ka->prob[p];
-    const int tl = t - first;
+    const int tl = t - ka->first[p], tm_n = ka->tiles_m[p], tn_n = ka->tiles_n[p];
     // tiles in groups of 4 tile-rows, column-major inside a group (L2 reuse of both panels)
     const int tg = tl / (4 * tn_n), gh = min(4, tm_n - tg * 4), in = tl - tg * 4 * tn_n;
     const int m0 = (tg * 4 + in % gh) * BM, n0 = (in / gh) * BN;
-
-    // ---- k schedule over the segments -------------------------------------------------------
-    int nk = 0;
-    for (int s = 0; s < P.n_seg; ++s) nk += P.seg[s].K / kBK;
+    const int nk = ka->nk[p];
 
     // DMA sources advance 64 k per issued stage; they are re-seated at each segment start.
     TileSrc<BM, NW> srcA;
@@ -340,6 +334,24 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(ldm_gemm_args_t a) 
 template <int BM, int BN, int STAGES, int KG = 1>
 int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
     auto* k = &gemm_bf16_kernel<BM, BN, STAGES, KG>;
+    GemmKArgs ka;
+    memset(&ka, 0, sizeof(ka));
+    ka.n_prob = a.n_prob;
+    int acc = 0;
+    for (int p = 0; p < LDM_GEMM_MAX_PROBS; ++p) {
+        if (p < a.n_prob) {
+            const ldm_gemm_prob_t& P = a.prob[p];
+            ka.prob[p] = P;
+            ka.first[p] = acc;
+            ka.tiles_m[p] = (P.M + BM - 1) / BM;
+            ka.tiles_n[p] = (P.N + BN - 1) / BN;
+            for (int g = 0; g < P.n_seg; ++g) ka.nk[p] += P.seg[g].K / kBK;
+            acc += ka.tiles_m[p] * ka.tiles_n[p];
+        } else {
+            ka.first[p] = 0x7fffffff;
+        }
+    }
+    ka.total = acc;
     constexpr int lds = STAGES * (BM + BN) * kBK * 2;
     static bool attr = false;
     if (!attr) {
@@ -349,7 +361,7 @@ int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
                     hipGetErrorString(e));
         attr = true;
     }
-    hipLaunchKernelGGL(k, dim3(total), dim3(256 * KG), lds, s, a);
+    hipLaunchKernelGGL(k, dim3(total), dim3(256 * KG), lds, s, ka);
     return launch_status("ldm_gemm_bf16");
 }
 

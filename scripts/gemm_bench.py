@@ -43,7 +43,7 @@ for (M, N, K) in SHAPES:
     B = torch.randn(N, K, device=dev, generator=g).bfloat16()
     C = torch.empty(M, N, device=dev)
     fl = 2.0 * M * N * K
-    res = {"M": M, "N": N, "K": K}
+    res = {"M": M, "N": N, "K": K, "splitk": int(os.environ.get("SPLITK", "1"))}
     reps = REPS if M * N * K < 1 << 34 else 5
     Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     CbT = torch.empty(N, M, device=dev, dtype=torch.bfloat16)
@@ -51,8 +51,16 @@ for (M, N, K) in SHAPES:
     outs = {"none": dict(colsum=cs), "c": dict(C=C), "cb": dict(Cb=Cb), "cbt": dict(CbT=CbT),
             "all": dict(C=C, Cb=Cb, CbT=CbT, colsum=cs)}[OUT]
     res["out"] = OUT
+    SPLIT = int(os.environ.get("SPLITK", "1"))      # emulate split-K: one problem per K slice
+    parts = [torch.empty(M, N, device=dev) for _ in range(SPLIT)] if SPLIT > 1 else None
     for tile in TILES:
-        args = ops.gemm_args([ops.gemm_problem([(A, B)], M, N, **outs)], tile)
+        if SPLIT > 1:
+            ks = K // SPLIT
+            probs = [ops.gemm_problem([(A[:, i * ks:(i + 1) * ks], B[:, i * ks:(i + 1) * ks])],
+                                      M, N, C=parts[i]) for i in range(SPLIT)]
+            args = ops.gemm_args(probs, tile)
+        else:
+            args = ops.gemm_args([ops.gemm_problem([(A, B)], M, N, **outs)], tile)
         us = timed(lambda: ops.gemm_launch(args, dev))
         res[f"gemm_t{tile}_us"] = round(us, 2)
         res[f"gemm_t{tile}_tflops"] = round(fl / us / 1e6, 1)
