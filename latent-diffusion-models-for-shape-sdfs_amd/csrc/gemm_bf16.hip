@@ -27,6 +27,7 @@
 #include "ddpm_common.h"
 
 #include <algorithm>
+#include <stdlib.h>
 #include <string.h>
 
 namespace ldm {
@@ -74,6 +75,19 @@ struct TileSrc {
                 (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 512), 16, 0, 0);
         if (!again) base += 2 * kBK;
     }
+    // register staging (RS kernels): the same pieces through VGPRs, written to the same
+    // lane-linear LDS image by ds_write_b128 once the compute of the previous stage is done
+    __device__ __forceinline__ void load(u32x4* r) {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) r[j] = *reinterpret_cast<const u32x4*>(base + voff[j]);
+        base += 2 * kBK;
+    }
+    __device__ __forceinline__ void store(unsigned short* dst, const u32x4* r, int wave,
+                                          int lane) const {
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+            *reinterpret_cast<u32x4*>(dst + (wave + NW * j) * 512 + lane * 8) = r[j];
+    }
 };
 
 // The launch's argument block: the caller's problems plus the tile bookkeeping the host
@@ -96,7 +110,7 @@ __device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, 
 // SIMD working on different stages, so one's LDS reads overlap the other's MFMAs) and the two
 // partial tiles are summed through LDS before the epilogue.  The ring holds STAGES / KG
 // "super-stages" of KG consecutive k-steps.
-template <int BM, int BN, int STAGES, int KG>
+template <int BM, int BN, int STAGES, int KG, bool RS>
 __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     constexpr int RM = BM / 64, RN = BN / 64, NW = 4 * KG;
@@ -155,13 +169,72 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
+    const int r32 = lane & 31, h = lane >> 5;
+    auto compute = [&](const unsigned short* sa) {
+        const unsigned short* sb = sa + A_ELEMS;
+        // every fragment of the stage first (one LDS round trip), then the MFMAs
+        u32x4 af[kBK / 16][RM], bf[kBK / 16][RN];
+#pragma unroll
+        for (int s = 0; s < kBK / 16; ++s) {
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+                af[s][i] = read_frag(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+                bf[s][j] = read_frag(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
+        }
+        __builtin_amdgcn_sched_barrier(0);     // keep the reads batched ahead of the MFMAs
+#pragma unroll
+        for (int s = 0; s < kBK / 16; ++s)
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        __builtin_bit_cast(bf16x8, af[s][i]),
+                        __builtin_bit_cast(bf16x8, bf[s][j]), acc[i][j], 0, 0, 0);
+    };
+
+    if constexpr (RS) {
+        // register-staged double buffer: stage it+1 waits in VGPRs while stage it computes
+        static_assert(KG == 1 && STAGES == 2, "register staging: 2 LDS buffers, one k-group");
+        u32x4 ra[TileSrc<BM, NW>::NP], rb[TileSrc<BN, NW>::NP];
+        auto load = [&]() {
+            if (seg_left == 0) {
+                ++seg;
+                const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[seg];
+                srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
+                srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
+                seg_left = S.K / kBK;
+            }
+            srcA.load(ra);
+            srcB.load(rb);
+            --seg_left;
+        };
+        auto store = [&](int q) {
+            unsigned short* st = smem + (q & 1) * STAGE_ELEMS;
+            srcA.store(st, ra, wave, lane);
+            srcB.store(st + A_ELEMS, rb, wave, lane);
+        };
+        load();
+        store(0);
+        if (nk > 1) load();
+        __syncthreads();
+        for (int it = 0; it < nk; ++it) {
+            compute(smem + (it & 1) * STAGE_ELEMS);
+            if (it + 1 < nk) {
+                store(it + 1);
+                if (it + 2 < nk) load();
+            }
+            __syncthreads();
+        }
+    } else {
     const int nks = (nk + KG - 1) / KG;                 // super-steps
     for (int ss = 0; ss < SS - 1; ++ss)
         if (ss < nks)
 #pragma unroll
             for (int u = 0; u < KG; ++u) issue(ss * KG + u);
 
-    const int r32 = lane & 31, h = lane >> 5;
     for (int it = 0; it < nks; ++it) {
         // RAW: this wave's pieces of super-stage it landed (SS-2 younger ones may still fly),
         // then the barrier makes every wave's pieces visible and retires every wave's reads of
@@ -174,31 +247,8 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
 #pragma unroll
             for (int u = 0; u < KG; ++u) issue((it + SS - 1) * KG + u);
         const int q = it * KG + grp;
-        if (KG == 1 || q < nk) {
-            const unsigned short* sa = smem + (q % STAGES) * STAGE_ELEMS;
-            const unsigned short* sb = sa + A_ELEMS;
-            // every fragment of the stage first (one LDS round trip), then the MFMAs
-            u32x4 af[kBK / 16][RM], bf[kBK / 16][RN];
-#pragma unroll
-            for (int s = 0; s < kBK / 16; ++s) {
-#pragma unroll
-                for (int i = 0; i < RM; ++i)
-                    af[s][i] = read_frag(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
-#pragma unroll
-                for (int j = 0; j < RN; ++j)
-                    bf[s][j] = read_frag(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
-            }
-            __builtin_amdgcn_sched_barrier(0);     // keep the reads batched ahead of the MFMAs
-#pragma unroll
-            for (int s = 0; s < kBK / 16; ++s)
-#pragma unroll
-                for (int i = 0; i < RM; ++i)
-#pragma unroll
-                    for (int j = 0; j < RN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                            __builtin_bit_cast(bf16x8, af[s][i]),
-                            __builtin_bit_cast(bf16x8, bf[s][j]), acc[i][j], 0, 0, 0);
-        }
+        if (KG == 1 || q < nk) compute(smem + (q % STAGES) * STAGE_ELEMS);
+    }
     }
 
     // ---- k-groups: sum the two partial tiles through LDS ---------------------------------
@@ -245,6 +295,30 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
             const bool ncol = n < P.N;
             const int nn = ncol ? n : P.N - 1;
             const float bias = P.bias ? P.bias[nn] : 0.f;
+            // The fp32 operands the mode reads (R or C; P_in) are fetched for all 16 rows in
+            // one batch before any use: padding rows read row 0 (a valid address) and drop the
+            // value.  A load guarded per element makes hipcc branch around it and wait for each
+            // one in turn (guide §5 "Projection GEMM", trap 4(c)): 16 dependent round trips.
+            const float* x1 = nullptr;                           // R (or C for ACCUM)
+            int64_t ld1 = 0;
+            if (mode == LDM_GEMM_RESID_SILU || mode == LDM_GEMM_ADD_R ||
+                (mode == LDM_GEMM_DGRAD_SILU && P.R)) {
+                x1 = P.R;
+                ld1 = P.ldr;
+            } else if (mode == LDM_GEMM_ACCUM) {
+                x1 = P.C;
+                ld1 = P.ldc;
+            }
+            const float* x2 = (mode == LDM_GEMM_DGRAD_SILU || mode == LDM_GEMM_LOSS) ? P.P_in
+                                                                                  : nullptr;
+            float v1[16], v2[16];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
+                const int bb = (ncol && b < P.M_valid) ? b : 0;
+                v1[v] = x1 ? x1[(int64_t)bb * ld1 + nn] : 0.f;
+                v2[v] = x2 ? x2[(int64_t)bb * P.ldp_in + nn] : 0.f;
+            }
             float out[16];
             float lsum = 0.f;
 #pragma unroll
@@ -253,8 +327,8 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                 const bool live = ncol && b < P.M_valid;   // padding rows: nothing read / fp32 kept
                 const bool inb = ncol && b < P.M;
                 const int bb = live ? b : 0;
-                const int64_t ir = (int64_t)bb * P.ldr + nn, ip = (int64_t)bb * P.ldp_in + nn;
                 const int64_t ic = (int64_t)bb * P.ldc + nn;
+                const float r1 = live ? v1[v] : 0.f, r2 = live ? v2[v] : 0.f;
                 const float pre = c[v] + bias;
                 float o = pre;
                 switch (mode) {
@@ -264,19 +338,19 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                         break;
                     case LDM_GEMM_RESID_SILU:
                         if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
-                        o = (live ? P.R[ir] : 0.f) + silu(pre);
+                        o = r1 + silu(pre);
                         break;
                     case LDM_GEMM_RELU: o = fmaxf(pre, 0.f); break;
-                    case LDM_GEMM_ACCUM: o = (live ? P.C[ic] : 0.f) + pre; break;
-                    case LDM_GEMM_ADD_R: o = (live ? P.R[ir] : 0.f) + pre; break;
+                    case LDM_GEMM_ACCUM: o = r1 + pre; break;
+                    case LDM_GEMM_ADD_R: o = r1 + pre; break;
                     case LDM_GEMM_DGRAD_SILU: {
-                        const float dh = (P.R && live) ? P.R[ir] + pre : pre;
+                        const float dh = P.R ? r1 + pre : pre;
                         if (P.C && live) P.C[ic] = dh;
-                        o = dh * silu_grad(live ? P.P_in[ip] : 0.f);
+                        o = dh * silu_grad(r2);
                         break;
                     }
                     case LDM_GEMM_LOSS: {
-                        const float d = pre - (live ? P.P_in[ip] : 0.f);
+                        const float d = pre - r2;
                         lsum += live ? d * d : 0.f;
                         o = P.scale * d;
                         break;
@@ -331,9 +405,9 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     }
 }
 
-template <int BM, int BN, int STAGES, int KG = 1>
+template <int BM, int BN, int STAGES, int KG = 1, bool RS = false>
 int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
-    auto* k = &gemm_bf16_kernel<BM, BN, STAGES, KG>;
+    auto* k = &gemm_bf16_kernel<BM, BN, STAGES, KG, RS>;
     GemmKArgs ka;
     memset(&ka, 0, sizeof(ka));
     ka.n_prob = a.n_prob;
@@ -405,9 +479,19 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
                     "alignment, ldct and M multiples of 4", p);
     }
     // tile: 128 x 128 once the 64 x 64 grid has >= 8 workgroups per CU (C19's 1M-row
-    // products); else 64 x 64 (config 2: 256-768 workgroups)
+    // products); else 64 x 64 (config 2: 256-768 workgroups) on a 3-stage ring (48 KiB, so
+    // three workgroups share a CU and a 768-tile launch is resident at once; ring depth
+    // beyond 2 buys a lone workgroup nothing -- the per-CU DMA rate bounds it: profiles/r02b)
+    // LDM_GEMM_TILE (tuning only) replaces the automatic choice
+    static const int forced = [] {
+        const char* e = getenv("LDM_GEMM_TILE");
+        return e ? atoi(e) : 0;
+    }();
     int tile = a.tile;
-    if (tile == 0) tile = gemm_tiles(a, 64, 64) >= 2048 ? 3 : 1;
+    if (tile == 0) {
+        const int t64 = gemm_tiles(a, 64, 64);
+        tile = forced ? forced : t64 >= 2048 ? 3 : 4;
+    }
     switch (tile) {
         case 1: return launch_gemm<64, 64, 4>(a, gemm_tiles(a, 64, 64), s);
         case 2: return launch_gemm<128, 64, 4>(a, gemm_tiles(a, 128, 64), s);
@@ -418,6 +502,12 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
         case 7: return launch_gemm<128, 64, 6, 2>(a, gemm_tiles(a, 128, 64), s);
         case 8: return launch_gemm<64, 64, 8>(a, gemm_tiles(a, 64, 64), s);
         case 9: return launch_gemm<128, 64, 5>(a, gemm_tiles(a, 128, 64), s);
+        case 10: return launch_gemm<64, 64, 2>(a, gemm_tiles(a, 64, 64), s);
+        case 11: return launch_gemm<64, 64, 4, 2>(a, gemm_tiles(a, 64, 64), s);
+        case 12: return launch_gemm<128, 64, 3>(a, gemm_tiles(a, 128, 64), s);
+        case 13: return launch_gemm<64, 64, 2, 1, true>(a, gemm_tiles(a, 64, 64), s);
+        case 14: return launch_gemm<128, 128, 2, 1, true>(a, gemm_tiles(a, 128, 128), s);
+        case 15: return launch_gemm<128, 64, 2, 1, true>(a, gemm_tiles(a, 128, 64), s);
         default: break;
     }
     set_error("ldm_gemm_bf16: tile %d", tile);

@@ -263,12 +263,14 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         {n: torch.empty_like(v) for n, v in state.masters.items()}
     T = schedule.T
     for _ in range(steps):
+        # full-batch steps (batch == M) take the latents as they are: no index, no gather
         idx = torch.randint(0, M, (batch,), device=device, generator=generator) \
-            if batch != M else torch.arange(M, device=device)
+            if batch != M else None
         t = torch.randint(0, T, (batch,), device=device, generator=generator, dtype=torch.int32)
         eps = torch.randn(batch, D, device=device, generator=generator)
         lo, hi = ldist.batch_shard(batch, rank, world)
-        x0 = latents[idx[lo:hi]].contiguous()
+        x0 = latents[idx[lo:hi]].contiguous() if idx is not None else \
+            latents[lo:hi].float().contiguous()
         loss, grads = train_step(denoiser, schedule, x0, t[lo:hi], eps[lo:hi], dtype=dtype,
                                  grads=grads, group=group)
         if state.optimizer is not None:          # caller-supplied torch optimizer
@@ -305,5 +307,10 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
     if state.optimizer is None:
         denoiser.invalidate()    # E tables (sampling) are rebuilt from the trained masters
         state.adam_table = None  # ... and so are the working copies the table pointed at
-    state.losses = [float(l) if isinstance(l, torch.Tensor) else l for l in state.losses]
+    # one device->host transfer for the whole run, not one per step
+    pend = [i for i, l in enumerate(state.losses) if isinstance(l, torch.Tensor)]
+    if pend:
+        vals = torch.cat([state.losses[i].reshape(1).float() for i in pend]).tolist()
+        for i, v in zip(pend, vals):
+            state.losses[i] = v
     return state

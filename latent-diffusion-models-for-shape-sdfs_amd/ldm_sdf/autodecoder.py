@@ -279,7 +279,11 @@ def train_autodecoder(decoder: SDFDecoder, xyz: torch.Tensor, sdf: torch.Tensor,
         state.lat_optimizer.step()
         state.step += 1
         state.losses.append(loss)
-    state.losses = [float(l) if isinstance(l, torch.Tensor) else l for l in state.losses]
+    pend = [i for i, l in enumerate(state.losses) if isinstance(l, torch.Tensor)]
+    if pend:                     # one device->host transfer for the whole run
+        vals = torch.cat([state.losses[i].reshape(1).float() for i in pend]).tolist()
+        for i, v in zip(pend, vals):
+            state.losses[i] = v
     for l in range(9):
         decoder.weights[l] = state.masters[f"W{l}"].detach().to("cpu").contiguous()
         decoder.biases[l] = state.masters[f"b{l}"].detach().to("cpu").contiguous()

@@ -39,11 +39,12 @@ def timed(fn):
 
 g = torch.Generator(device=dev).manual_seed(0)
 for (M, N, K) in SHAPES:
-    A = torch.randn(M, K, device=dev, generator=g).bfloat16()
-    B = torch.randn(N, K, device=dev, generator=g).bfloat16()
+    PAD = int(os.environ.get("PAD", "0"))         # extra row pitch (elements): L2 channel spread
+    A = torch.randn(M, K + PAD, device=dev, generator=g).bfloat16()[:, :K]
+    B = torch.randn(N, K + PAD, device=dev, generator=g).bfloat16()[:, :K]
     C = torch.empty(M, N, device=dev)
     fl = 2.0 * M * N * K
-    res = {"M": M, "N": N, "K": K, "splitk": int(os.environ.get("SPLITK", "1"))}
+    res = {"M": M, "N": N, "K": K, "splitk": int(os.environ.get("SPLITK", "1")), "pad": PAD}
     reps = REPS if M * N * K < 1 << 34 else 5
     Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     CbT = torch.empty(N, M, device=dev, dtype=torch.bfloat16)

@@ -54,4 +54,11 @@ for key in sorted(vals, key=lambda k: -sum(dur[k])):
         out.append("  hbm read %.3f MB (FETCH_SIZE x2)" % (a["FETCH_SIZE"] * 1024 * 2 / 1e6))
     if "WRITE_SIZE" in a:
         out.append("  hbm write %.3f MB" % (a["WRITE_SIZE"] * 1024 / 1e6))
+    if "TCC_HIT_sum" in a:
+        h, m = a["TCC_HIT_sum"], a.get("TCC_MISS_sum", 0.0)
+        out.append("  l2: hit %.3g miss %.3g (hit rate %.3f; x128 B = %.1f MB requested)" % (
+            h, m, h / max(1.0, h + m), (h + m) * 128 / 1e6))
+    if "TA_BUSY_avr" in a and "GRBM_GUI_ACTIVE" in a:
+        out.append("  ta busy avr %.3f max %.3f (of GPU cycles)" % (
+            a["TA_BUSY_avr"] / a["GRBM_GUI_ACTIVE"], a.get("TA_BUSY_max", 0) / a["GRBM_GUI_ACTIVE"]))
     print("\n".join(out))
