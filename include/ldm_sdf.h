@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LDM_ABI_VERSION 2
+#define LDM_ABI_VERSION 3
 
 /* dtypes */
 #define LDM_F32 0
@@ -327,13 +327,23 @@ int ldm_latent_l2_reg(const float* z, int S, int L, float coef, float* loss_io, 
  *                        layer below's pre-activation, fused into the G W product)
  *   LDM_GEMM_LOSS        d = pre - P_in (targets); out = scale * d; loss_part += d^2 (A9)
  *   LDM_GEMM_ADD_R       out = R + pre
+ *   LDM_GEMM_RELU_BWD    out = Rb[m][n] > 0 ? pre : 0   (Rb bf16: the ReLU backward through the
+ *                        saved post-activation, fused into the G W product; C19)
  * Outputs (each optional): C fp32 [m][n] (ldc; in DGRAD_SILU C receives dh), Cb bf16 [m][n]
  * (ldcb), CbT bf16 TRANSPOSED [n][m] (ldct; M and ldct multiples of 4), colsum fp32
  * [ceil(M/32)][N]: per 32-row block column sums of out (bias gradients, summed in fixed order
  * by the caller), loss_part fp32 [ceil(M/32)][ceil(N/32)]: sums of d^2 (LOSS).
+ * Split-K (k_split > 1; n_seg == 1, mode STORE or ACCUM, C the only output, K a multiple of
+ * 128 * k_split): the K range is cut into k_split slices that run as separate tiles, each
+ * writing its raw fp32 partial [M_valid][N] into ws (k_split * M * N floats); a second kernel
+ * sums the slices in slice order (deterministic) and applies bias / ACCUM.  For the weight
+ * gradients G^T X of C19, contracted over ~1M samples into a 512 x 512 output.
  * Up to LDM_GEMM_MAX_PROBS independent problems share one launch.  tile: 0 = auto, 1 = 64x64,
  * 2 = 128x64, 3 = 128x128, 4 = 64x64 with a 3-deep ring; 5 / 6 / 7 = 64x64 / 128x128 / 128x64
- * with 8 waves in two k-groups (csrc/gemm_bf16.hip). */
+ * with 8 waves in two k-groups; 16 / 17 / 18 = persistent 128x128 (4-deep ring) / 128x128
+ * (2-deep ring, 2 workgroups per CU) / 64x64 (3-deep ring): one workgroup per CU slot loops
+ * over tiles and its LDS ring streams the next tile's k-steps under the current tile's last
+ * MFMAs and epilogue (csrc/gemm_bf16.hip). */
 #define LDM_GEMM_MAX_SEGS 8
 #define LDM_GEMM_MAX_PROBS 4
 #define LDM_GEMM_STORE 0
@@ -344,6 +354,7 @@ int ldm_latent_l2_reg(const float* z, int S, int L, float coef, float* loss_io, 
 #define LDM_GEMM_DGRAD_SILU 5
 #define LDM_GEMM_LOSS 6
 #define LDM_GEMM_ADD_R 7
+#define LDM_GEMM_RELU_BWD 8
 typedef struct ldm_gemm_seg {
     const void* A; const void* B;    /* bf16 */
     int64_t lda, ldb;
@@ -362,6 +373,15 @@ typedef struct ldm_gemm_prob {
     void* CbT;         int64_t ldct;
     float* colsum;
     float* loss_part;
+    int32_t k_split;   /* 0 or 1: whole K per tile; > 1: split-K into ws (see above) */
+    int32_t ct_blk;    /* > 0: CbT written m-blocked, [ceil(M/ct_blk)][N][ct_blk] (ldct unused):
+                        * the sample-axis operands of C19, whose 1M-long rows would otherwise put
+                        * every row of a tile in its own memory page */
+    float* ws;
+    const void* Rb;    int64_t ldrb;   /* bf16 [m][n] (LDM_GEMM_RELU_BWD) */
+    int64_t slice_a, slice_b;          /* split-K: slice s starts s * slice_a (A) / s * slice_b
+                                        * (B) elements in (0: s * K / k_split, contiguous K);
+                                        * with ct_blk-blocked operands each slice is one block */
 } ldm_gemm_prob_t;
 typedef struct ldm_gemm_args {
     int32_t n_prob, tile;

@@ -192,7 +192,6 @@ int launch(std::initializer_list<ldm_gemm_prob_t> ps, hipStream_t s) {
     for (const auto& p : ps) a.prob[a.n_prob++] = p;
     return gemm_bf16(a, s);
 }
-#define LDM_TRY(x) do { if (int e_ = (x)) return e_; } while (0)
 
 int check_desc(const ldm_denoiser_t* w, int B, bool bwd) {
     LDM_REQUIRE(w && w->abi_version == LDM_ABI_VERSION, LDM_EINVAL,

@@ -41,46 +41,55 @@ __device__ __forceinline__ unsigned pack2_bf16(float a, float b) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
 }
 
-// Per-lane source pointers of one operand tile (ROWS x 64 k): piece i (1 KiB) = tile rows
-// 8i..8i+7; the NW waves of the workgroup issue pieces w, w + NW, ...  Lane L: row 8i+L/8, LDS
-// chunk L%8 <- global chunk (L%8) ^ ((row >> 1) & 7).  Rows past the end are clamped (valid
-// bytes, never stored).
-template <int ROWS, int NW>
+// Per-lane source pointers of one operand tile (ROWS x KB k): piece i (1 KiB) = tile rows
+// RP*i .. RP*i+RP-1 (RP = 1024 / (2 KB): 8 rows of 128 B at KB = 64, 4 rows of 256 B at
+// KB = 128); the NW waves of the workgroup issue pieces w, w + NW, ...  Lane L: row
+// RP*i + L/(KB/8), LDS chunk L%(KB/8) <- global chunk (L%(KB/8)) ^ swz(row).  Rows past the end
+// are clamped (valid bytes, never stored).
+// swz: KB = 64 -> (row >> 1) & 7 (two 128-B rows span the 64 banks); KB = 128 -> row & 15.
+// Either way the 16 rows one ds_read_b128 lane group reads hit 16 distinct 16-B bank quads.
+template <int KB>
+__device__ __forceinline__ int swz(int row) {
+    return KB == 64 ? (row >> 1) & 7 : row & 15;
+}
+template <int ROWS, int NW, int KB>
 struct TileSrc {
-    static constexpr int NP = ROWS / (8 * NW);          // pieces per wave
-    static_assert(NP >= 1 && ROWS % (8 * NW) == 0, "tile rows vs issuing waves");
+    static constexpr int CPR = KB / 8;                   // 16-B chunks per row
+    static constexpr int RP = 64 / CPR;                  // rows per 1 KiB piece
+    static constexpr int NP = ROWS / (RP * NW);          // pieces per wave
+    static_assert(NP >= 1 && ROWS % (RP * NW) == 0, "tile rows vs issuing waves");
     // Scalar base + 32-bit per-lane byte offsets: the DMA issues in the saddr form (one SGPR
     // pair, no 64-bit vector address math per piece), and the k step is a scalar add.
     const char* base;                                    // wave-uniform
     uint32_t voff[NP];
     __device__ __forceinline__ void init(const unsigned short* src, int64_t ld, int row0,
                                          int nrows, int wave, int lane) {
-        const int rl = lane >> 3, cc = lane & 7;
+        const int rl = lane / CPR, cc = lane % CPR;
         base = reinterpret_cast<const char*>(src);
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
-            const int rr = 8 * (wave + NW * j) + rl;
+            const int rr = RP * (wave + NW * j) + rl;
             const int row = min(row0 + rr, nrows - 1);
-            voff[j] = (uint32_t)(((int64_t)row * ld + 8 * (cc ^ ((rr >> 1) & 7))) * 2);
+            voff[j] = (uint32_t)(((int64_t)row * ld + 8 * (cc ^ swz<KB>(rr))) * 2);
         }
     }
-    // issue the next 64-k stage into LDS `dst` and step on; `again`: re-issue the previous
+    // issue the next KB-deep stage into LDS `dst` and step on; `again`: re-issue the previous
     // stage instead (a dummy that keeps every wave's vmcnt arithmetic uniform)
     __device__ __forceinline__ void issue(unsigned short* dst, int wave, bool again) {
-        const char* b = again ? base - 2 * kBK : base;
+        const char* b = again ? base - 2 * KB : base;
 #pragma unroll
         for (int j = 0; j < NP; ++j)
             __builtin_amdgcn_global_load_lds(
                 (const void*)(b + voff[j]),
                 (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 512), 16, 0, 0);
-        if (!again) base += 2 * kBK;
+        if (!again) base += 2 * KB;
     }
     // register staging (RS kernels): the same pieces through VGPRs, written to the same
     // lane-linear LDS image by ds_write_b128 once the compute of the previous stage is done
     __device__ __forceinline__ void load(u32x4* r) {
 #pragma unroll
         for (int j = 0; j < NP; ++j) r[j] = *reinterpret_cast<const u32x4*>(base + voff[j]);
-        base += 2 * kBK;
+        base += 2 * KB;
     }
     __device__ __forceinline__ void store(unsigned short* dst, const u32x4* r, int wave,
                                           int lane) const {
@@ -91,18 +100,40 @@ struct TileSrc {
 };
 
 // The launch's argument block: the caller's problems plus the tile bookkeeping the host
-// resolves once (first tile and tile counts per problem, k-steps), so a workgroup finds its
-// problem with one batch of scalar loads instead of a dependent chain.
+// resolves once (first tile and tile counts per problem, k-steps per tile, split-K slices), so
+// a workgroup finds its problem with one batch of scalar loads instead of a dependent chain.
 struct GemmKArgs {
     int n_prob, total;
     int first[LDM_GEMM_MAX_PROBS];      // first tile of each problem (INT_MAX when unused)
-    int tiles_m[LDM_GEMM_MAX_PROBS], tiles_n[LDM_GEMM_MAX_PROBS], nk[LDM_GEMM_MAX_PROBS];
+    int tiles_m[LDM_GEMM_MAX_PROBS], tiles_n[LDM_GEMM_MAX_PROBS];
+    int nk[LDM_GEMM_MAX_PROBS];         // k-steps per tile (per slice when split)
+    int ksplit[LDM_GEMM_MAX_PROBS];     // slices (1: whole K)
     ldm_gemm_prob_t prob[LDM_GEMM_MAX_PROBS];
 };
+typedef const __attribute__((address_space(4))) GemmKArgs KArgs;
+typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
 
+template <int KB>
 __device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, int chunk) {
-    const int c = chunk ^ ((row >> 1) & 7);
-    return *reinterpret_cast<const u32x4*>(tile + row * kBK + 8 * c);
+    const int c = chunk ^ swz<KB>(row);
+    return *reinterpret_cast<const u32x4*>(tile + row * KB + 8 * c);
+}
+
+// Tile t of the launch -> (problem, output origin, split-K slice).  Tiles of a problem are
+// slice-major; inside a slice, groups of 4 tile-rows, column-major inside a group (L2 reuse of
+// both panels).
+struct TileLoc {
+    int p, m0, n0, slice;
+};
+template <int BM, int BN>
+__device__ __forceinline__ TileLoc locate(KArgs* ka, int t) {
+    const int p = (t >= ka->first[1]) + (t >= ka->first[2]) + (t >= ka->first[3]);
+    const int tm_n = ka->tiles_m[p], tn_n = ka->tiles_n[p];
+    int tl = t - ka->first[p];
+    const int slice = tl / (tm_n * tn_n);
+    tl -= slice * tm_n * tn_n;
+    const int tg = tl / (4 * tn_n), gh = min(4, tm_n - tg * 4), in = tl - tg * 4 * tn_n;
+    return {p, (tg * 4 + in % gh) * BM, (in / gh) * BN, slice};
 }
 
 // KG = 1: 4 waves, 2 x 2 over the output tile, every wave walks every k-step.
@@ -110,82 +141,125 @@ __device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, 
 // SIMD working on different stages, so one's LDS reads overlap the other's MFMAs) and the two
 // partial tiles are summed through LDS before the epilogue.  The ring holds STAGES / KG
 // "super-stages" of KG consecutive k-steps.
-template <int BM, int BN, int STAGES, int KG, bool RS>
+// PERSIST: one workgroup per resident slot walks a list of tiles (the XCD's contiguous share
+// of the launch, strided by the XCD's workgroup count, so the tiles an XCD runs at once share
+// their operand panels in its L2).  The ring is one continuous stream of k-steps across tile
+// boundaries: the next tile's first stages are in flight while the current tile finishes its
+// MFMAs and runs its epilogue (which touches no LDS), so no workgroup pays the pipeline fill of
+// a short-K tile (C19: K = 512, 8 k-steps) and the epilogue of one tile overlaps loads of the
+// next.
+template <int BM, int BN, int STAGES, int KG, bool RS, bool PERSIST, int KB>
 __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     constexpr int RM = BM / 64, RN = BN / 64, NW = 4 * KG;
-    constexpr int A_ELEMS = BM * kBK, STAGE_ELEMS = (BM + BN) * kBK;
-    constexpr int G = (BM + BN) / (8 * NW);           // DMA pieces per wave per stage
+    constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
+    constexpr int G = TileSrc<BM, NW, KB>::NP + TileSrc<BN, NW, KB>::NP;   // DMA pieces/wave/stage
     constexpr int SS = STAGES / KG;                   // super-stages in the ring
     static_assert(STAGES % KG == 0 && SS >= 2, "ring of whole super-stages");
+    static_assert(!PERSIST || (KG == 1 && !RS), "persistent: one k-group, LDS-DMA ring");
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int grp = wave >> 2, w4 = wave & 3;
     const int wr = w4 >> 1, wc = w4 & 1;
+    const int r32 = lane & 31, h = lane >> 5;
 
-    // ---- which problem / tile: XCD-aware deal of the linear workgroup id (bijective) ------
     // The argument block is read through the kernarg segment pointer (scalar loads at a
     // runtime offset); indexing the by-value parameter by a runtime problem id would copy it
     // to scratch.
-    typedef const __attribute__((address_space(4))) GemmKArgs KArgs;
     KArgs* ka = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     const int lid = blockIdx.x, tot_all = ka->total;
-    int t;
-    {
-        const int q = tot_all / 8, r = tot_all % 8, x = lid % 8;
-        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
-    }
-    const int p = (t >= ka->first[1]) + (t >= ka->first[2]) + (t >= ka->first[3]);
-    const __attribute__((address_space(4))) ldm_gemm_prob_t& P = ka->prob[p];
-    const int tl = t - ka->first[p], tm_n = ka->tiles_m[p], tn_n = ka->tiles_n[p];
-    // tiles in groups of 4 tile-rows, column-major inside a group (L2 reuse of both panels)
-    const int tg = tl / (4 * tn_n), gh = min(4, tm_n - tg * 4), in = tl - tg * 4 * tn_n;
-    const int m0 = (tg * 4 + in % gh) * BM, n0 = (in / gh) * BN;
-    const int nk = ka->nk[p];
 
-    // DMA sources advance 64 k per issued stage; they are re-seated at each segment start.
-    TileSrc<BM, NW> srcA;
-    TileSrc<BN, NW> srcB;
-    int seg = -1, seg_left = 0;
-    auto issue = [&](int q) {                 // stage q (q >= nk: dummy re-issue)
-        const bool again = q >= nk;
-        if (!again && seg_left == 0) {
-            ++seg;
-            const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[seg];
-            srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
-            srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
-            seg_left = S.K / kBK;
+    // ---- tile walk --------------------------------------------------------------------------
+    // non-persistent: one tile, XCD-aware deal of the linear workgroup id (bijective);
+    // persistent: tiles t0, t0 + tstep, ... < tend (the XCD's contiguous chunk)
+    int t0, tstep, tend;
+    if constexpr (PERSIST) {
+        // XCD x (= lid % 8 under round-robin dispatch) has nx workgroups; its chunk of the
+        // tiles is proportional to nx (any grid size, also below 8)
+        const int Gd = gridDim.x, q = Gd >> 3, r = Gd & 7, x = lid & 7;
+        const int nx = q + (x < r), cum = x * q + min(x, r);
+        t0 = (int)((int64_t)tot_all * cum / Gd) + (lid >> 3);
+        tend = (int)((int64_t)tot_all * (cum + nx) / Gd);
+        tstep = nx;
+        if (t0 >= tend) return;                       // no tile (whole workgroup, uniform)
+    } else {
+        const int q = tot_all / 8, r = tot_all % 8, x = lid % 8;
+        t0 = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
+        tstep = 1;
+        tend = t0 + 1;
+    }
+
+    // ---- DMA issue cursor: tile ti, k-step ki of nki; sources re-seated per tile / segment --
+    TileSrc<BM, NW, KB> srcA;
+    TileSrc<BN, NW, KB> srcB;
+    int ti = t0, ki = 0, nki = 0, seg = -1, seg_left = 0, qi = 0;
+    TileLoc il{};
+    auto seat = [&](int sg, int kofs) {       // sources of segment sg, kofs k-steps in
+        KProb& P = ka->prob[il.p];
+        const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[sg];
+        srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, il.m0, P.M, wave, lane);
+        srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, il.n0, P.N, wave, lane);
+        if (P.slice_a) {                      // split-K slice = one block of a blocked operand
+            srcA.base += 2 * P.slice_a * il.slice;
+            srcB.base += 2 * P.slice_b * il.slice;
+            seg_left = ka->nk[il.p];
+        } else {
+            srcA.base += 2 * KB * kofs;
+            srcB.base += 2 * KB * kofs;
+            seg_left = S.K / KB - kofs;
         }
-        unsigned short* st = smem + (q % STAGES) * STAGE_ELEMS;
+    };
+    auto issue = [&]() {                      // the next stage (past the last tile: a dummy)
+        const bool again = ti >= tend;
+        if (!again) {
+            if (ki == 0) {
+                il = locate<BM, BN>(ka, ti);
+                nki = ka->nk[il.p];
+                seg = 0;
+                seat(0, il.slice * nki);
+            } else if (seg_left == 0) {
+                seat(++seg, 0);
+            }
+        }
+        unsigned short* st = smem + (qi % STAGES) * STAGE_ELEMS;
+        ++qi;
         srcA.issue(st, wave, again);
         srcB.issue(st + A_ELEMS, wave, again);
-        if (!again) --seg_left;
+        if (!again) {
+            --seg_left;
+            if (++ki == nki) {
+                ki = 0;
+                ti += tstep;
+            }
+        }
     };
 
     f32x16 acc[RM][RN];
+    auto zero_acc = [&]() {
 #pragma unroll
-    for (int i = 0; i < RM; ++i)
+        for (int i = 0; i < RM; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
+            for (int j = 0; j < RN; ++j)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+                for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+    };
+    zero_acc();
 
-    const int r32 = lane & 31, h = lane >> 5;
     auto compute = [&](const unsigned short* sa) {
         const unsigned short* sb = sa + A_ELEMS;
         // every fragment of the stage first (one LDS round trip), then the MFMAs
-        u32x4 af[kBK / 16][RM], bf[kBK / 16][RN];
+        u32x4 af[KB / 16][RM], bf[KB / 16][RN];
 #pragma unroll
-        for (int s = 0; s < kBK / 16; ++s) {
+        for (int s = 0; s < KB / 16; ++s) {
 #pragma unroll
             for (int i = 0; i < RM; ++i)
-                af[s][i] = read_frag(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
+                af[s][i] = read_frag<KB>(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
 #pragma unroll
             for (int j = 0; j < RN; ++j)
-                bf[s][j] = read_frag(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
+                bf[s][j] = read_frag<KB>(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
         }
         __builtin_amdgcn_sched_barrier(0);     // keep the reads batched ahead of the MFMAs
 #pragma unroll
-        for (int s = 0; s < kBK / 16; ++s)
+        for (int s = 0; s < KB / 16; ++s)
 #pragma unroll
             for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -195,18 +269,187 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                         __builtin_bit_cast(bf16x8, bf[s][j]), acc[i][j], 0, 0, 0);
     };
 
+    // ---- epilogue ------------------------------------------------------------------------
+    // Called once per accumulator tile with compile-time (i, j), so every acc index stays a
+    // constant (a runtime-indexed accumulator array goes to scratch: guide rule 20).
+    auto epi = [&](const TileLoc& L, const f32x16& c, const int i, const int j) {
+        KProb& P = ka->prob[L.p];
+        const int m0 = L.m0, n0 = L.n0;
+        const int mode = P.mode;
+        const int rb = m0 + wr * (BM / 2) + i * 32;           // first row of this 32-row block
+        const int n = n0 + wc * (BN / 2) + j * 32 + r32;
+        const bool ncol = n < P.N;
+        const int nn = ncol ? n : P.N - 1;
+        if (ka->ksplit[L.p] > 1) {                             // split-K: raw partial slab
+            float* dst = P.ws + (int64_t)L.slice * P.M * P.N;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
+                if (ncol && b < P.M_valid) dst[(int64_t)b * P.N + n] = c[v];
+            }
+            return;
+        }
+        const float bias = P.bias ? P.bias[nn] : 0.f;
+        // The operands the mode reads (R or C; P_in; Rb) are fetched for all 16 rows in one
+        // batch before any use: padding rows read row 0 (a valid address) and drop the value.
+        // A load guarded per element makes hipcc branch around it and wait for each one in
+        // turn (guide §5 "Projection GEMM", trap 4(c)): 16 dependent round trips.
+        const float* x1 = nullptr;                           // R (or C for ACCUM)
+        int64_t ld1 = 0;
+        if (mode == LDM_GEMM_RESID_SILU || mode == LDM_GEMM_ADD_R ||
+            (mode == LDM_GEMM_DGRAD_SILU && P.R)) {
+            x1 = P.R;
+            ld1 = P.ldr;
+        } else if (mode == LDM_GEMM_ACCUM) {
+            x1 = P.C;
+            ld1 = P.ldc;
+        }
+        const float* x2 = (mode == LDM_GEMM_DGRAD_SILU || mode == LDM_GEMM_LOSS) ? P.P_in
+                                                                              : nullptr;
+        const unsigned short* xb =
+            mode == LDM_GEMM_RELU_BWD ? reinterpret_cast<const unsigned short*>(P.Rb) : nullptr;
+        float v1[16], v2[16];
+        unsigned short vb[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
+            const int bb = (ncol && b < P.M_valid) ? b : 0;
+            v1[v] = x1 ? x1[(int64_t)bb * ld1 + nn] : 0.f;
+            v2[v] = x2 ? x2[(int64_t)bb * P.ldp_in + nn] : 0.f;
+            vb[v] = xb ? xb[(int64_t)bb * P.ldrb + nn] : (unsigned short)0;
+        }
+        float out[16];
+        float lsum = 0.f;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
+            const bool live = ncol && b < P.M_valid;   // padding rows: nothing read / fp32 kept
+            const bool inb = ncol && b < P.M;
+            const int bb = live ? b : 0;
+            const int64_t ic = (int64_t)bb * P.ldc + nn;
+            const float r1 = live ? v1[v] : 0.f, r2 = live ? v2[v] : 0.f;
+            const float pre = c[v] + bias;
+            float o = pre;
+            switch (mode) {
+                case LDM_GEMM_SILU:
+                    if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
+                    o = silu(pre);
+                    break;
+                case LDM_GEMM_RESID_SILU:
+                    if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
+                    o = r1 + silu(pre);
+                    break;
+                case LDM_GEMM_RELU: o = fmaxf(pre, 0.f); break;
+                case LDM_GEMM_ACCUM: o = r1 + pre; break;
+                case LDM_GEMM_ADD_R: o = r1 + pre; break;
+                case LDM_GEMM_DGRAD_SILU: {
+                    const float dh = P.R ? r1 + pre : pre;
+                    if (P.C && live) P.C[ic] = dh;
+                    o = dh * silu_grad(r2);
+                    break;
+                }
+                case LDM_GEMM_LOSS: {
+                    const float d = pre - r2;
+                    lsum += live ? d * d : 0.f;
+                    o = P.scale * d;
+                    break;
+                }
+                case LDM_GEMM_RELU_BWD: {             // bf16 > 0: sign bit clear, not +0
+                    const unsigned short u = vb[v];
+                    o = (u != 0 && (u & 0x8000u) == 0) ? pre : 0.f;
+                    break;
+                }
+                default: break;
+            }
+            out[v] = live ? o : 0.f;
+            if (mode != LDM_GEMM_DGRAD_SILU && P.C && live) P.C[ic] = out[v];
+            if (P.Cb && inb)
+                reinterpret_cast<unsigned short*>(P.Cb)[(int64_t)b * P.ldcb + nn] =
+                    (unsigned short)(pack2_bf16(out[v], 0.f) & 0xffffu);
+        }
+        if (P.CbT && ncol) {                 // [n][b]: 4 consecutive rows per 8-byte store
+            const int kt = P.ct_blk;
+            unsigned short* T = reinterpret_cast<unsigned short*>(P.CbT);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int b = rb + 8 * g + 4 * h;
+                if (b < P.M) {
+                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                    const u32x2 w = {pack2_bf16(out[4 * g], out[4 * g + 1]),
+                                     pack2_bf16(out[4 * g + 2], out[4 * g + 3])};
+                    const int64_t at = kt ? ((int64_t)(b / kt) * P.N + n) * kt + b % kt
+                                          : (int64_t)n * P.ldct + b;
+                    *reinterpret_cast<u32x2*>(T + at) = w;
+                }
+            }
+        }
+        if (P.colsum) {                      // one partial per 32-row block and column
+            float cs = 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) cs += out[v];
+            cs += __shfl_xor(cs, 32);
+            if (h == 0 && ncol && rb < P.M) P.colsum[(int64_t)(rb / 32) * P.N + n] = cs;
+        }
+        if (mode == LDM_GEMM_LOSS && P.loss_part) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
+            if (lane == 0 && rb < P.M)
+                P.loss_part[(int64_t)(rb / 32) * ((P.N + 31) / 32) + (n0 + wc * (BN / 2) + j * 32) / 32] = lsum;
+        }
+    };
+    auto epilogue = [&](const TileLoc& L, bool do0, bool do1) {
+        if (do0) {
+            epi(L, acc[0][0], 0, 0);
+            if constexpr (RN > 1) epi(L, acc[0][RN - 1], 0, 1);
+        }
+        if constexpr (RM > 1) {
+            if (do1) {
+                epi(L, acc[RM - 1][0], 1, 0);
+                if constexpr (RN > 1) epi(L, acc[RM - 1][RN - 1], 1, 1);
+            }
+        }
+    };
+
+    if constexpr (PERSIST) {
+        // ---- persistent walk: one continuous k-step stream over the workgroup's tiles -------
+        // Every iteration issues one stage (a dummy re-issue once the tiles run out), so the
+        // counted wait below is the same every time: this wave's pieces of the stage about to
+        // be computed landed while SS-2 younger stages may still fly.  Epilogue stores also
+        // count in vmcnt: the wait after an epilogue over-waits for them (never under-waits).
+        for (int u = 0; u < SS - 1; ++u) issue();
+        int tc = t0, kc = 0, qc = 0;
+        TileLoc cl = locate<BM, BN>(ka, tc);
+        int nkc = ka->nk[cl.p];
+        for (;;) {
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((SS - 2) * G) : "memory");
+            issue();
+            compute(smem + (qc % STAGES) * STAGE_ELEMS);
+            ++qc;
+            if (++kc == nkc) {
+                epilogue(cl, true, true);
+                zero_acc();
+                tc += tstep;
+                if (tc >= tend) break;
+                cl = locate<BM, BN>(ka, tc);
+                nkc = ka->nk[cl.p];
+                kc = 0;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // dummies land before LDS is freed
+        return;
+    } else {
+    const TileLoc L0 = locate<BM, BN>(ka, t0);
+    const int nk = ka->nk[L0.p];
+
     if constexpr (RS) {
         // register-staged double buffer: stage it+1 waits in VGPRs while stage it computes
         static_assert(KG == 1 && STAGES == 2, "register staging: 2 LDS buffers, one k-group");
-        u32x4 ra[TileSrc<BM, NW>::NP], rb[TileSrc<BN, NW>::NP];
+        u32x4 ra[TileSrc<BM, NW, KB>::NP], rb[TileSrc<BN, NW, KB>::NP];
+        il = L0;
+        seg = 0;
+        seat(0, L0.slice * nk);
         auto load = [&]() {
-            if (seg_left == 0) {
-                ++seg;
-                const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[seg];
-                srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
-                srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
-                seg_left = S.K / kBK;
-            }
+            if (seg_left == 0) seat(++seg, 0);
             srcA.load(ra);
             srcB.load(rb);
             --seg_left;
@@ -230,10 +473,11 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         }
     } else {
     const int nks = (nk + KG - 1) / KG;                 // super-steps
+    // issue() re-issues a dummy past the tile's last k-step (keeps vmcnt arithmetic uniform)
     for (int ss = 0; ss < SS - 1; ++ss)
         if (ss < nks)
 #pragma unroll
-            for (int u = 0; u < KG; ++u) issue(ss * KG + u);
+            for (int u = 0; u < KG; ++u) issue();
 
     for (int it = 0; it < nks; ++it) {
         // RAW: this wave's pieces of super-stage it landed (SS-2 younger ones may still fly),
@@ -245,7 +489,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         if (it + SS - 1 < nks)
 #pragma unroll
-            for (int u = 0; u < KG; ++u) issue((it + SS - 1) * KG + u);
+            for (int u = 0; u < KG; ++u) issue();
         const int q = it * KG + grp;
         if (KG == 1 || q < nk) compute(smem + (q % STAGES) * STAGE_ELEMS);
     }
@@ -283,131 +527,42 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         }
         if (RM == 1 && grp != 0) return;
     }
-
-    // ---- epilogue ------------------------------------------------------------------------
-    // Called once per accumulator tile with compile-time (i, j), so every acc index stays a
-    // constant (a runtime-indexed accumulator array goes to scratch: guide rule 20).
-    const int mode = P.mode;
-    auto epi = [&](const f32x16& c, const int i, const int j) {
-        const int rb = m0 + wr * (BM / 2) + i * 32;           // first row of this 32-row block
-        {
-            const int n = n0 + wc * (BN / 2) + j * 32 + r32;
-            const bool ncol = n < P.N;
-            const int nn = ncol ? n : P.N - 1;
-            const float bias = P.bias ? P.bias[nn] : 0.f;
-            // The fp32 operands the mode reads (R or C; P_in) are fetched for all 16 rows in
-            // one batch before any use: padding rows read row 0 (a valid address) and drop the
-            // value.  A load guarded per element makes hipcc branch around it and wait for each
-            // one in turn (guide §5 "Projection GEMM", trap 4(c)): 16 dependent round trips.
-            const float* x1 = nullptr;                           // R (or C for ACCUM)
-            int64_t ld1 = 0;
-            if (mode == LDM_GEMM_RESID_SILU || mode == LDM_GEMM_ADD_R ||
-                (mode == LDM_GEMM_DGRAD_SILU && P.R)) {
-                x1 = P.R;
-                ld1 = P.ldr;
-            } else if (mode == LDM_GEMM_ACCUM) {
-                x1 = P.C;
-                ld1 = P.ldc;
-            }
-            const float* x2 = (mode == LDM_GEMM_DGRAD_SILU || mode == LDM_GEMM_LOSS) ? P.P_in
-                                                                                  : nullptr;
-            float v1[16], v2[16];
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
-                const int bb = (ncol && b < P.M_valid) ? b : 0;
-                v1[v] = x1 ? x1[(int64_t)bb * ld1 + nn] : 0.f;
-                v2[v] = x2 ? x2[(int64_t)bb * P.ldp_in + nn] : 0.f;
-            }
-            float out[16];
-            float lsum = 0.f;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
-                const bool live = ncol && b < P.M_valid;   // padding rows: nothing read / fp32 kept
-                const bool inb = ncol && b < P.M;
-                const int bb = live ? b : 0;
-                const int64_t ic = (int64_t)bb * P.ldc + nn;
-                const float r1 = live ? v1[v] : 0.f, r2 = live ? v2[v] : 0.f;
-                const float pre = c[v] + bias;
-                float o = pre;
-                switch (mode) {
-                    case LDM_GEMM_SILU:
-                        if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
-                        o = silu(pre);
-                        break;
-                    case LDM_GEMM_RESID_SILU:
-                        if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
-                        o = r1 + silu(pre);
-                        break;
-                    case LDM_GEMM_RELU: o = fmaxf(pre, 0.f); break;
-                    case LDM_GEMM_ACCUM: o = r1 + pre; break;
-                    case LDM_GEMM_ADD_R: o = r1 + pre; break;
-                    case LDM_GEMM_DGRAD_SILU: {
-                        const float dh = P.R ? r1 + pre : pre;
-                        if (P.C && live) P.C[ic] = dh;
-                        o = dh * silu_grad(r2);
-                        break;
-                    }
-                    case LDM_GEMM_LOSS: {
-                        const float d = pre - r2;
-                        lsum += live ? d * d : 0.f;
-                        o = P.scale * d;
-                        break;
-                    }
-                    default: break;
-                }
-                out[v] = live ? o : 0.f;
-                if (mode != LDM_GEMM_DGRAD_SILU && P.C && live) P.C[ic] = out[v];
-                if (P.Cb && inb)
-                    reinterpret_cast<unsigned short*>(P.Cb)[(int64_t)b * P.ldcb + nn] =
-                        (unsigned short)(pack2_bf16(out[v], 0.f) & 0xffffu);
-            }
-            if (P.CbT && ncol) {                 // [n][b]: 4 consecutive rows per 8-byte store
-                unsigned short* T = reinterpret_cast<unsigned short*>(P.CbT) + (int64_t)n * P.ldct;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int b = rb + 8 * g + 4 * h;
-                    if (b < P.M) {
-                        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                        const u32x2 w = {pack2_bf16(out[4 * g], out[4 * g + 1]),
-                                         pack2_bf16(out[4 * g + 2], out[4 * g + 3])};
-                        *reinterpret_cast<u32x2*>(T + b) = w;
-                    }
-                }
-            }
-            if (P.colsum) {                      // one partial per 32-row block and column
-                float cs = 0.f;
-#pragma unroll
-                for (int v = 0; v < 16; ++v) cs += out[v];
-                cs += __shfl_xor(cs, 32);
-                if (h == 0 && ncol && rb < P.M) P.colsum[(int64_t)(rb / 32) * P.N + n] = cs;
-            }
-            if (mode == LDM_GEMM_LOSS && P.loss_part) {
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
-                if (lane == 0 && rb < P.M)
-                    P.loss_part[(int64_t)(rb / 32) * ((P.N + 31) / 32) + (n0 + wc * (BN / 2) + j * 32) / 32] = lsum;
-            }
-        }
-    };
-    const bool do0 = KG == 1 || RM == 1 || grp == 0;
-    const bool do1 = KG == 1 || grp == 1;
-    if (do0) {
-        epi(acc[0][0], 0, 0);
-        if constexpr (RN > 1) epi(acc[0][RN - 1], 0, 1);
-    }
-    if constexpr (RM > 1) {
-        if (do1) {
-            epi(acc[RM - 1][0], 1, 0);
-            if constexpr (RN > 1) epi(acc[RM - 1][RN - 1], 1, 1);
-        }
+    epilogue(L0, KG == 1 || RM == 1 || grp == 0, KG == 1 || grp == 1);
     }
 }
 
-template <int BM, int BN, int STAGES, int KG = 1, bool RS = false>
-int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
-    auto* k = &gemm_bf16_kernel<BM, BN, STAGES, KG, RS>;
+// Split-K combine: C[m][n] = (ACCUM ? C[m][n] : 0) + sum_s ws[s][m][n] + bias[n], slices summed
+// in order 0..S-1 (deterministic).  4 consecutive columns per thread.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(ldm_gemm_prob_t P, int S) {
+    const int64_t n4 = (P.N + 3) / 4;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)P.M_valid * n4) return;
+    const int m = (int)(i / n4), c0 = (int)(i - (int64_t)m * n4) * 4;
+    const int64_t slab = (int64_t)P.M * P.N;
+    float v[4];
+    int nc = min(4, P.N - c0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = 0.f;
+    for (int s = 0; s < S; ++s) {
+        const float* src = P.ws + s * slab + (int64_t)m * P.N + c0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (c < nc) v[c] += src[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (c >= nc) break;
+        float o = v[c] + (P.bias ? P.bias[c0 + c] : 0.f);
+        float* dst = P.C + (int64_t)m * P.ldc + c0 + c;
+        if (P.mode == LDM_GEMM_ACCUM) o = *dst + o;
+        *dst = o;
+    }
+}
+
+template <int BM, int BN, int STAGES, int KG = 1, bool RS = false, bool PERSIST = false,
+          int KB = 64>
+int launch_gemm(const ldm_gemm_args_t& a, hipStream_t s) {
+    auto* k = &gemm_bf16_kernel<BM, BN, STAGES, KG, RS, PERSIST, KB>;
     GemmKArgs ka;
     memset(&ka, 0, sizeof(ka));
     ka.n_prob = a.n_prob;
@@ -419,24 +574,48 @@ int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
             ka.first[p] = acc;
             ka.tiles_m[p] = (P.M + BM - 1) / BM;
             ka.tiles_n[p] = (P.N + BN - 1) / BN;
-            for (int g = 0; g < P.n_seg; ++g) ka.nk[p] += P.seg[g].K / kBK;
-            acc += ka.tiles_m[p] * ka.tiles_n[p];
+            ka.ksplit[p] = P.k_split > 1 ? P.k_split : 1;
+            int nk = 0;
+            for (int g = 0; g < P.n_seg; ++g) nk += P.seg[g].K / KB;
+            ka.nk[p] = nk / ka.ksplit[p];
+            acc += ka.tiles_m[p] * ka.tiles_n[p] * ka.ksplit[p];
         } else {
             ka.first[p] = 0x7fffffff;
         }
     }
     ka.total = acc;
-    constexpr int lds = STAGES * (BM + BN) * kBK * 2;
-    static bool attr = false;
-    if (!attr) {
+    constexpr int lds = STAGES * (BM + BN) * KB * 2;
+    static int grid_cap = 0;                  // persistent: resident workgroups on the device
+    if (grid_cap == 0) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_gemm_bf16: hipFuncSetAttribute: %s",
                     hipGetErrorString(e));
-        attr = true;
+        int per_cu = 0, dev = 0, cus = 0;
+        if (PERSIST) {
+            LDM_REQUIRE(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                            &per_cu, reinterpret_cast<const void*>(k), 256 * KG, lds) ==
+                                hipSuccess &&
+                            hipGetDevice(&dev) == hipSuccess &&
+                            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                                                  dev) == hipSuccess &&
+                            per_cu >= 1,
+                        LDM_EINVAL, "ldm_gemm_bf16: persistent occupancy query failed");
+        }
+        grid_cap = PERSIST ? per_cu * cus : 1;
     }
-    hipLaunchKernelGGL(k, dim3(total), dim3(256 * KG), lds, s, ka);
-    return launch_status("ldm_gemm_bf16");
+    const int grid = PERSIST ? std::min(acc, grid_cap) : acc;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256 * KG), lds, s, ka);
+    LDM_TRY(launch_status("ldm_gemm_bf16"));
+    for (int p = 0; p < a.n_prob; ++p) {
+        const ldm_gemm_prob_t& P = a.prob[p];
+        if (ka.ksplit[p] <= 1 || P.M_valid == 0) continue;
+        const int64_t n = (int64_t)P.M_valid * ((P.N + 3) / 4);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           s, P, ka.ksplit[p]);
+        LDM_TRY(launch_status("ldm_gemm_bf16 (split-K combine)"));
+    }
+    return 0;
 }
 
 }  // namespace
@@ -444,7 +623,8 @@ int launch_gemm(const ldm_gemm_args_t& a, int total, hipStream_t s) {
 int gemm_tiles(const ldm_gemm_args_t& a, int bm, int bn) {
     int total = 0;
     for (int p = 0; p < a.n_prob; ++p)
-        total += ((a.prob[p].M + bm - 1) / bm) * ((a.prob[p].N + bn - 1) / bn);
+        total += ((a.prob[p].M + bm - 1) / bm) * ((a.prob[p].N + bn - 1) / bn) *
+                 (a.prob[p].k_split > 1 ? a.prob[p].k_split : 1);
     return total;
 }
 
@@ -462,19 +642,37 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
             LDM_REQUIRE(S.A && S.B && S.K > 0 && S.K % kBK == 0, LDM_EINVAL,
                         "ldm_gemm_bf16: problem %d seg %d: K=%d must be a positive multiple of 64",
                         p, s, S.K);
+            const int kmin = P.k_split > 1 && P.slice_a ? S.K / P.k_split : S.K;
             LDM_REQUIRE(LDM_ALIGNED(S.A, 16) && LDM_ALIGNED(S.B, 16) && S.lda % 8 == 0 &&
-                            S.ldb % 8 == 0 && S.lda >= S.K && S.ldb >= S.K,
+                            S.ldb % 8 == 0 && S.lda >= kmin && S.ldb >= kmin,
                         LDM_EALIGN, "ldm_gemm_bf16: problem %d seg %d: operands must be 16-B "
                         "aligned with row strides a multiple of 8 elements", p, s);
         }
-        LDM_REQUIRE(P.mode >= LDM_GEMM_STORE && P.mode <= LDM_GEMM_ADD_R, LDM_EINVAL,
+        LDM_REQUIRE(P.mode >= LDM_GEMM_STORE && P.mode <= LDM_GEMM_RELU_BWD, LDM_EINVAL,
                     "ldm_gemm_bf16: problem %d: mode %d", p, P.mode);
+        LDM_REQUIRE(P.mode != LDM_GEMM_RELU_BWD || P.Rb, LDM_EINVAL,
+                    "ldm_gemm_bf16: problem %d: RELU_BWD needs Rb", p);
+        if (P.k_split > 1 && P.slice_a) {
+            LDM_REQUIRE(P.slice_b && P.seg[0].lda >= P.seg[0].K / P.k_split &&
+                            P.seg[0].ldb >= P.seg[0].K / P.k_split,
+                        LDM_EINVAL, "ldm_gemm_bf16: problem %d: sliced split-K needs both "
+                        "slice strides and row strides >= K / k_split", p);
+        }
+        if (P.k_split > 1) {
+            LDM_REQUIRE(P.n_seg == 1 && P.seg[0].K % (2 * kBK * P.k_split) == 0 && P.ws && P.C &&
+                            (P.mode == LDM_GEMM_STORE || P.mode == LDM_GEMM_ACCUM) && !P.Cb &&
+                            !P.CbT && !P.colsum && !P.P,
+                        LDM_EINVAL, "ldm_gemm_bf16: problem %d: split-K %d needs one segment, "
+                        "K a multiple of 128 * k_split, ws, C, mode STORE/ACCUM and no other "
+                        "output", p, P.k_split);
+        }
         const bool needR = P.mode == LDM_GEMM_RESID_SILU || P.mode == LDM_GEMM_ADD_R;
         const bool needPin = P.mode == LDM_GEMM_DGRAD_SILU || P.mode == LDM_GEMM_LOSS;
         LDM_REQUIRE((!needR || P.R) && (!needPin || P.P_in) &&
                         (P.mode != LDM_GEMM_ACCUM || P.C),
                     LDM_EINVAL, "ldm_gemm_bf16: problem %d: mode %d operand missing", p, P.mode);
-        LDM_REQUIRE(!P.CbT || (LDM_ALIGNED(P.CbT, 8) && P.ldct % 4 == 0 && P.M % 4 == 0),
+        LDM_REQUIRE(!P.CbT || (LDM_ALIGNED(P.CbT, 8) && P.ldct % 4 == 0 && P.M % 4 == 0 &&
+                               P.ct_blk % 4 == 0 && P.ct_blk >= 0),
                     LDM_EALIGN, "ldm_gemm_bf16: problem %d: transposed output needs 8-B "
                     "alignment, ldct and M multiples of 4", p);
     }
@@ -490,24 +688,43 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     int tile = a.tile;
     if (tile == 0) {
         const int t64 = gemm_tiles(a, 64, 64);
-        tile = forced ? forced : t64 >= 2048 ? 3 : 4;
+        tile = forced ? forced : 4;
+        (void)t64;
+    }
+    if (tile >= 20) {                          // 128-deep stages: every K a multiple of 128
+        for (int p = 0; p < a.n_prob; ++p)
+            for (int g = 0; g < a.prob[p].n_seg; ++g)
+                LDM_REQUIRE(a.prob[p].seg[g].K % (2 * kBK) == 0, LDM_EINVAL,
+                            "ldm_gemm_bf16: tile %d needs every K a multiple of 128", tile);
     }
     switch (tile) {
-        case 1: return launch_gemm<64, 64, 4>(a, gemm_tiles(a, 64, 64), s);
-        case 2: return launch_gemm<128, 64, 4>(a, gemm_tiles(a, 128, 64), s);
-        case 3: return launch_gemm<128, 128, 3>(a, gemm_tiles(a, 128, 128), s);
-        case 4: return launch_gemm<64, 64, 3>(a, gemm_tiles(a, 64, 64), s);
-        case 5: return launch_gemm<64, 64, 6, 2>(a, gemm_tiles(a, 64, 64), s);
-        case 6: return launch_gemm<128, 128, 4, 2>(a, gemm_tiles(a, 128, 128), s);
-        case 7: return launch_gemm<128, 64, 6, 2>(a, gemm_tiles(a, 128, 64), s);
-        case 8: return launch_gemm<64, 64, 8>(a, gemm_tiles(a, 64, 64), s);
-        case 9: return launch_gemm<128, 64, 5>(a, gemm_tiles(a, 128, 64), s);
-        case 10: return launch_gemm<64, 64, 2>(a, gemm_tiles(a, 64, 64), s);
-        case 11: return launch_gemm<64, 64, 4, 2>(a, gemm_tiles(a, 64, 64), s);
-        case 12: return launch_gemm<128, 64, 3>(a, gemm_tiles(a, 128, 64), s);
-        case 13: return launch_gemm<64, 64, 2, 1, true>(a, gemm_tiles(a, 64, 64), s);
-        case 14: return launch_gemm<128, 128, 2, 1, true>(a, gemm_tiles(a, 128, 128), s);
-        case 15: return launch_gemm<128, 64, 2, 1, true>(a, gemm_tiles(a, 128, 64), s);
+        case 1: return launch_gemm<64, 64, 4>(a, s);
+        case 2: return launch_gemm<128, 64, 4>(a, s);
+        case 3: return launch_gemm<128, 128, 3>(a, s);
+        case 4: return launch_gemm<64, 64, 3>(a, s);
+        case 5: return launch_gemm<64, 64, 6, 2>(a, s);
+        case 6: return launch_gemm<128, 128, 4, 2>(a, s);
+        case 7: return launch_gemm<128, 64, 6, 2>(a, s);
+        case 8: return launch_gemm<64, 64, 8>(a, s);
+        case 9: return launch_gemm<128, 64, 5>(a, s);
+        case 10: return launch_gemm<64, 64, 2>(a, s);
+        case 11: return launch_gemm<64, 64, 4, 2>(a, s);
+        case 12: return launch_gemm<128, 64, 3>(a, s);
+        case 13: return launch_gemm<64, 64, 2, 1, true>(a, s);
+        case 14: return launch_gemm<128, 128, 2, 1, true>(a, s);
+        case 15: return launch_gemm<128, 64, 2, 1, true>(a, s);
+        case 16: return launch_gemm<128, 128, 4, 1, false, true>(a, s);
+        case 17: return launch_gemm<128, 128, 2, 1, false, true>(a, s);
+        case 18: return launch_gemm<64, 64, 3, 1, false, true>(a, s);
+        case 20: return launch_gemm<64, 64, 2, 1, false, false, 128>(a, s);
+        case 21: return launch_gemm<64, 64, 3, 1, false, false, 128>(a, s);
+        case 22: return launch_gemm<128, 64, 2, 1, false, false, 128>(a, s);
+        case 23: return launch_gemm<128, 128, 2, 1, false, false, 128>(a, s);
+        case 24: return launch_gemm<64, 64, 4, 2, false, false, 128>(a, s);
+        case 25: return launch_gemm<64, 64, 2, 1, false, true, 128>(a, s);
+        case 26: return launch_gemm<128, 128, 2, 1, false, true, 128>(a, s);
+        case 27: return launch_gemm<64, 64, 2, 1, true, false, 128>(a, s);
+        case 28: return launch_gemm<128, 64, 2, 1, true, false, 128>(a, s);
         default: break;
     }
     set_error("ldm_gemm_bf16: tile %d", tile);

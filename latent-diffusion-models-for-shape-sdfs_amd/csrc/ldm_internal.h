@@ -19,6 +19,11 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
         }                                    \
     } while (0)
 
+#define LDM_TRY(x)                       \
+    do {                                 \
+        if (int e_ = (x)) return e_;     \
+    } while (0)
+
 #define LDM_ALIGNED(p, a) ((((uintptr_t)(p)) & ((a) - 1)) == 0)
 
 inline int launch_status(const char* what) {

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("LDM_SDF_LIB", LIB_PATH)
 HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                             "..", "..", "include", "ldm_sdf.h"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER = 0, 1
@@ -88,7 +88,7 @@ class LinearArgs(C.Structure):
 
 GEMM_MAX_SEGS, GEMM_MAX_PROBS = 8, 4
 (GEMM_STORE, GEMM_SILU, GEMM_RESID_SILU, GEMM_RELU, GEMM_ACCUM, GEMM_DGRAD_SILU, GEMM_LOSS,
- GEMM_ADD_R) = range(8)
+ GEMM_ADD_R, GEMM_RELU_BWD) = range(9)
 
 
 class GemmSeg(C.Structure):
@@ -102,7 +102,9 @@ class GemmProb(C.Structure):
                 ("bias", _vp), ("R", _vp), ("ldr", C.c_int64), ("P_in", _vp),
                 ("ldp_in", C.c_int64), ("C", _vp), ("ldc", C.c_int64), ("P", _vp),
                 ("ldp", C.c_int64), ("Cb", _vp), ("ldcb", C.c_int64), ("CbT", _vp),
-                ("ldct", C.c_int64), ("colsum", _vp), ("loss_part", _vp)]
+                ("ldct", C.c_int64), ("colsum", _vp), ("loss_part", _vp),
+                ("k_split", C.c_int32), ("ct_blk", C.c_int32), ("ws", _vp), ("Rb", _vp),
+                ("ldrb", C.c_int64), ("slice_a", C.c_int64), ("slice_b", C.c_int64)]
 
 
 class GemmArgs(C.Structure):

@@ -134,6 +134,9 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
     if tuple(z.shape) != (S, L) or tuple(xyz.shape) != (S, P, 3):
         raise capi.LdmError(f"autodecoder_train_step: z{tuple(z.shape)} xyz{tuple(xyz.shape)} "
                             f"sdf{tuple(sdf.shape)}")
+    if dtype == "bf16":
+        return _train_step_gemm_bf16(masters, z, xyz, sdf, L=L, H=H, skip=skip, delta=delta,
+                                     reg_lambda=reg_lambda, epoch=epoch, grads=grads)
     dev = z.device
     cp = capi.COMPUTE_CODES[dtype]
     wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
@@ -204,6 +207,213 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
     if grads is None:
         grads = {k: torch.empty_like(v) for k, v in masters.items()}
     master_grads(gw, L, skip, hs, grads)
+    return loss, grads, gz
+
+
+_KQ = 128          # row padding of the sample axis (the K of the weight-gradient products)
+_KSEG = 64         # column padding of [z || xyz] (a GEMM K segment)
+
+
+def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda, epoch,
+                          grads):
+    """bf16 matrix-core step on ``ldm_gemm_bf16`` (include/ldm_sdf.h).
+
+    Every activation is kept once in bf16, in both layouts: ``h_l`` [Np, w] (the A operand of
+    the next forward product and of the G W products' ReLU mask) and ``h_l^T`` [w, Np] (the B
+    operand of the weight gradients, whose sum runs over the samples).  The epilogues write
+    them (``Cb`` / ``CbT``), the ReLU backward rides in the G W products (``relu_bwd`` on the
+    saved bf16 post-activation), the bias gradients are the epilogues' 32-row column sums, and
+    the weight gradients are split-K products over the sample axis.  The latent gradient needs
+    no [N, L] product: per shape, ``sum_p g4 W4z + g0 W0`` = (per-shape column sums of g4 and
+    g0) x the latent columns, a [S, H] x [H, L] product in fp32.  Numerics: operands rounded to
+    bf16 (RNE), fp32 accumulation -- as the ``ldm_linear`` bf16 path."""
+    dev = z.device
+    S, P = sdf.shape
+    N = S * P
+    Np = -(-N // _KQ) * _KQ
+    hs = masters[f"W{skip - 1}"].shape[0]
+    hsp = -(-hs // 64) * 64                      # skip width padded to a GEMM K segment
+    zw = -(-(L + 3) // _KSEG) * _KSEG
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    f32 = dict(device=dev, dtype=torch.float32)
+
+    # ---- working weights (bf16, padded) and their transposes for the G W products
+    W = {}
+    W0 = torch.zeros(H, zw, **bf)
+    W0[:, :L + 3] = masters["W0"]
+    W["W0"] = W0
+    for l in range(1, 8):
+        if l == skip - 1:
+            Wp = torch.zeros(hsp, H, **bf)
+            Wp[:hs] = masters[f"W{l}"]
+            W[f"W{l}"] = Wp
+        elif l == skip:
+            Ws = masters[f"W{l}"]
+            Wh = torch.zeros(H, hsp, **bf)
+            Wh[:, :hs] = Ws[:, :hs]
+            Wz = torch.zeros(H, zw, **bf)
+            Wz[:, :L + 3] = Ws[:, hs:]
+            W["W4h"], W["W4z"] = Wh, Wz
+        else:
+            W[f"W{l}"] = masters[f"W{l}"].to(torch.bfloat16)
+    WT = {k: v.t().contiguous() for k, v in W.items() if k != "W0"}
+    bias = {f"b{l}": masters[f"b{l}"].contiguous() for l in range(9)}
+    bp = torch.zeros(hsp, **f32)
+    bp[:hs] = masters[f"b{skip - 1}"]
+    bias[f"b{skip - 1}"] = bp
+    # the 512 -> 1 layer as a K = 64 product for its backward (g8 in column 0, zeros beside)
+    w8 = masters["W8"].reshape(-1)
+    W8T = torch.zeros(H, 64, **bf)
+    W8T[:, 0] = w8
+    W8 = w8.to(torch.bfloat16).reshape(1, H).contiguous()
+
+    # ---- inputs: Zx = [z_s || xyz || 0] per sample, rows >= N zero, both layouts.  The
+    # sample-axis (transposed) operands are k-BLOCKED, [nblk][width][KT]: a weight-gradient
+    # slice is one block, so the rows it streams lie KT * 2 bytes apart inside one block
+    # instead of 2 MB apart (one memory page per row: measured 9 us per k-step, TLB-bound).
+    KT = next(kt for kt in (8192, 4096, 2048, 1024, 512, 256, 128) if Np % kt == 0)
+    nblk = Np // KT
+    owner = torch.arange(S, device=dev).repeat_interleave(P)
+    owner_pad = torch.full((Np,), S, device=dev, dtype=torch.long)
+    owner_pad[:N] = owner
+    Zx = torch.zeros(Np, zw, **bf)
+    Zx[:N, :L] = z[owner]
+    Zx[:N, L:L + 3] = xyz.reshape(N, 3)
+    ZxT = torch.zeros(nblk, zw, KT, **bf)
+    zT = torch.zeros(L, S + 1, **bf)              # column S: the padding rows' zero code
+    zT[:, :S] = z.t()
+    ZxT.permute(1, 0, 2)[:L] = zT[:, owner_pad.view(nblk, KT)]
+    xyz_pad = torch.zeros(Np, 3, **f32)
+    xyz_pad[:N] = xyz.reshape(N, 3)
+    ZxT.permute(1, 0, 2)[L:L + 3] = xyz_pad.t().reshape(3, nblk, KT).to(torch.bfloat16)
+
+    # ---- forward: h_l = ReLU(...) in bf16, both layouts (rows >= N written as zeros)
+    h, hT = [], []
+    x = Zx
+    for l in range(8):
+        width = hsp if l == skip - 1 else H
+        y = torch.empty(Np, width, **bf)
+        yT = torch.empty(nblk, width, KT, **bf)
+        segs = ([(x, W["W4h"]), (Zx, W["W4z"])] if l == skip else [(x, W[f"W{l}"])])
+        ops.gemm([ops.gemm_problem(segs, Np, width, mode="relu", M_valid=N, bias=bias[f"b{l}"],
+                                   Cb=y, CbT=yT, ct_blk=KT)])
+        h.append(y)
+        hT.append(yT)
+        x = y
+    pre = torch.empty(Np, 1, **f32)
+    ops.gemm([ops.gemm_problem([(x, W8)], Np, 1, M_valid=N, bias=bias["b8"], C=pre)])
+    loss, g8 = ops.sdf_l1_loss(pre[:N].reshape(N, 1), sdf.reshape(N, 1).contiguous(), delta,
+                               1.0 / N)
+
+    # ---- backward
+    gw = {}
+    gb = {}
+    ws_cache = {}
+
+    def ws_for(n):
+        t = ws_cache.get(n)
+        if t is None:
+            t = ws_cache[n] = torch.empty(n, **f32)
+        return t
+
+    def wgrad(gT, xT, M_, N_, out):
+        """out [M_, N_] fp32 = sum over the samples of gT x xT^T; gT [nblk, M_, KT] and
+        xT [nblk, N_, KT] blocked: split-K with one slice per block."""
+        if nblk == 1:
+            return ops.gemm_problem([(gT[0], xT[0])], M_, N_, C=out)
+        return ops.gemm_problem([(gT[0], xT[0])], M_, N_, C=out, k_split=nblk,
+                                ws=ws_for(nblk * M_ * N_),
+                                slices=(gT.shape[1] * KT, xT.shape[1] * KT))
+
+    # layer 8: dW8 = g8^T h7, db8 = sum g8; g7 = (g8 w8) * [h7 > 0]
+    g8b = torch.zeros(Np, 64, **bf)
+    g8b[:N, 0] = g8.reshape(N)
+    g8row = g8b[:, 0].contiguous().reshape(nblk, 1, KT)      # blocked [nblk][1][KT]
+    gw["W8"] = torch.empty(1, H, **f32)
+    gb["b8"] = torch.empty(1, **f32)
+    ops.colsum(g8.reshape(N, 1), gb["b8"])
+    nrow32 = -(-Np // 32)
+    g_cur = torch.empty(Np, H, **bf)
+    gT_cur = torch.empty(nblk, H, KT, **bf)
+    cs = torch.empty(nrow32, H, **f32)
+    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"]),
+              ops.gemm_problem([(g8b, W8T)], Np, H, mode="relu_bwd", M_valid=N, Rb=h[7],
+                               Cb=g_cur, CbT=gT_cur, colsum=cs, ct_blk=KT)])
+    colsums = {7: cs}
+    gcs = {}                                       # g_l per 32-row block sums (bias / latent)
+    Gs = {}                                        # per-shape column sums of g_skip and g_0
+    onehot = None
+    if P % 32:                                     # 32-row blocks straddle shapes: a one-hot
+        sid = torch.arange(S, device=dev)[:, None, None]   # product sums each shape's rows
+        onehot = (owner_pad.view(1, nblk, KT) == sid).to(torch.bfloat16).permute(1, 0, 2)
+        onehot = onehot.contiguous()               # blocked [nblk][S][KT]
+    for l in range(7, -1, -1):
+        # g_cur = dL/d pre_l (bf16, both layouts); its column sums are colsums[l]
+        gcs[l] = colsums[l]
+        wout = hsp if l == skip - 1 else H
+        if l == skip:
+            gw["W4h"] = torch.empty(H, hsp, **f32)
+            gw["W4z"] = torch.empty(H, zw, **f32)
+            probs = [wgrad(gT_cur, hT[l - 1], H, hsp, gw["W4h"]),
+                     wgrad(gT_cur, ZxT, H, zw, gw["W4z"])]
+        elif l == 0:
+            gw["W0"] = torch.empty(H, zw, **f32)
+            probs = [wgrad(gT_cur, ZxT, H, zw, gw["W0"])]
+        else:
+            win = h[l - 1].shape[1]
+            gw[f"W{l}"] = torch.empty(wout, win, **f32)
+            probs = [wgrad(gT_cur, hT[l - 1], wout, win, gw[f"W{l}"])]
+        if onehot is not None and l in (skip, 0):
+            Gs[l] = torch.empty(S, H, **f32)
+            probs.append(wgrad(onehot, gT_cur, S, H, Gs[l]))
+        if l > 0:
+            win = h[l - 1].shape[1]
+            WdT = WT["W4h"] if l == skip else WT[f"W{l}"]          # [win, wout]
+            g_nxt = torch.empty(Np, win, **bf)
+            gT_nxt = torch.empty(nblk, win, KT, **bf)
+            cs = torch.empty(nrow32, win, **f32)
+            probs.append(ops.gemm_problem([(g_cur, WdT)], Np, win, mode="relu_bwd", M_valid=N,
+                                          Rb=h[l - 1], Cb=g_nxt, CbT=gT_nxt, colsum=cs,
+                                          ct_blk=KT))
+            colsums[l - 1] = cs
+        ops.gemm(probs)
+        if l > 0:
+            g_prev_keep = (g_cur, gT_cur)            # noqa: F841 (alive until the launch is queued)
+            g_cur, gT_cur = g_nxt, gT_nxt
+    for l in range(8):
+        width = gcs[l].shape[1]
+        gb[f"b{l}"] = torch.empty(width, **f32)
+        ops.colsum(gcs[l], gb[f"b{l}"])
+
+    # ---- latent gradient: per shape sum_p (g4 W4z + g0 W0)[:, :L]
+    if onehot is None:                             # shape s = 32-row blocks [s P/32, (s+1) P/32)
+        for l in (skip, 0):
+            Gs[l] = torch.empty(S, H, **f32)
+            ops.colsum_segments(gcs[l][:N // 32].contiguous(), S, Gs[l])
+    G4, G0 = Gs[skip], Gs[0]
+    gz = torch.empty(S, L, **f32)
+    Wm = masters[f"W{skip}"]
+    ops.linear(G4, Wm[:, hs:hs + L].t(), gz, compute=capi.COMPUTE_FP32)
+    ops.linear(G0, masters["W0"][:, :L].t(), gz, epi=capi.EPI_ACCUM, compute=capi.COMPUTE_FP32)
+    coef = reg_lambda * min(1.0, epoch / 100.0) / S
+    if coef != 0.0:
+        ops.latent_l2_reg(z, coef, loss, gz)
+
+    if grads is None:
+        grads = {k: torch.empty_like(v) for k, v in masters.items()}
+    grads["W0"].copy_(gw["W0"][:, :L + 3])
+    for l in range(1, 9):
+        if l == skip - 1:
+            grads[f"W{l}"].copy_(gw[f"W{l}"][:hs])
+            grads[f"b{l}"].copy_(gb[f"b{l}"][:hs])
+            continue
+        if l == skip:
+            grads[f"W{l}"][:, :hs].copy_(gw["W4h"][:, :hs])
+            grads[f"W{l}"][:, hs:].copy_(gw["W4z"][:, :L + 3])
+        else:
+            grads[f"W{l}"].copy_(gw[f"W{l}"].reshape(grads[f"W{l}"].shape))
+        grads[f"b{l}"].copy_(gb[f"b{l}"].reshape(grads[f"b{l}"].shape))
+    grads["b0"].copy_(gb["b0"])
     return loss, grads, gz
 
 

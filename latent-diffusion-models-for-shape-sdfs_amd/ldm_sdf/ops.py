@@ -359,7 +359,8 @@ def latent_l2_reg(z: torch.Tensor, coef: float, loss_io: torch.Tensor,
 _GEMM_MODES = {"store": capi.GEMM_STORE, "silu": capi.GEMM_SILU,
                "resid_silu": capi.GEMM_RESID_SILU, "relu": capi.GEMM_RELU,
                "accum": capi.GEMM_ACCUM, "dgrad_silu": capi.GEMM_DGRAD_SILU,
-               "loss": capi.GEMM_LOSS, "add_r": capi.GEMM_ADD_R}
+               "loss": capi.GEMM_LOSS, "add_r": capi.GEMM_ADD_R,
+               "relu_bwd": capi.GEMM_RELU_BWD}
 
 
 def _rowmajor(t: Optional[torch.Tensor], what: str, dtype=None) -> int:
@@ -375,9 +376,15 @@ def _rowmajor(t: Optional[torch.Tensor], what: str, dtype=None) -> int:
 
 def gemm_problem(segs, M: int, N: int, *, mode: str = "store", M_valid: Optional[int] = None,
                  bias=None, R=None, P_in=None, C=None, P=None, Cb=None, CbT=None, colsum=None,
-                 loss_part=None, scale: float = 1.0) -> capi.GemmProb:
+                 loss_part=None, scale: float = 1.0, Rb=None, k_split: int = 1,
+                 ws=None, ct_blk: int = 0, slices=None) -> capi.GemmProb:
     """One problem of ``ldm_gemm_bf16`` (include/ldm_sdf.h): ``segs`` = [(A [M,K] bf16,
-    B [N,K] bf16), ...] as row-contiguous views; outputs / operands as documented there."""
+    B [N,K] bf16), ...] as row-contiguous views; outputs / operands as documented there.
+    ``Rb``: bf16 [M,N] post-activation of mode "relu_bwd"; ``k_split`` > 1 with ``ws``
+    (fp32, >= k_split * M * N elements): split-K into that workspace.  ``ct_blk`` > 0: CbT
+    is written blocked, [ceil(M/ct_blk), N, ct_blk].  ``slices`` = (slice_a, slice_b): split-K
+    over blocked operands -- ``segs`` holds ONE block of each ([M, kb] / [N, kb] views) and
+    slice s reads the block s * slice_a (s * slice_b) elements further; K = k_split * kb."""
     pr = capi.GemmProb()
     pr.M, pr.N = int(M), int(N)
     pr.M_valid = int(M if M_valid is None else M_valid)
@@ -390,18 +397,37 @@ def gemm_problem(segs, M: int, N: int, *, mode: str = "store", M_valid: Optional
         if A.shape[0] < M or B.shape[0] < N or A.shape[1] != B.shape[1]:
             raise capi.LdmError(f"gemm seg {i}: A{tuple(A.shape)} B{tuple(B.shape)} vs M={M} N={N}")
         g = pr.seg[i]
-        g.A, g.B, g.lda, g.ldb, g.K = A.data_ptr(), B.data_ptr(), la, lb, A.shape[1]
+        g.A, g.B, g.lda, g.ldb = A.data_ptr(), B.data_ptr(), la, lb
+        g.K = A.shape[1] * (k_split if slices else 1)
     pr.mode = _GEMM_MODES[mode]
     pr.scale = float(scale)
     for name, t, dt in (("R", R, torch.float32), ("P_in", P_in, torch.float32),
                         ("C", C, torch.float32), ("P", P, torch.float32),
                         ("Cb", Cb, torch.bfloat16), ("CbT", CbT, torch.bfloat16)):
+        if name == "CbT" and ct_blk and t is not None:   # blocked [nblk, N, ct_blk]
+            if (t.dtype != torch.bfloat16 or not t.is_contiguous()
+                    or t.numel() < -(-M // ct_blk) * N * ct_blk):
+                raise capi.LdmError("gemm: blocked CbT must be contiguous bf16 "
+                                    "[ceil(M/ct_blk), N, ct_blk]")
+            pr.CbT, pr.ldct = t.data_ptr(), 0
+            continue
         ld = _rowmajor(t, name, dt)
         setattr(pr, name, capi.ptr(t))
         if t is not None:
             setattr(pr, {"R": "ldr", "P_in": "ldp_in", "C": "ldc", "P": "ldp", "Cb": "ldcb",
                          "CbT": "ldct"}[name], ld)
-    for name, t in (("bias", bias), ("colsum", colsum), ("loss_part", loss_part)):
+    if Rb is not None:
+        pr.ldrb = _rowmajor(Rb, "Rb", torch.bfloat16)
+        pr.Rb = Rb.data_ptr()
+    pr.k_split = int(k_split)
+    pr.ct_blk = int(ct_blk)
+    if slices:
+        pr.slice_a, pr.slice_b = int(slices[0]), int(slices[1])
+    if k_split > 1:
+        if ws is None or ws.dtype != torch.float32 or ws.numel() < k_split * M * N:
+            raise capi.LdmError(f"gemm: split-K {k_split} needs an fp32 ws of "
+                                f"{k_split * M * N} elements")
+    for name, t in (("bias", bias), ("colsum", colsum), ("loss_part", loss_part), ("ws", ws)):
         if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
             raise capi.LdmError(f"gemm: {name} must be contiguous fp32")
         setattr(pr, name, capi.ptr(t))

@@ -73,6 +73,17 @@ for (M, N, K) in SHAPES:
     res["max_err"] = float((C - ref).abs().max())
     us = timed(lambda: torch.mm(A, B.T))
     res["torch_mm_us"], res["torch_mm_tflops"] = round(us, 2), round(fl / us / 1e6, 1)
+    if os.environ.get("GRAPH_REF"):      # hipBLASLt device time: torch.mm replayed from a graph
+        Cm = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        n_in = 20 if reps > 5 else 2
+        torch.mm(A, B.T, out=Cm)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(n_in):
+                torch.mm(A, B.T, out=Cm)
+        us = timed(lambda: gr.replay()) / n_in
+        res["torch_mm_graph_us"], res["torch_mm_graph_tflops"] = round(us, 2), round(fl / us / 1e6, 1)
     if M * N * K < 1 << 34:
         Af = A.float()
         us = timed(lambda: ops.linear(Af, B, C, compute=capi.COMPUTE_BF16))

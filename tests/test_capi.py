@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_error_path_without_gpu():
     from ldm_sdf import _capi as capi
     lib = capi.load()
-    assert lib.ldm_abi_version() == 2
+    assert lib.ldm_abi_version() == 3
     # argument validation runs before any device work
     assert lib.ldm_grid_coords(0, 0, 0, 0.0, 0.0, None, None) == -22
     assert b"bad grid slab" in lib.ldm_last_error()
@@ -58,6 +58,8 @@ def test_struct_layouts_match_c():
       printf("%zu %zu %zu %zu %zu\n", sizeof(ldm_gemm_seg_t), sizeof(ldm_gemm_prob_t),
              sizeof(ldm_gemm_args_t), offsetof(ldm_gemm_prob_t, bias),
              offsetof(ldm_gemm_prob_t, loss_part));
+      printf("%zu %zu %zu\n", offsetof(ldm_gemm_prob_t, ws), offsetof(ldm_gemm_prob_t, ldrb),
+             offsetof(ldm_gemm_prob_t, slice_b));
       return 0; }
     '''
     tmp = "/tmp/ldm_layout_check"
@@ -81,3 +83,5 @@ def test_struct_layouts_match_c():
     assert sizes[12:17] == [ctypes.sizeof(capi.GemmSeg), ctypes.sizeof(capi.GemmProb),
                             ctypes.sizeof(capi.GemmArgs), capi.GemmProb.bias.offset,
                             capi.GemmProb.loss_part.offset]
+    assert sizes[17:20] == [capi.GemmProb.ws.offset, capi.GemmProb.ldrb.offset,
+                            capi.GemmProb.slice_b.offset]

@@ -38,13 +38,17 @@ def _bf_close(got, want, tol):
     return bool(((got.double() - w).abs() <= tol + w.abs() * 2 ** -8).all())
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 16, 17, 18, 20, 21, 22, 23, 24, 25, 26])
 @pytest.mark.parametrize("M,N,Ks", [(1000, 1024, (2048,)), (64, 64, (64,)), (130, 70, (128, 64)),
                                     (1024, 256, (1024,)), (96, 2048, (256, 128, 64, 512))])
 def test_gemm_store_segments_tiles(dev, tile, M, N, Ks):
-    from ldm_sdf import ops
+    from ldm_sdf import ops, LdmError
     g = torch.Generator().manual_seed(M * 7 + N + len(Ks) * 13 + tile)
     segs = [(_rand((M, K), g, dev).bfloat16(), _rand((N, K), g, dev).bfloat16()) for K in Ks]
+    if tile >= 20 and any(K % 128 for K in Ks):      # 128-deep stages: K must fit them
+        with pytest.raises(LdmError):
+            ops.gemm([ops.gemm_problem(segs, M, N, C=torch.zeros(M, N, device=dev))], tile=tile)
+        return
     bias = _rand((N,), g, dev)
     Mp = (M + 3) // 4 * 4
     C = torch.full((M, N), 7.0, device=dev)
@@ -71,18 +75,22 @@ def test_gemm_store_segments_tiles(dev, tile, M, N, Ks):
     assert (cs.double() - csw).abs().max() < tol * 32
 
 
+@pytest.mark.parametrize("tile", [0, 16, 21])
 @pytest.mark.parametrize("mode", ["silu", "resid_silu", "relu", "accum", "add_r", "dgrad_silu",
-                                  "loss"])
-def test_gemm_epilogues(dev, mode):
+                                  "loss", "relu_bwd"])
+def test_gemm_epilogues(dev, mode, tile):
     from ldm_sdf import ops
     g = torch.Generator().manual_seed(hash(mode) % 1000)
-    M, N, K = 200, 192, 320
+    M, N, K = 200, 192, 384
     Mv = 190
     A = _rand((M, K), g, dev).bfloat16()
     B = _rand((N, K), g, dev, 0.1).bfloat16()
     bias = _rand((N,), g, dev)
     R = _rand((M, N), g, dev)
     Pin = _rand((M, N), g, dev)
+    Rb = _rand((M, N), g, dev).bfloat16()
+    Rb[::7] = 0.0                              # +0 and -0 both mask the gradient
+    Rb[3::11] = -0.0
     C0 = _rand((M, N), g, dev)
     C = C0.clone()
     P = torch.zeros(M, N, device=dev)
@@ -100,7 +108,9 @@ def test_gemm_epilogues(dev, mode):
     if mode == "loss":
         kw["loss_part"] = lp
         kw["scale"] = 0.37
-    ops.gemm([ops.gemm_problem([(A, B)], M, N, mode=mode, **kw)])
+    if mode == "relu_bwd":
+        kw["Rb"] = Rb
+    ops.gemm([ops.gemm_problem([(A, B)], M, N, mode=mode, **kw)], tile=tile)
     torch.cuda.synchronize()
     pre = A.double() @ B.double().T + bias.double()
     sig = torch.sigmoid
@@ -120,6 +130,8 @@ def test_gemm_epilogues(dev, mode):
         dh = Rd + pre
         s = sig(Pd)
         out = dh * s * (1 + Pd * (1 - s))
+    elif mode == "relu_bwd":
+        out = torch.where(Rb.double() > 0, pre, torch.zeros_like(pre))
     else:
         d = pre - Pd
         out = 0.37 * d
@@ -175,3 +187,98 @@ def test_gemm_rejects_bad_args(dev):
     with pytest.raises(LdmError):                     # resid_silu without R
         ops.gemm([ops.gemm_problem([(A, A)], 64, 64, mode="resid_silu",
                                    C=torch.zeros(64, 64, device=dev))])
+
+
+@pytest.mark.parametrize("tile", [0, 4, 16, 20, 26])
+@pytest.mark.parametrize("ks,mode", [(2, "store"), (8, "store"), (4, "accum")])
+def test_gemm_split_k(dev, tile, ks, mode):
+    """Split-K (C19's weight gradients G^T X over ~1M samples): slices write raw partials to
+    ws, a second kernel sums them in slice order and applies bias / ACCUM.  Ragged M / N and an
+    M_valid row mask; the result is deterministic (two launches give the same bits)."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(ks * 31 + tile)
+    M, N, K, Mv = 330, 200, 128 * ks * 3, 321
+    A = _rand((M, K), g, dev).bfloat16()
+    B = _rand((N, K), g, dev).bfloat16()
+    bias = _rand((N,), g, dev)
+    C0 = _rand((M, N), g, dev)
+    ws = torch.full((ks * M * N,), float("nan"), device=dev)
+    outs = []
+    for _ in range(2):
+        C = C0.clone()
+        ops.gemm([ops.gemm_problem([(A, B)], M, N, mode=mode, M_valid=Mv, bias=bias, C=C,
+                                   k_split=ks, ws=ws)], tile=tile)
+        outs.append(C)
+    torch.cuda.synchronize()
+    want = A.double() @ B.double().T + bias.double()
+    if mode == "accum":
+        want = want + C0.double()
+    C = outs[0]
+    assert (C[:Mv].double() - want[:Mv]).abs().max() < 2e-6 * math.sqrt(K) * 4 * 2
+    assert torch.equal(C[Mv:], C0[Mv:])                  # padding rows untouched
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_gemm_persistent_many_tiles(dev):
+    """Persistent tiles (16 / 17 / 18) when the launch has several tiles per resident workgroup:
+    K segments of different lengths, two problems with different k-step counts, a ragged M, the
+    RELU_BWD mask and both bf16 layouts -- equal to the one-tile-per-workgroup kernel bit for
+    bit (same k order, same epilogue)."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(5)
+    M1, N1, M2, N2 = 40000, 384, 9000, 256
+    A1 = _rand((M1, 128), g, dev).bfloat16()
+    A1b = _rand((M1, 64), g, dev).bfloat16()
+    B1 = _rand((N1, 128), g, dev, 0.1).bfloat16()
+    B1b = _rand((N1, 64), g, dev, 0.1).bfloat16()
+    A2 = _rand((M2, 512), g, dev).bfloat16()
+    B2 = _rand((N2, 512), g, dev, 0.1).bfloat16()
+    Rb = _rand((M2, N2), g, dev).bfloat16()
+    bias = _rand((N1,), g, dev)
+    res = {}
+    for tile in (4, 16, 17, 18):
+        C1 = torch.zeros(M1, N1, device=dev)
+        Cb1 = torch.zeros(M1, N1, device=dev, dtype=torch.bfloat16)
+        C2 = torch.zeros(M2, N2, device=dev)
+        CbT2 = torch.zeros(N2, M2, device=dev, dtype=torch.bfloat16)
+        ops.gemm([ops.gemm_problem([(A1, B1), (A1b, B1b)], M1, N1, mode="relu", bias=bias,
+                                   C=C1, Cb=Cb1),
+                  ops.gemm_problem([(A2, B2)], M2, N2, mode="relu_bwd", Rb=Rb, C=C2, CbT=CbT2,
+                                   M_valid=M2 - 37)], tile=tile)
+        torch.cuda.synchronize()
+        res[tile] = (C1, Cb1, C2, CbT2)
+    want1 = (A1.double() @ B1.double().T + A1b.double() @ B1b.double().T + bias.double()).clamp_min(0)
+    assert (res[16][0].double() - want1).abs().max() < 2e-6 * math.sqrt(192) * 4
+    for tile in (16, 17, 18):
+        for got, ref in zip(res[tile], res[4]):
+            assert torch.equal(got, ref), tile
+
+
+def test_gemm_blocked_transpose_and_sliced_split_k(dev):
+    """C19's sample-axis operands: a forward writes CbT k-blocked ([M/KT][N][KT], ct_blk),
+    and a weight-gradient product sums over the blocks as split-K slices (slices = block
+    strides).  Equal to the plain transposed layout / the fp64 product of the same bf16 values."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(11)
+    M, N, K, KT, Mv = 2048, 96, 128, 256, 2000
+    A = _rand((M, K), g, dev).bfloat16()
+    B = _rand((N, K), g, dev).bfloat16()
+    plain = torch.zeros(N, M, device=dev, dtype=torch.bfloat16)
+    blocked = torch.full((M // KT, N, KT), 3.0, device=dev, dtype=torch.bfloat16)
+    ops.gemm([ops.gemm_problem([(A, B)], M, N, mode="relu", M_valid=Mv, CbT=plain)])
+    ops.gemm([ops.gemm_problem([(A, B)], M, N, mode="relu", M_valid=Mv, CbT=blocked,
+                               ct_blk=KT)])
+    torch.cuda.synchronize()
+    assert torch.equal(blocked.permute(1, 0, 2).reshape(N, M), plain)
+    # weight gradient: G^T [N2][M] (blocked) x X^T [N][M] (blocked) over the M samples
+    N2 = 72
+    G = _rand((N2, M), g, dev).bfloat16()
+    Gb = G.view(N2, M // KT, KT).permute(1, 0, 2).contiguous()
+    out = torch.zeros(N2, N, device=dev)
+    ks = M // KT
+    ws = torch.empty(ks * N2 * N, device=dev)
+    ops.gemm([ops.gemm_problem([(Gb[0], blocked[0])], N2, N, C=out, k_split=ks, ws=ws,
+                               slices=(N2 * KT, N * KT))])
+    torch.cuda.synchronize()
+    want = G.double() @ plain.double().T
+    assert (out.double() - want).abs().max() < 2e-6 * math.sqrt(M) * 4 * 4
