@@ -27,6 +27,7 @@
 #include "ddpm_common.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <stdlib.h>
 #include <string.h>
 
@@ -272,129 +273,180 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     // ---- epilogue ------------------------------------------------------------------------
     // Called once per accumulator tile with compile-time (i, j), so every acc index stays a
     // constant (a runtime-indexed accumulator array goes to scratch: guide rule 20).
+    // Every field of the problem is read ONCE into scalar registers and pinned there (an empty
+    // asm makes the value opaque, so the compiler cannot re-materialise it as a kernarg load),
+    // and the mode is dispatched once per tile to a body specialised at compile time.  The
+    // generic form re-read the argument block after every store and branched on the mode per
+    // element: an s_load round trip per element, ~20 us per 128 x 128 tile (profiles/r02*).
     auto epi = [&](const TileLoc& L, const f32x16& c, const int i, const int j) {
         KProb& P = ka->prob[L.p];
+        int mode = P.mode, Mv = P.M_valid, Mr = P.M, Nc = P.N, ksp = ka->ksplit[L.p];
+        int kt = P.ct_blk;
+        float scale = P.scale;
+        const float* bias_p = P.bias;
+        const float* Rp = P.R;
+        const float* Pin = P.P_in;
+        const unsigned short* Rbp = reinterpret_cast<const unsigned short*>(P.Rb);
+        float* Cp = P.C;
+        float* Pp = P.P;
+        unsigned short* Cbp = reinterpret_cast<unsigned short*>(P.Cb);
+        unsigned short* CbTp = reinterpret_cast<unsigned short*>(P.CbT);
+        float* csp = P.colsum;
+        float* lpp = P.loss_part;
+        float* wsp = P.ws;
+        int64_t ldr = P.ldr, ldpin = P.ldp_in, ldrb = P.ldrb, ldc = P.ldc, ldp = P.ldp,
+                ldcb = P.ldcb, ldct = P.ldct;
+        asm volatile("" : "+s"(mode), "+s"(Mv), "+s"(Mr), "+s"(Nc), "+s"(ksp), "+s"(kt),
+                     "+s"(scale));
+        asm volatile("" : "+s"(bias_p), "+s"(Rp), "+s"(Pin), "+s"(Rbp), "+s"(Cp), "+s"(Pp));
+        asm volatile("" : "+s"(Cbp), "+s"(CbTp), "+s"(csp), "+s"(lpp), "+s"(wsp));
+        asm volatile("" : "+s"(ldr), "+s"(ldpin), "+s"(ldrb), "+s"(ldc), "+s"(ldp), "+s"(ldcb),
+                     "+s"(ldct));
         const int m0 = L.m0, n0 = L.n0;
-        const int mode = P.mode;
         const int rb = m0 + wr * (BM / 2) + i * 32;           // first row of this 32-row block
         const int n = n0 + wc * (BN / 2) + j * 32 + r32;
-        const bool ncol = n < P.N;
-        const int nn = ncol ? n : P.N - 1;
-        if (ka->ksplit[L.p] > 1) {                             // split-K: raw partial slab
-            float* dst = P.ws + (int64_t)L.slice * P.M * P.N;
+        const bool ncol = n < Nc;
+        const int nn = ncol ? n : Nc - 1;
+        auto row = [&](int v) { return rb + (v & 3) + 8 * (v >> 2) + 4 * h; };
+        if (ksp > 1) {                                         // split-K: raw partial slab
+            float* dst = wsp + (int64_t)L.slice * Mr * Nc;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
-                if (ncol && b < P.M_valid) dst[(int64_t)b * P.N + n] = c[v];
+                const int b = row(v);
+                if (ncol && b < Mv) dst[(int64_t)b * Nc + n] = c[v];
             }
             return;
         }
-        const float bias = P.bias ? P.bias[nn] : 0.f;
-        // The operands the mode reads (R or C; P_in; Rb) are fetched for all 16 rows in one
-        // batch before any use: padding rows read row 0 (a valid address) and drop the value.
-        // A load guarded per element makes hipcc branch around it and wait for each one in
-        // turn (guide §5 "Projection GEMM", trap 4(c)): 16 dependent round trips.
-        const float* x1 = nullptr;                           // R (or C for ACCUM)
-        int64_t ld1 = 0;
-        if (mode == LDM_GEMM_RESID_SILU || mode == LDM_GEMM_ADD_R ||
-            (mode == LDM_GEMM_DGRAD_SILU && P.R)) {
-            x1 = P.R;
-            ld1 = P.ldr;
-        } else if (mode == LDM_GEMM_ACCUM) {
-            x1 = P.C;
-            ld1 = P.ldc;
-        }
-        const float* x2 = (mode == LDM_GEMM_DGRAD_SILU || mode == LDM_GEMM_LOSS) ? P.P_in
-                                                                              : nullptr;
-        const unsigned short* xb =
-            mode == LDM_GEMM_RELU_BWD ? reinterpret_cast<const unsigned short*>(P.Rb) : nullptr;
-        float v1[16], v2[16];
-        unsigned short vb[16];
+        const float bias = bias_p ? bias_p[nn] : 0.f;
+        auto body = [&](auto mc) {
+            constexpr int MODE = decltype(mc)::value;
+            constexpr bool X1R = MODE == LDM_GEMM_RESID_SILU || MODE == LDM_GEMM_ADD_R ||
+                                 MODE == LDM_GEMM_DGRAD_SILU;
+            constexpr bool X1C = MODE == LDM_GEMM_ACCUM;
+            constexpr bool X2 = MODE == LDM_GEMM_DGRAD_SILU || MODE == LDM_GEMM_LOSS;
+            constexpr bool XB = MODE == LDM_GEMM_RELU_BWD;
+            // operands for all 16 rows in one batch (padding rows read row 0, a valid
+            // address, and drop the value): no per-element load-use round trip
+            float v1[16], v2[16];
+            unsigned short vb[16];
+            const bool has1 = X1C || (X1R && Rp != nullptr);
+            const float* x1 = X1C ? Cp : Rp;
+            const int64_t ld1 = X1C ? ldc : ldr;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
-            const int bb = (ncol && b < P.M_valid) ? b : 0;
-            v1[v] = x1 ? x1[(int64_t)bb * ld1 + nn] : 0.f;
-            v2[v] = x2 ? x2[(int64_t)bb * P.ldp_in + nn] : 0.f;
-            vb[v] = xb ? xb[(int64_t)bb * P.ldrb + nn] : (unsigned short)0;
-        }
-        float out[16];
-        float lsum = 0.f;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int b = rb + (v & 3) + 8 * (v >> 2) + 4 * h;
-            const bool live = ncol && b < P.M_valid;   // padding rows: nothing read / fp32 kept
-            const bool inb = ncol && b < P.M;
-            const int bb = live ? b : 0;
-            const int64_t ic = (int64_t)bb * P.ldc + nn;
-            const float r1 = live ? v1[v] : 0.f, r2 = live ? v2[v] : 0.f;
-            const float pre = c[v] + bias;
-            float o = pre;
-            switch (mode) {
-                case LDM_GEMM_SILU:
-                    if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
-                    o = silu(pre);
-                    break;
-                case LDM_GEMM_RESID_SILU:
-                    if (P.P && live) P.P[(int64_t)bb * P.ldp + nn] = pre;
-                    o = r1 + silu(pre);
-                    break;
-                case LDM_GEMM_RELU: o = fmaxf(pre, 0.f); break;
-                case LDM_GEMM_ACCUM: o = r1 + pre; break;
-                case LDM_GEMM_ADD_R: o = r1 + pre; break;
-                case LDM_GEMM_DGRAD_SILU: {
-                    const float dh = P.R ? r1 + pre : pre;
-                    if (P.C && live) P.C[ic] = dh;
-                    o = dh * silu_grad(r2);
-                    break;
+            for (int v = 0; v < 16; ++v) {
+                const int b = row(v);
+                const int bb = (ncol && b < Mv) ? b : 0;
+                v1[v] = 0.f;
+                v2[v] = 0.f;
+                vb[v] = 0;
+                if constexpr (X1R || X1C) {
+                    if (has1) v1[v] = x1[(int64_t)bb * ld1 + nn];
                 }
-                case LDM_GEMM_LOSS: {
-                    const float d = pre - r2;
+                if constexpr (X2) v2[v] = Pin[(int64_t)bb * ldpin + nn];
+                if constexpr (XB) vb[v] = Rbp[(int64_t)bb * ldrb + nn];
+            }
+            float out[16], pre_v[16], dh[16];
+            float lsum = 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const bool live = ncol && row(v) < Mv;
+                const float pre = c[v] + bias;
+                pre_v[v] = pre;
+                float o = pre;
+                if constexpr (MODE == LDM_GEMM_SILU) o = silu(pre);
+                if constexpr (MODE == LDM_GEMM_RESID_SILU) o = v1[v] + silu(pre);
+                if constexpr (MODE == LDM_GEMM_RELU) o = fmaxf(pre, 0.f);
+                if constexpr (MODE == LDM_GEMM_ACCUM || MODE == LDM_GEMM_ADD_R) o = v1[v] + pre;
+                if constexpr (MODE == LDM_GEMM_DGRAD_SILU) {
+                    dh[v] = v1[v] + pre;                       // v1 = 0 without R
+                    o = dh[v] * silu_grad(v2[v]);
+                }
+                if constexpr (MODE == LDM_GEMM_LOSS) {
+                    const float d = pre - v2[v];
                     lsum += live ? d * d : 0.f;
-                    o = P.scale * d;
-                    break;
+                    o = scale * d;
                 }
-                case LDM_GEMM_RELU_BWD: {             // bf16 > 0: sign bit clear, not +0
+                if constexpr (MODE == LDM_GEMM_RELU_BWD) {   // bf16 > 0: sign clear, not +0
                     const unsigned short u = vb[v];
                     o = (u != 0 && (u & 0x8000u) == 0) ? pre : 0.f;
-                    break;
                 }
-                default: break;
+                out[v] = live ? o : 0.f;
             }
-            out[v] = live ? o : 0.f;
-            if (mode != LDM_GEMM_DGRAD_SILU && P.C && live) P.C[ic] = out[v];
-            if (P.Cb && inb)
-                reinterpret_cast<unsigned short*>(P.Cb)[(int64_t)b * P.ldcb + nn] =
-                    (unsigned short)(pack2_bf16(out[v], 0.f) & 0xffffu);
-        }
-        if (P.CbT && ncol) {                 // [n][b]: 4 consecutive rows per 8-byte store
-            const int kt = P.ct_blk;
-            unsigned short* T = reinterpret_cast<unsigned short*>(P.CbT);
+            // stores: one uniform branch per output, per-lane row predicates inside
+            if (Cp) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int b = rb + 8 * g + 4 * h;
-                if (b < P.M) {
-                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                    const u32x2 w = {pack2_bf16(out[4 * g], out[4 * g + 1]),
-                                     pack2_bf16(out[4 * g + 2], out[4 * g + 3])};
-                    const int64_t at = kt ? ((int64_t)(b / kt) * P.N + n) * kt + b % kt
-                                          : (int64_t)n * P.ldct + b;
-                    *reinterpret_cast<u32x2*>(T + at) = w;
+                for (int v = 0; v < 16; ++v) {
+                    const int b = row(v);
+                    if (ncol && b < Mv)
+                        Cp[(int64_t)b * ldc + n] = MODE == LDM_GEMM_DGRAD_SILU ? dh[v] : out[v];
                 }
             }
-        }
-        if (P.colsum) {                      // one partial per 32-row block and column
-            float cs = 0.f;
+            if constexpr (MODE == LDM_GEMM_SILU || MODE == LDM_GEMM_RESID_SILU) {
+                if (Pp) {
 #pragma unroll
-            for (int v = 0; v < 16; ++v) cs += out[v];
-            cs += __shfl_xor(cs, 32);
-            if (h == 0 && ncol && rb < P.M) P.colsum[(int64_t)(rb / 32) * P.N + n] = cs;
-        }
-        if (mode == LDM_GEMM_LOSS && P.loss_part) {
+                    for (int v = 0; v < 16; ++v) {
+                        const int b = row(v);
+                        if (ncol && b < Mv) Pp[(int64_t)b * ldp + n] = pre_v[v];
+                    }
+                }
+            }
+            if (Cbp) {
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
-            if (lane == 0 && rb < P.M)
-                P.loss_part[(int64_t)(rb / 32) * ((P.N + 31) / 32) + (n0 + wc * (BN / 2) + j * 32) / 32] = lsum;
+                for (int v = 0; v < 16; ++v) {
+                    const int b = row(v);
+                    if (ncol && b < Mr)
+                        Cbp[(int64_t)b * ldcb + n] =
+                            (unsigned short)(pack2_bf16(out[v], 0.f) & 0xffffu);
+                }
+            }
+            if (CbTp && ncol) {               // [n][b]: 4 consecutive rows per 8-byte store
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int b = rb + 8 * g + 4 * h;
+                    if (b < Mr) {
+                        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                        const u32x2 w = {pack2_bf16(out[4 * g], out[4 * g + 1]),
+                                         pack2_bf16(out[4 * g + 2], out[4 * g + 3])};
+                        const int64_t at = kt ? ((int64_t)(b / kt) * Nc + n) * kt + b % kt
+                                              : (int64_t)n * ldct + b;
+                        *reinterpret_cast<u32x2*>(CbTp + at) = w;
+                    }
+                }
+            }
+            if (csp) {                        // one partial per 32-row block and column
+                float cs = 0.f;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) cs += out[v];
+                cs += __shfl_xor(cs, 32);
+                if (h == 0 && ncol && rb < Mr) csp[(int64_t)(rb / 32) * Nc + n] = cs;
+            }
+            if constexpr (MODE == LDM_GEMM_LOSS) {
+                if (lpp) {
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
+                    if (lane == 0 && rb < Mr)
+                        lpp[(int64_t)(rb / 32) * ((Nc + 31) / 32) +
+                            (n0 + wc * (BN / 2) + j * 32) / 32] = lsum;
+                }
+            }
+        };
+        typedef std::integral_constant<int, LDM_GEMM_STORE> E0;
+        switch (mode) {
+            case LDM_GEMM_SILU: body(std::integral_constant<int, LDM_GEMM_SILU>{}); break;
+            case LDM_GEMM_RESID_SILU:
+                body(std::integral_constant<int, LDM_GEMM_RESID_SILU>{});
+                break;
+            case LDM_GEMM_RELU: body(std::integral_constant<int, LDM_GEMM_RELU>{}); break;
+            case LDM_GEMM_ACCUM: body(std::integral_constant<int, LDM_GEMM_ACCUM>{}); break;
+            case LDM_GEMM_DGRAD_SILU:
+                body(std::integral_constant<int, LDM_GEMM_DGRAD_SILU>{});
+                break;
+            case LDM_GEMM_LOSS: body(std::integral_constant<int, LDM_GEMM_LOSS>{}); break;
+            case LDM_GEMM_ADD_R: body(std::integral_constant<int, LDM_GEMM_ADD_R>{}); break;
+            case LDM_GEMM_RELU_BWD:
+                body(std::integral_constant<int, LDM_GEMM_RELU_BWD>{});
+                break;
+            default: body(E0{}); break;
         }
     };
     auto epilogue = [&](const TileLoc& L, bool do0, bool do1) {
@@ -676,20 +728,24 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
                     LDM_EALIGN, "ldm_gemm_bf16: problem %d: transposed output needs 8-B "
                     "alignment, ldct and M multiples of 4", p);
     }
-    // tile: 128 x 128 once the 64 x 64 grid has >= 8 workgroups per CU (C19's 1M-row
-    // products); else 64 x 64 (config 2: 256-768 workgroups) on a 3-stage ring (48 KiB, so
-    // three workgroups share a CU and a 768-tile launch is resident at once; ring depth
-    // beyond 2 buys a lone workgroup nothing -- the per-CU DMA rate bounds it: profiles/r02b)
-    // LDM_GEMM_TILE (tuning only) replaces the automatic choice
+    // Automatic tile (profiles/r02k, gemm_bench.py; LDM_GEMM_TILE replaces it for tuning):
+    //  * >= 2048 64 x 64 tiles (C19's 1M-row products): 128 x 64, register-staged (1.10 ms for
+    //    1M x 512 x 512, 64 x 64 DMA 1.39 ms; larger tiles cut the per-CU operand bytes);
+    //  * else every K a multiple of 128 (config 2): 128-deep stages; one wave of workgroups
+    //    (<= 256 tiles) on 8 waves in two k-groups with a 4-deep ring (11.1 us for the block
+    //    GEMM 1000 x 1024 x 2048), more tiles at 2 workgroups per CU (2 stages, 64 KiB);
+    //  * else 64 x 64 on a 3-deep 64-k ring.
     static const int forced = [] {
         const char* e = getenv("LDM_GEMM_TILE");
         return e ? atoi(e) : 0;
     }();
     int tile = a.tile;
     if (tile == 0) {
+        bool k128 = true;
+        for (int p = 0; p < a.n_prob; ++p)
+            for (int g = 0; g < a.prob[p].n_seg; ++g) k128 = k128 && a.prob[p].seg[g].K % 128 == 0;
         const int t64 = gemm_tiles(a, 64, 64);
-        tile = forced ? forced : 4;
-        (void)t64;
+        tile = forced ? forced : t64 >= 2048 ? 15 : !k128 ? 4 : t64 <= 256 ? 24 : 20;
     }
     if (tile >= 20) {                          // 128-deep stages: every K a multiple of 128
         for (int p = 0; p < a.n_prob; ++p)

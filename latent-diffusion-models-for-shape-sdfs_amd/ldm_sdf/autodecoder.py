@@ -30,6 +30,7 @@ every operand row is a multiple of 16 bytes and the matrix-core path can use vec
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -211,6 +212,9 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
 
 
 _KQ = 128          # row padding of the sample axis (the K of the weight-gradient products)
+# ldm_gemm_bf16 tile of the weight-gradient products (128 x 128: each slice walks KT = 8192
+# samples, long enough for the bigger tile's per-CU operand economy; tuning: AD_WG_TILE)
+_WG_TILE = int(os.environ.get("AD_WG_TILE", "3"))
 _KSEG = 64         # column padding of [z || xyz] (a GEMM K segment)
 
 
@@ -336,9 +340,9 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
     g_cur = torch.empty(Np, H, **bf)
     gT_cur = torch.empty(nblk, H, KT, **bf)
     cs = torch.empty(nrow32, H, **f32)
-    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"]),
-              ops.gemm_problem([(g8b, W8T)], Np, H, mode="relu_bwd", M_valid=N, Rb=h[7],
+    ops.gemm([ops.gemm_problem([(g8b, W8T)], Np, H, mode="relu_bwd", M_valid=N, Rb=h[7],
                                Cb=g_cur, CbT=gT_cur, colsum=cs, ct_blk=KT)])
+    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"])], tile=_WG_TILE)
     colsums = {7: cs}
     gcs = {}                                       # g_l per 32-row block sums (bias / latent)
     Gs = {}                                        # per-shape column sums of g_skip and g_0
@@ -366,17 +370,19 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
         if onehot is not None and l in (skip, 0):
             Gs[l] = torch.empty(S, H, **f32)
             probs.append(wgrad(onehot, gT_cur, S, H, Gs[l]))
+        # weight gradients (long K per slice): larger tiles than the 1M-row G W product, so
+        # their own launch
+        ops.gemm(probs, tile=_WG_TILE)
         if l > 0:
             win = h[l - 1].shape[1]
             WdT = WT["W4h"] if l == skip else WT[f"W{l}"]          # [win, wout]
             g_nxt = torch.empty(Np, win, **bf)
             gT_nxt = torch.empty(nblk, win, KT, **bf)
             cs = torch.empty(nrow32, win, **f32)
-            probs.append(ops.gemm_problem([(g_cur, WdT)], Np, win, mode="relu_bwd", M_valid=N,
-                                          Rb=h[l - 1], Cb=g_nxt, CbT=gT_nxt, colsum=cs,
-                                          ct_blk=KT))
+            ops.gemm([ops.gemm_problem([(g_cur, WdT)], Np, win, mode="relu_bwd", M_valid=N,
+                                       Rb=h[l - 1], Cb=g_nxt, CbT=gT_nxt, colsum=cs,
+                                       ct_blk=KT)])
             colsums[l - 1] = cs
-        ops.gemm(probs)
         if l > 0:
             g_prev_keep = (g_cur, gT_cur)            # noqa: F841 (alive until the launch is queued)
             g_cur, gT_cur = g_nxt, gT_nxt
