@@ -424,9 +424,9 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                 if (lpp) {
 #pragma unroll
                     for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
-                    if (lane == 0 && rb < Mr)
-                        lpp[(int64_t)(rb / 32) * ((Nc + 31) / 32) +
-                            (n0 + wc * (BN / 2) + j * 32) / 32] = lsum;
+                    const int cb = n0 + wc * (BN / 2) + j * 32;     // first column of the block
+                    if (lane == 0 && rb < Mr && cb < Nc)    // (a block wholly past N: no slot)
+                        lpp[(int64_t)(rb / 32) * ((Nc + 31) / 32) + cb / 32] = lsum;
                 }
             }
         };

@@ -40,7 +40,7 @@ def decoder():
 def test_native_library_is_loaded(dev):
     import ldm_sdf._capi as capi
     lib = capi.load()
-    assert lib.ldm_abi_version() == 2
+    assert lib.ldm_abi_version() == capi.ABI_VERSION
     maps = open("/proc/self/maps").read()
     assert "libldm_sdf.so" in maps
 
