@@ -53,6 +53,9 @@ struct LoopArgs {
     int hier;              // 1: XCD-hierarchical, 2: hierarchical arrival + direct poll,
                            // 0: one flat counter
     unsigned spin_limit;   // polls before a barrier wait gives up (status 1)
+    unsigned long long* hg;  // replica loop: tagged h granules [8 XCDs][2][MBX][H]
+    unsigned long long* xg;  // replica loop: tagged x granules [8 XCDs][2][MBX][D]
+    int tagged;              // replica loop: 1 = tagged-granule hand-offs, 0 = XCD barriers
 };
 
 template <typename TW, int NJ>
@@ -499,6 +502,64 @@ __device__ __forceinline__ bool replica_sync(unsigned* sync, unsigned xcc, unsig
     return *ok != 0;
 }
 
+// Data-tagged granule hand-off (MI355X guide: handoff-1to1 / allgather rows, "keep 8-byte
+// granules, flat sweep").  A producer stores {value, tag} as ONE 8-byte agent-scope store
+// (single-copy atomic: a reader sees the old pair or the new one); a consumer sweeps the
+// granules it needs with agent-scope (L1-bypassing) 8-byte loads and re-polls any whose tag is
+// not yet the layer's.  The data is its own flag: no arrival counter, no generation word, no
+// drain before a flag -- one L2 round trip after the last producer's store instead of the
+// barrier's three.  Tags are the launch's phase numbers (1, 2, ...); the host zeroes the
+// granules before every launch, so no stale tag can match.  Double buffering is WAR-safe by
+// data dependence: a workgroup can only hold every granule of layer k+1 once every workgroup
+// has published its layer-k+1 rows, i.e. finished reading layer k; layer k+2 then overwrites
+// layer k's buffer (the same argument holds for the x ping-pong between steps).
+__device__ __forceinline__ void publish_tagged(u64* g, float v, unsigned tag) {
+    const u64 w = ((u64)tag << 32) | __builtin_bit_cast(unsigned, v);
+    __hip_atomic_store(g, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// n granules -> xs[0..n), every thread granules tid, tid + NT, ... (all loads issued before any
+// tag test).  Returns false (and sets the status word) if a granule never arrives.
+template <int NT, int U>
+__device__ __forceinline__ bool stage_tagged(float* xs, const u64* G, int n, unsigned tag,
+                                             unsigned* status, unsigned limit) {
+    bool good = true;
+    for (int base = 0; base < n; base += NT * U) {
+        u64 t[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * NT + (int)threadIdx.x;
+            t[u] = __hip_atomic_load(G + (i < n ? i : 0), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * NT + (int)threadIdx.x;
+            if (i < n) {
+                unsigned spins = 0;
+                while ((unsigned)(t[u] >> 32) != tag) {
+                    if ((spins & 63) == 63 &&
+                        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        good = false;
+                        break;
+                    }
+                    if (++spins > limit) {
+                        __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        good = false;
+                        break;
+                    }
+#if LDM_LOOP_SLEEP > 0
+                    __builtin_amdgcn_s_sleep(LDM_LOOP_SLEEP);
+#endif
+                    t[u] = __hip_atomic_load(G + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                xs[i] = __builtin_bit_cast(float, (unsigned)t[u]);
+            }
+        }
+    }
+    return good;
+}
+
 constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per wave
 
 template <int D_, int MBX>
@@ -579,7 +640,34 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     const float bi = a.b_in[mh];
     const float bo = a.b_out[mo];
     float* hrep = a.h + (size_t)xcc * 2 * MBX * H;       // [2][MBX][H] per replica
+    u64* hgr = a.hg + (size_t)xcc * 2 * MBX * H;          // tagged: [2][MBX][H] per replica
+    u64* xgr = a.xg + (size_t)xcc * 2 * MBX * D_;         // tagged: [2][MBX][D] per replica
+    const bool tagged = a.tagged != 0;
+    unsigned* status = sync + 32 * R_STATUS;
     unsigned phase = 0;
+    // layer boundary: the barrier form publishes, then waits for the XCD's workgroups; the
+    // tagged form has nothing to wait for here (the next layer's stage polls the data)
+    auto boundary = [&]() -> bool {
+        if (tagged) return true;
+        return replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit);
+    };
+    // stage this replica's [MBX][K] activations of the layer that published under tag `tg`
+    auto stage_act = [&](float* dst, const float* plain, const u64* gran, int K, unsigned tg) {
+        if (!tagged || gran == nullptr) {
+#pragma unroll
+            for (int b = 0; b < MBX; ++b) stage<NT>(dst + b * K, plain + (size_t)b * K, K >> 1);
+            __syncthreads();
+            return true;
+        }
+        if (threadIdx.x == 0) *ok = 1;
+        __syncthreads();
+        // only this replica's nsh shapes are published (rows of a missing second shape are
+        // computed on whatever the LDS holds and never written)
+        const bool good = stage_tagged<NT, 2>(dst, gran, nsh * K, tg, status, a.spin_limit);
+        if (!good) *ok = 0;
+        __syncthreads();
+        return *ok != 0;
+    };
 
     for (int s = 0; s < a.steps; ++s) {
         const int t = a.t_hi - s;
@@ -594,19 +682,27 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
             reinterpret_cast<const unsigned*>(xin + (size_t)sq * D + mo), __ATOMIC_RELAXED,
             __HIP_MEMORY_SCOPE_AGENT));
         const float c1 = a.c1[t], c2 = a.c2[t], sg = a.sg[t];
-        // in-projection over this replica's shapes
+        // in-projection over this replica's shapes (step 0: the caller's x; later: the
+        // previous out-projection's tagged granules)
+        if (tagged && s > 0) {
+            if (!stage_act(xs, nullptr, xgr + (size_t)(s & 1) * MBX * D, D, phase)) return;
+        } else {
 #pragma unroll
-        for (int b = 0; b < MBX; ++b)
-            stage<NT>(xs + b * D, xin + (size_t)((int)xcc + 8 * (b < nsh ? b : 0)) * D, D >> 1);
-        __syncthreads();
+            for (int b = 0; b < MBX; ++b)
+                stage<NT>(xs + b * D, xin + (size_t)((int)xcc + 8 * (b < nsh ? b : 0)) * D, D >> 1);
+            __syncthreads();
+        }
         {
             float v[NV];
             rows_partial<R, R, NJD, MBX>(v, get_in, xs, D, lane);
             const float acc = reduce_scatter<NV>(v, lane);
-            if (wr_h) publish(hrep + (size_t)qb * H + mh, acc + bi);
+            ++phase;
+            if (wr_h) {
+                if (tagged) publish_tagged(hgr + (size_t)qb * H + mh, acc + bi, phase);
+                else publish(hrep + (size_t)qb * H + mh, acc + bi);
+            }
         }
-        ++phase;
-        if (!replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit)) return;
+        if (!boundary()) return;
         // the four blocks as four compile-time copies (a runtime block index into wb would
         // put the register-resident weights in scratch)
         bool alive = true;
@@ -615,18 +711,23 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
             if (!alive) return;
             const float* hin = hrep + (size_t)(k & 1) * MBX * H;
             float* hout = hrep + (size_t)((k + 1) & 1) * MBX * H;
-            stage<NT>(xs, hin, (MBX * H) >> 1);
-            __syncthreads();
+            if (!stage_act(xs, hin, tagged ? hgr + (size_t)(k & 1) * MBX * H : nullptr, H,
+                           phase)) {
+                alive = false;
+                return;
+            }
             float v[NV];
             rows_partial<R, R, NJH, MBX>(v, [&](int r, int j) { return wb[k][r][j]; }, xs, H,
                                          lane);
             const float acc = reduce_scatter<NV>(v, lane);
+            ++phase;
             if (wr_h) {
                 const float pre = acc + ep[k];
-                publish(hout + (size_t)qb * H + mh, xs[qb * H + mh] + silu(pre));
+                const float hv = xs[qb * H + mh] + silu(pre);
+                if (tagged) publish_tagged(hgr + (size_t)((k + 1) & 1) * MBX * H + (size_t)qb * H + mh, hv, phase);
+                else publish(hout + (size_t)qb * H + mh, hv);
             }
-            ++phase;
-            alive = replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit);
+            alive = boundary();
         };
         static_assert(NB == 4, "four residual blocks");
         block(std::integral_constant<int, 0>{});
@@ -634,22 +735,26 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         block(std::integral_constant<int, 2>{});
         block(std::integral_constant<int, 3>{});
         if (!alive) return;
-        stage<NT>(xs, hrep + (size_t)(NB & 1) * MBX * H, (MBX * H) >> 1);
-        __syncthreads();
+        if (!stage_act(xs, hrep + (size_t)(NB & 1) * MBX * H,
+                       tagged ? hgr + (size_t)(NB & 1) * MBX * H : nullptr, H, phase))
+            return;
         {
             float v[NV];
             // out-projection: RO rows, zero-padded to the R-row reduce-scatter
             rows_partial<R, RO, NJH, MBX>(v, get_out, xs, H, lane);
             const float acc = reduce_scatter<NV>(v, lane);
+            ++phase;
             if (wr_o) {
                 const float pre = acc + bo;
                 const bool noise = t > 0;
-                publish(xout + (size_t)sb * D + mo,
-                        ddpm_update(xp, pre, noise ? zp : 0.f, c1, c2, sg, noise));
+                const float xv = ddpm_update(xp, pre, noise ? zp : 0.f, c1, c2, sg, noise);
+                publish(xout + (size_t)sb * D + mo, xv);          // the caller's ping-pong
+                if (tagged)
+                    publish_tagged(xgr + (size_t)((s & 1) ^ 1) * MBX * D + (size_t)qb * D + mo,
+                                   xv, phase);
             }
         }
-        ++phase;
-        if (!replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit)) return;
+        if (!boundary()) return;
     }
 }
 
@@ -734,12 +839,14 @@ int launch_loop(const LoopArgs& a, hipStream_t s) {
 using namespace ldm;
 
 // ws = [activations: 32 H floats (chip-wide loop: [2][B][H], B <= 16; replica loop:
-// [8 XCDs][2][MBX <= 2][H])] [sync words: kSyncBytes]
+// [8 XCDs][2][MBX <= 2][H])] [sync words: kSyncBytes] [replica loop's tagged granules:
+// h [8][2][2][H] then x [8][2][2][512], 8 bytes each; zeroed with the sync words per launch]
 static size_t act_floats(int H) { return (size_t)32 * H; }
+static size_t gran_bytes(int H) { return (size_t)8 * 2 * 2 * (H + 512) * 8; }
 
 extern "C" size_t ldm_sample_loop_ws_bytes(int B, int H) {
     (void)B;
-    return act_floats(H) * sizeof(float) + kSyncBytes;
+    return act_floats(H) * sizeof(float) + kSyncBytes + gran_bytes(H);
 }
 
 extern "C" int ldm_sample_loop_supported(const ldm_denoiser_t* w, int B) {
@@ -787,8 +894,14 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
     }
     for (int k = 0; k < 4; ++k)
         LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
+    a.hg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.ctr) + kSyncBytes);
+    a.xg = a.hg + (size_t)8 * 2 * 2 * w->H;
+    // replica hand-offs: tagged granules (default) or XCD-local barriers ("0", A/B)
+    const char* tg = getenv("LDM_SAMPLE_LOOP_TAGGED");
+    a.tagged = (tg && tg[0] == '0') ? 0 : 1;
     hipStream_t st = (hipStream_t)s;
-    if (hipMemsetAsync(a.ctr, 0, kSyncBytes, st) != hipSuccess) return launch_status("sample_loop memset");
+    const size_t zero = kSyncBytes + (replica && a.tagged ? gran_bytes(w->H) : 0);
+    if (hipMemsetAsync(a.ctr, 0, zero, st) != hipSuccess) return launch_status("sample_loop memset");
     if (replica) return launch_replica(a, st);
     if (w->dtype == LDM_BF16)
         return B <= 8 ? launch_loop<unsigned short, 8>(a, st) : launch_loop<unsigned short, 16>(a, st);

@@ -36,7 +36,9 @@ sg = ldm_sdf.Sampler(den, sch, B, dtype="bf16", device=dev, persistent=False)
 ref = sg.run(xT, noise).clone()
 res["graph_steps_per_s"] = timeit(sg)
 for mode in os.environ.get("MODES", "replica,xcd,flat").split(","):
-    os.environ["LDM_SAMPLE_LOOP_BARRIER"] = mode
+    # "replica": tagged-granule hand-offs (default); "replica0": the same loop on XCD barriers
+    os.environ["LDM_SAMPLE_LOOP_BARRIER"] = mode.rstrip("0")
+    os.environ["LDM_SAMPLE_LOOP_TAGGED"] = "0" if mode.endswith("0") else "1"
     sp = ldm_sdf.Sampler(den, sch, B, dtype="bf16", device=dev, persistent=True)
     out = sp.run(xT, noise).clone()
     res[f"loop_{mode}_status"] = sp.loop.status()
