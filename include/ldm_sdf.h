@@ -221,6 +221,25 @@ typedef struct ldm_adamw_tensor {
 } ldm_adamw_tensor_t;
 int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double lr, double beta1,
                     double beta2, double eps, double weight_decay, int step, ldm_stream_t s);
+/* One whole single-rank training step: ldm_denoiser_train_step, then ldm_adamw_multi over
+ * `tensors` (hyper-parameters as there; eps_adam is AdamW's eps).  The updates run in three
+ * batches, each as soon as its gradients are final and no later launch of the step reads its
+ * weights (matched by gradient pointer): grads->w_out / w_in / w_blk[k] after the backward's
+ * dtemb launch, w_t1 / w_t2 after its last GEMM, everything else after the bias sums.  With a
+ * `side` stream the batches run there behind fork events, on a grid capped at 2 workgroups per
+ * CU, overlapping the backward's tail; s then waits for side.  side == NULL or == s: all in
+ * order on s, one AdamW launch after the bias sums.  Results are those of the two calls in
+ * sequence, bit for bit (each update reads only its own tensor's final gradient).  Measured
+ * (DESIGN.md §5): the overlap does NOT pay at config 2 -- the HBM-bound AdamW slows the
+ * latency-bound GEMMs beside it more than it hides -- so ldm_sdf.train passes side = NULL.  A data-parallel step needs the gradient all-reduce
+ * in between: use the two calls there. */
+int ldm_denoiser_train_step_adamw(const ldm_denoiser_t* w, const ldm_sched_t* sc,
+                                  const float* x0, const float* eps, const int32_t* t, int B,
+                                  void* saved, const ldm_denoiser_grads_t* grads,
+                                  float* loss_out, const ldm_adamw_tensor_t* tensors, int n,
+                                  double lr, double beta1, double beta2, double eps_adam,
+                                  double weight_decay, int step, ldm_stream_t s,
+                                  ldm_stream_t side);
 /* AdamW on fp32 masters p [n] with grads g, moments m, v (torch.optim.AdamW's order; step is
  * 1-based).  p_bf16 (may be NULL): bf16 [n] working copy of the updated p, written in the same
  * pass (RNE). */

@@ -261,8 +261,16 @@ int forward(const ldm_denoiser_t* w, const TrainWs& L, const float* eps_target,
 }
 
 // Backward GEMMs from go_b / go_T (dL/d eps_hat in bf16) and the saved activations.
+// `hook` (may be null) is called at point 0 once the gradients of the in-projection,
+// out-projection and block weights are final and no later launch of this backward reads those
+// weights (after the dtemb launch, the last reader of the blocks' U_k), and at point 1 after
+// the last GEMM (the time-MLP weights), so their optimizer updates can start there.
+struct StepHook {
+    int (*fn)(void* ctx, int point, hipStream_t s);
+    void* ctx;
+};
 int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads_t* gr,
-             float* dx, hipStream_t s) {
+             float* dx, hipStream_t s, const StepHook* hook = nullptr) {
     const int Bp = L.Bp, B = L.B, D = L.D, H = L.H, TE = L.TE, nb = L.nb;
     const bf16_t* const* Wt = reinterpret_cast<const bf16_t* const*>(w->wt_blk);
     {
@@ -310,6 +318,7 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
         seg(dwi, L.dh0_T, Bp, L.xt_T, Bp, Bp);
         dwi.C = gr->w_in; dwi.ldc = D;
         LDM_TRY(launch({dt, dwi}, s));
+        if (hook) LDM_TRY(hook->fn(hook->ctx, 0, s));
     }
     {
         ldm_gemm_prob_t dw2 = prob(H, H, H);                     // dWt2 = dtemb^T u
@@ -334,6 +343,7 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
             LDM_TRY(launch({dw1}, s));
         }
     }
+    if (hook) LDM_TRY(hook->fn(hook->ctx, 1, s));
     return 0;
 }
 
@@ -472,11 +482,24 @@ struct AdamJobs {
     float decay, omb1, b2, omb2, eps, step_size, bc2_sqrt;
 };
 
+typedef const __attribute__((address_space(4))) AdamJobs KJobs;
+template <typename KJ>
+__device__ __forceinline__ void adamw_tile(KJ* kj, unsigned short (&sT)[64][64 + 8], int tile);
+
 __global__ __launch_bounds__(256) void adamw_multi_kernel(AdamJobs jobs) {
-    typedef const __attribute__((address_space(4))) AdamJobs KJ;
+    typedef KJobs KJ;
     KJ* kj = (KJ*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ unsigned short sT[64][64 + 8];
-    const int tile = blockIdx.x;
+    // grid-stride over the tiles: a capped grid leaves wave slots free on every CU for work on
+    // another stream (ldm_denoiser_train_step_adamw); uncapped, one tile per workgroup
+    for (int tile = blockIdx.x; tile < kj->first[kj->n]; tile += gridDim.x) {
+        __syncthreads();                   // the previous tile's transposed reads of sT are done
+        adamw_tile(kj, sT, tile);
+    }
+}
+
+template <typename KJ>
+__device__ __forceinline__ void adamw_tile(KJ* kj, unsigned short (&sT)[64][64 + 8], int tile) {
     int j = 0;
     for (int i = 1; i < kj->n; ++i)
         if (tile >= kj->first[i]) j = i;
@@ -575,16 +598,18 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(AdamJobs jobs) {
 }  // namespace
 }  // namespace ldm
 
-extern "C" int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double lr,
-                               double beta1, double beta2, double eps, double weight_decay,
-                               int step, ldm_stream_t s) {
-    LDM_REQUIRE(tensors && n >= 1 && n <= LDM_ADAMW_MAX_TENSORS && step >= 1, LDM_EINVAL,
-                "ldm_adamw_multi: 1..%d tensors, step >= 1", LDM_ADAMW_MAX_TENSORS);
+namespace ldm {
+namespace {
+// One adamw_multi_kernel launch over the tensors list[0..n) (host descriptors).
+int adamw_launch(const ldm_adamw_tensor_t* const* list, int n, double lr, double beta1,
+                 double beta2, double eps, double weight_decay, int step, hipStream_t s,
+                 int grid_cap = 0) {
+    if (n == 0) return 0;
     AdamJobs J;
     memset(&J, 0, sizeof(J));
     int tiles = 0;
     for (int i = 0; i < n; ++i) {
-        const ldm_adamw_tensor_t& T = tensors[i];
+        const ldm_adamw_tensor_t& T = *list[i];
         LDM_REQUIRE(T.p && T.g && T.m && T.v && T.rows >= 1 && T.cols >= 1, LDM_EINVAL,
                     "ldm_adamw_multi: tensor %d incomplete", i);
         J.t[i] = T;
@@ -602,6 +627,124 @@ extern "C" int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double 
     J.eps = (float)eps;
     J.step_size = (float)(lr / bc1);
     J.bc2_sqrt = (float)sqrt(bc2);
-    hipLaunchKernelGGL(adamw_multi_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)s, J);
+    const int grid = grid_cap > 0 && grid_cap < tiles ? grid_cap : tiles;
+    hipLaunchKernelGGL(adamw_multi_kernel, dim3(grid), dim3(256), 0, s, J);
     return launch_status("ldm_adamw_multi");
+}
+
+// Fork / join events of ldm_denoiser_train_step_adamw, per device (created once): three forks
+// (one per AdamW batch) and the join.
+constexpr int kForks = 3;
+int fork_events(hipEvent_t (&ev)[kForks + 1]) {
+    static hipEvent_t pool[64][kForks + 1];
+    int dev = 0;
+    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, LDM_EINVAL,
+                "train_step_adamw: no current device");
+    for (int i = 0; i <= kForks; ++i) {
+        if (!pool[dev][i]) {
+            const hipError_t e = hipEventCreateWithFlags(&pool[dev][i], hipEventDisableTiming);
+            LDM_REQUIRE(e == hipSuccess, (int)e, "train_step_adamw: hipEventCreate: %s",
+                        hipGetErrorString(e));
+        }
+        ev[i] = pool[dev][i];
+    }
+    return 0;
+}
+
+// The step's AdamW in three batches, each started as soon as its gradients are final and no
+// later launch of the step reads its weights: 0 = block, in- and out-projection weights (after
+// the dtemb launch), 1 = the time-MLP weights (after the last GEMM), 2 = the biases (after the
+// bias sums).  With a side stream every batch runs there behind a fork event, on a capped grid
+// (2 workgroups per CU) so the main stream's GEMMs keep wave slots; the main stream waits for
+// the side stream at the end.
+struct AdamSplit {
+    const ldm_adamw_tensor_t* batch[kForks][LDM_ADAMW_MAX_TENSORS];
+    int nb[kForks];
+    double lr, beta1, beta2, eps, wd;
+    int step, grid_cap;
+    hipStream_t side;
+    hipEvent_t ev[kForks + 1];
+};
+
+int adam_batch(AdamSplit& A, int i, hipStream_t s) {
+    if (A.nb[i] == 0) return 0;
+    hipStream_t q = s;
+    if (A.side) {
+        LDM_REQUIRE(hipEventRecord(A.ev[i], s) == hipSuccess &&
+                        hipStreamWaitEvent(A.side, A.ev[i], 0) == hipSuccess,
+                    LDM_EINVAL, "train_step_adamw: fork failed");
+        q = A.side;
+    }
+    return adamw_launch(A.batch[i], A.nb[i], A.lr, A.beta1, A.beta2, A.eps, A.wd, A.step, q,
+                        A.side ? A.grid_cap : 0);
+}
+
+int adam_hook(void* ctx, int point, hipStream_t s) {
+    return adam_batch(*static_cast<AdamSplit*>(ctx), point, s);
+}
+}  // namespace
+}  // namespace ldm
+
+extern "C" int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double lr,
+                               double beta1, double beta2, double eps, double weight_decay,
+                               int step, ldm_stream_t s) {
+    LDM_REQUIRE(tensors && n >= 1 && n <= LDM_ADAMW_MAX_TENSORS && step >= 1, LDM_EINVAL,
+                "ldm_adamw_multi: 1..%d tensors, step >= 1", LDM_ADAMW_MAX_TENSORS);
+    const ldm_adamw_tensor_t* list[LDM_ADAMW_MAX_TENSORS];
+    for (int i = 0; i < n; ++i) list[i] = &tensors[i];
+    return adamw_launch(list, n, lr, beta1, beta2, eps, weight_decay, step, (hipStream_t)s);
+}
+
+extern "C" int ldm_denoiser_train_step_adamw(
+    const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, const float* eps,
+    const int32_t* t, int B, void* saved, const ldm_denoiser_grads_t* grads, float* loss_out,
+    const ldm_adamw_tensor_t* tensors, int n, double lr, double beta1, double beta2,
+    double eps_adam, double weight_decay, int step, ldm_stream_t s, ldm_stream_t side) {
+    LDM_TRY(check_desc(w, B, true));
+    LDM_TRY(check_grads(w, grads));
+    LDM_REQUIRE(sc && sc->abi_version == LDM_ABI_VERSION && sc->sqrt_ab && sc->sqrt_1mab,
+                LDM_EINVAL, "ldm_denoiser_train_step_adamw: bad schedule");
+    LDM_REQUIRE(x0 && eps && t && saved && LDM_ALIGNED(saved, 256), LDM_EINVAL,
+                "ldm_denoiser_train_step_adamw: x0, eps, t and a 256-B aligned workspace are "
+                "required");
+    LDM_REQUIRE(tensors && n >= 1 && n <= LDM_ADAMW_MAX_TENSORS && step >= 1, LDM_EINVAL,
+                "ldm_denoiser_train_step_adamw: 1..%d tensors, step >= 1",
+                LDM_ADAMW_MAX_TENSORS);
+    AdamSplit A;
+    memset(&A, 0, sizeof(A));
+    A.lr = lr; A.beta1 = beta1; A.beta2 = beta2; A.eps = eps_adam; A.wd = weight_decay;
+    A.step = step;
+    A.side = side == s ? nullptr : (hipStream_t)side;
+    if (A.side) {
+        LDM_TRY(fork_events(A.ev));
+        int dev = 0, cus = 0;
+        LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
+                        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
+                            hipSuccess,
+                    LDM_EINVAL, "train_step_adamw: device query failed");
+        A.grid_cap = 2 * cus;
+    }
+    // batch of each tensor, matched by its gradient pointer
+    for (int i = 0; i < n; ++i) {
+        const float* g = tensors[i].g;
+        bool b0 = g == grads->w_out || g == grads->w_in;
+        for (int k = 0; k < w->n_blocks; ++k) b0 = b0 || g == grads->w_blk[k];
+        // without a side stream one launch after the bias sums (fewer launches, same bits)
+        const int bi = !A.side ? 2 : b0 ? 0 : (g == grads->w_t1 || g == grads->w_t2) ? 1 : 2;
+        A.batch[bi][A.nb[bi]++] = &tensors[i];
+    }
+    const TrainWs L = layout(w, B, saved);
+    hipStream_t st = (hipStream_t)s;
+    const float nf = (float)B * (float)w->D;
+    const StepHook hook = {adam_hook, &A};
+    LDM_TRY(prep_inputs(w, L, x0, eps, t, sc, st));
+    LDM_TRY(forward(w, L, eps, nullptr, 2.f / nf, st));
+    LDM_TRY(backward(w, L, grads, nullptr, st, &hook));        // batches 0 and 1
+    LDM_TRY(finalize(L, grads, nullptr, loss_out, 1.f / nf, st));
+    LDM_TRY(adam_batch(A, 2, st));
+    if (A.side)
+        LDM_REQUIRE(hipEventRecord(A.ev[kForks], A.side) == hipSuccess &&
+                        hipStreamWaitEvent(st, A.ev[kForks], 0) == hipSuccess,
+                    LDM_EINVAL, "train_step_adamw: join failed");
+    return 0;
 }

@@ -270,6 +270,199 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                         __builtin_bit_cast(bf16x8, bf[s][j]), acc[i][j], 0, 0, 0);
     };
 
+    // ---- LDS-transposed epilogue (non-persistent kernels) -------------------------------------
+    // The accumulator layout gives a lane ONE column of 16 rows, so the row-major outputs above
+    // take one 4-byte (bf16: 2-byte) store per element: 16-52 store instructions per 32 x 32
+    // block, and a one-tile-per-CU launch ends in that store-issue tail (the block GEMM: 11 us
+    // with a plain store, 18.7 us with RESID_SILU's four outputs, profiles/r02f).  Here the
+    // block goes through a per-wave 4 KiB LDS tile first, so a lane holds 4 consecutive columns
+    // of 4 rows: every row-major operand moves as 16-byte (bf16: 8-byte) vectors, 4 per output.
+    // The element-wise arithmetic is the same expression per element as epi(), so the outputs
+    // are bit-identical; the column sums and the transposed bf16 copy are formed from the
+    // results read back in accumulator layout, in epi()'s order (bit-identical too).
+    // Falls back to the accumulator-layout stores for a block that crosses N, or operands whose
+    // pointers / strides do not allow the vectors.
+    constexpr int EPI_LDS_OFF = KG == 2 ? RM * 4 * RN * 16 * 64 * 4 : 0;   // past KG's `red`
+    static_assert(PERSIST || EPI_LDS_OFF + NW * 4096 <= STAGES * STAGE_ELEMS * 2,
+                  "epilogue scratch fits the ring");
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    auto epi_lds = [&](const TileLoc& L, const f32x16& c, const int i, const int nb,
+                       const int mode, const int Mv, const int Mr, const int Nc, const int ksp,
+                       const int kt, const float scale, const float* bias_p, const float* Rp,
+                       const float* Pin, const unsigned short* Rbp, float* Cp, float* Pp,
+                       unsigned short* Cbp, unsigned short* CbTp, float* csp, float* lpp,
+                       float* wsp, const int64_t ldr, const int64_t ldpin, const int64_t ldrb,
+                       const int64_t ldc, const int64_t ldp, const int64_t ldcb,
+                       const int64_t ldct) {
+        const int rb = L.m0 + wr * (BM / 2) + i * 32;      // first row of this 32-row block
+        float* sc = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + EPI_LDS_OFF) +
+                    wave * 1024;
+        auto arow = [&](int v) { return (v & 3) + 8 * (v >> 2) + 4 * h; };   // block-local row
+        const int rl = lane >> 3, cq = 4 * (lane & 7);   // row layout: rows rl + 8p, 4 columns
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sc[arow(v) * 32 + r32] = c[v];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        f32x4 cv[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+            cv[p] = *reinterpret_cast<const f32x4*>(sc + (rl + 8 * p) * 32 + cq);
+        const int n4 = nb + cq;
+        if (ksp > 1) {                                       // split-K: raw partial slab
+            float* dst = wsp + (int64_t)L.slice * Mr * Nc;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int b = rb + rl + 8 * p;
+                if (b < Mv) *reinterpret_cast<f32x4*>(dst + (int64_t)b * Nc + n4) = cv[p];
+            }
+            asm volatile("" ::: "memory");
+            return;
+        }
+        const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 bias4 = bias_p ? *reinterpret_cast<const f32x4*>(bias_p + n4) : zero4;
+        auto body = [&](auto mc) {
+            constexpr int MODE = decltype(mc)::value;
+            constexpr bool X1R = MODE == LDM_GEMM_RESID_SILU || MODE == LDM_GEMM_ADD_R ||
+                                 MODE == LDM_GEMM_DGRAD_SILU;
+            constexpr bool X1C = MODE == LDM_GEMM_ACCUM;
+            constexpr bool X2 = MODE == LDM_GEMM_DGRAD_SILU || MODE == LDM_GEMM_LOSS;
+            constexpr bool XB = MODE == LDM_GEMM_RELU_BWD;
+            constexpr bool LS = MODE == LDM_GEMM_LOSS;
+            f32x4 v1[4], v2[4];
+            u32x2 vb[4];
+            const bool has1 = X1C || (X1R && Rp != nullptr);
+            const float* x1 = X1C ? Cp : Rp;
+            const int64_t ld1 = X1C ? ldc : ldr;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {    // padding rows read row 0 (valid) and drop it
+                const int b = rb + rl + 8 * p;
+                const int bb = b < Mv ? b : 0;
+                v1[p] = zero4;
+                v2[p] = zero4;
+                vb[p] = u32x2{0u, 0u};
+                if constexpr (X1R || X1C) {
+                    if (has1)
+                        v1[p] = *reinterpret_cast<const f32x4*>(x1 + (int64_t)bb * ld1 + n4);
+                }
+                if constexpr (X2)
+                    v2[p] = *reinterpret_cast<const f32x4*>(Pin + (int64_t)bb * ldpin + n4);
+                if constexpr (XB)
+                    vb[p] = *reinterpret_cast<const u32x2*>(Rbp + (int64_t)bb * ldrb + n4);
+            }
+            f32x4 out[4], pre_v[4], dh[4], dd[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const bool live = rb + rl + 8 * p < Mv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {      // epi()'s expressions, element for element
+                    const float pre = cv[p][e] + bias4[e];
+                    pre_v[p][e] = pre;
+                    float o = pre;
+                    dh[p][e] = 0.f;
+                    dd[p][e] = 0.f;
+                    if constexpr (MODE == LDM_GEMM_SILU) o = silu(pre);
+                    if constexpr (MODE == LDM_GEMM_RESID_SILU) o = v1[p][e] + silu(pre);
+                    if constexpr (MODE == LDM_GEMM_RELU) o = fmaxf(pre, 0.f);
+                    if constexpr (MODE == LDM_GEMM_ACCUM || MODE == LDM_GEMM_ADD_R)
+                        o = v1[p][e] + pre;
+                    if constexpr (MODE == LDM_GEMM_DGRAD_SILU) {
+                        dh[p][e] = v1[p][e] + pre;
+                        o = dh[p][e] * silu_grad(v2[p][e]);
+                    }
+                    if constexpr (LS) {
+                        dd[p][e] = pre - v2[p][e];
+                        o = scale * dd[p][e];
+                    }
+                    if constexpr (MODE == LDM_GEMM_RELU_BWD) {
+                        const unsigned u = (vb[p][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                        o = (u != 0 && (u & 0x8000u) == 0) ? pre : 0.f;
+                    }
+                    out[p][e] = live ? o : 0.f;
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int b = rb + rl + 8 * p;
+                if (Cp && b < Mv)
+                    *reinterpret_cast<f32x4*>(Cp + (int64_t)b * ldc + n4) =
+                        MODE == LDM_GEMM_DGRAD_SILU ? dh[p] : out[p];
+                if constexpr (MODE == LDM_GEMM_SILU || MODE == LDM_GEMM_RESID_SILU) {
+                    if (Pp && b < Mv)
+                        *reinterpret_cast<f32x4*>(Pp + (int64_t)b * ldp + n4) = pre_v[p];
+                }
+                if (Cbp && b < Mr)
+                    *reinterpret_cast<u32x2*>(Cbp + (int64_t)b * ldcb + n4) = u32x2{
+                        pack2_bf16(out[p][0], out[p][1]), pack2_bf16(out[p][2], out[p][3])};
+            }
+            if (CbTp || csp || (LS && lpp)) {   // back to accumulator layout through the tile
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    *reinterpret_cast<f32x4*>(sc + (rl + 8 * p) * 32 + cq) = LS ? dd[p] : out[p];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                float oa[16];
+                float lsum = 0.f;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    oa[v] = sc[arow(v) * 32 + r32];
+                    if constexpr (LS) {             // epi()'s loss expressions, in its order
+                        const float d = oa[v];
+                        const bool live = rb + arow(v) < Mv;
+                        lsum += live ? d * d : 0.f;
+                        oa[v] = live ? scale * d : 0.f;
+                    }
+                }
+                const int n = nb + r32;
+                if (CbTp) {                   // [n][b]: 4 consecutive rows per 8-byte store
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int b = rb + 8 * g + 4 * h;
+                        if (b < Mr) {
+                            const u32x2 w = {pack2_bf16(oa[4 * g], oa[4 * g + 1]),
+                                             pack2_bf16(oa[4 * g + 2], oa[4 * g + 3])};
+                            const int64_t at = kt ? ((int64_t)(b / kt) * Nc + n) * kt + b % kt
+                                                  : (int64_t)n * ldct + b;
+                            *reinterpret_cast<u32x2*>(CbTp + at) = w;
+                        }
+                    }
+                }
+                if (csp) {                    // one partial per 32-row block and column
+                    float cs = 0.f;
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) cs += oa[v];
+                    cs += __shfl_xor(cs, 32);
+                    if (h == 0 && rb < Mr) csp[(int64_t)(rb / 32) * Nc + n] = cs;
+                }
+                if constexpr (LS) {
+                    if (lpp) {
+#pragma unroll
+                        for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
+                        if (lane == 0 && rb < Mr)      // the block lies inside N here
+                            lpp[(int64_t)(rb / 32) * ((Nc + 31) / 32) + nb / 32] = lsum;
+                    }
+                }
+            }
+            asm volatile("" ::: "memory");
+        };
+        switch (mode) {
+            case LDM_GEMM_SILU: body(std::integral_constant<int, LDM_GEMM_SILU>{}); break;
+            case LDM_GEMM_RESID_SILU:
+                body(std::integral_constant<int, LDM_GEMM_RESID_SILU>{});
+                break;
+            case LDM_GEMM_RELU: body(std::integral_constant<int, LDM_GEMM_RELU>{}); break;
+            case LDM_GEMM_ACCUM: body(std::integral_constant<int, LDM_GEMM_ACCUM>{}); break;
+            case LDM_GEMM_DGRAD_SILU:
+                body(std::integral_constant<int, LDM_GEMM_DGRAD_SILU>{});
+                break;
+            case LDM_GEMM_LOSS: body(std::integral_constant<int, LDM_GEMM_LOSS>{}); break;
+            case LDM_GEMM_ADD_R: body(std::integral_constant<int, LDM_GEMM_ADD_R>{}); break;
+            case LDM_GEMM_RELU_BWD:
+                body(std::integral_constant<int, LDM_GEMM_RELU_BWD>{});
+                break;
+            default: body(std::integral_constant<int, LDM_GEMM_STORE>{}); break;
+        }
+    };
+
     // ---- epilogue ------------------------------------------------------------------------
     // Called once per accumulator tile with compile-time (i, j), so every acc index stays a
     // constant (a runtime-indexed accumulator array goes to scratch: guide rule 20).
@@ -296,13 +489,40 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         float* wsp = P.ws;
         int64_t ldr = P.ldr, ldpin = P.ldp_in, ldrb = P.ldrb, ldc = P.ldc, ldp = P.ldp,
                 ldcb = P.ldcb, ldct = P.ldct;
-        asm volatile("" : "+s"(mode), "+s"(Mv), "+s"(Mr), "+s"(Nc), "+s"(ksp), "+s"(kt),
-                     "+s"(scale));
-        asm volatile("" : "+s"(bias_p), "+s"(Rp), "+s"(Pin), "+s"(Rbp), "+s"(Cp), "+s"(Pp));
-        asm volatile("" : "+s"(Cbp), "+s"(CbTp), "+s"(csp), "+s"(lpp), "+s"(wsp));
-        asm volatile("" : "+s"(ldr), "+s"(ldpin), "+s"(ldrb), "+s"(ldc), "+s"(ldp), "+s"(ldcb),
-                     "+s"(ldct));
+        if constexpr (PERSIST) {
+            // (the non-persistent kernels take the LDS path below for every mode; there these
+            // pins broke the build: "illegal VGPR to SGPR copy")
+            asm volatile("" : "+s"(mode), "+s"(Mv), "+s"(Mr), "+s"(Nc), "+s"(ksp), "+s"(kt),
+                         "+s"(scale));
+            asm volatile("" : "+s"(bias_p), "+s"(Rp), "+s"(Pin), "+s"(Rbp), "+s"(Cp), "+s"(Pp));
+            asm volatile("" : "+s"(Cbp), "+s"(CbTp), "+s"(csp), "+s"(lpp), "+s"(wsp));
+            asm volatile("" : "+s"(ldr), "+s"(ldpin), "+s"(ldrb), "+s"(ldc), "+s"(ldp),
+                         "+s"(ldcb), "+s"(ldct));
+        }
         const int m0 = L.m0, n0 = L.n0;
+        if constexpr (!PERSIST) {
+            // LDS-transposed path (see the note above epi): uniform eligibility test
+            const int nb = n0 + wc * (BN / 2) + j * 32;        // first column of the block
+            auto al = [](const void* p, int a) {
+                return ((uintptr_t)p & (uintptr_t)(a - 1)) == 0;
+            };
+            bool ok = nb + 32 <= Nc;
+            if (ksp > 1) {
+                ok = ok && (Nc & 3) == 0 && al(wsp, 16);
+            } else {
+                ok = ok && (!Cp || (al(Cp, 16) && (ldc & 3) == 0)) &&
+                     (!Pp || (al(Pp, 16) && (ldp & 3) == 0)) &&
+                     (mode == LDM_GEMM_ACCUM || !Rp || (al(Rp, 16) && (ldr & 3) == 0)) &&
+                     (!Pin || (al(Pin, 16) && (ldpin & 3) == 0)) &&
+                     (!Cbp || (al(Cbp, 8) && (ldcb & 3) == 0)) &&
+                     (!Rbp || (al(Rbp, 8) && (ldrb & 3) == 0)) && (!bias_p || al(bias_p, 16));
+            }
+            if (ok) {
+                epi_lds(L, c, i, nb, mode, Mv, Mr, Nc, ksp, kt, scale, bias_p, Rp, Pin, Rbp, Cp,
+                        Pp, Cbp, CbTp, csp, lpp, wsp, ldr, ldpin, ldrb, ldc, ldp, ldcb, ldct);
+                return;
+            }
+        }
         const int rb = m0 + wr * (BM / 2) + i * 32;           // first row of this 32-row block
         const int n = n0 + wc * (BN / 2) + j * 32 + r32;
         const bool ncol = n < Nc;
@@ -449,7 +669,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
             default: body(E0{}); break;
         }
     };
-    auto epilogue = [&](const TileLoc& L, bool do0, bool do1) {
+        auto epilogue = [&](const TileLoc& L, bool do0, bool do1) {
         if (do0) {
             epi(L, acc[0][0], 0, 0);
             if constexpr (RN > 1) epi(L, acc[0][RN - 1], 0, 1);
@@ -579,6 +799,8 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         }
         if (RM == 1 && grp != 0) return;
     }
+    // the epilogue's LDS tiles overwrite ring slots other waves may still be reading
+    if constexpr (KG == 1 && !RS) __syncthreads();
     epilogue(L0, KG == 1 || RM == 1 || grp == 0, KG == 1 || grp == 1);
     }
 }
@@ -680,6 +902,11 @@ int gemm_tiles(const ldm_gemm_args_t& a, int bm, int bn) {
     return total;
 }
 
+int env_int(const char* name) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : 0;
+}
+
 int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     LDM_REQUIRE(a.n_prob >= 1 && a.n_prob <= LDM_GEMM_MAX_PROBS, LDM_EINVAL,
                 "ldm_gemm_bf16: n_prob %d", a.n_prob);
@@ -731,10 +958,13 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     // Automatic tile (profiles/r02k, gemm_bench.py; LDM_GEMM_TILE replaces it for tuning):
     //  * >= 2048 64 x 64 tiles (C19's 1M-row products): 128 x 64, register-staged (1.10 ms for
     //    1M x 512 x 512, 64 x 64 DMA 1.39 ms; larger tiles cut the per-CU operand bytes);
-    //  * else every K a multiple of 128 (config 2): 128-deep stages; one wave of workgroups
-    //    (<= 256 tiles) on 8 waves in two k-groups with a 4-deep ring (11.1 us for the block
-    //    GEMM 1000 x 1024 x 2048), more tiles at 2 workgroups per CU (2 stages, 64 KiB);
-    //  * else 64 x 64 on a 3-deep 64-k ring.
+    //  * <= 256 tiles with every K a multiple of 128 (config 2's forward): 128-deep stages on
+    //    8 waves in two k-groups with a 4-deep ring (11.1 us for the block GEMM 1000 x 1024 x
+    //    2048);
+    //  * else 64 x 64 on a 3-deep 64-k ring (48 KiB: 3 workgroups per CU, so config 2's
+    //    768-tile backward launches run in ONE wave of workgroups; the 128-deep 2-stage tile at
+    //    2 per CU left half a wave: the step 0.348 -> 0.317-0.326 ms, scripts/train_tiles2.sh,
+    //    profiles/r02h/train_tiles2.log).
     static const int forced = [] {
         const char* e = getenv("LDM_GEMM_TILE");
         return e ? atoi(e) : 0;
@@ -745,7 +975,12 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
         for (int p = 0; p < a.n_prob; ++p)
             for (int g = 0; g < a.prob[p].n_seg; ++g) k128 = k128 && a.prob[p].seg[g].K % 128 == 0;
         const int t64 = gemm_tiles(a, 64, 64);
-        tile = forced ? forced : t64 >= 2048 ? 15 : !k128 ? 4 : t64 <= 256 ? 24 : 20;
+        // tuning knobs per launch size class (tile counts at 64 x 64): <= 256, <= 512, < 2048
+        static const int by_size[3] = {env_int("LDM_GEMM_TILE_SMALL"),
+                                       env_int("LDM_GEMM_TILE_MID"), env_int("LDM_GEMM_TILE_BIG")};
+        const int cls = t64 <= 256 ? 0 : t64 <= 512 ? 1 : 2;
+        tile = forced ? forced : t64 >= 2048 ? 15 : by_size[cls] ? by_size[cls]
+             : (k128 && t64 <= 256) ? 24 : 4;
     }
     if (tile >= 20) {                          // 128-deep stages: every K a multiple of 128
         for (int p = 0; p < a.n_prob; ++p)

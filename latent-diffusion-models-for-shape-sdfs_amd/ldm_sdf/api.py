@@ -233,15 +233,28 @@ def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
     return loss, grads
 
 
+def _adam_table(denoiser: MLPDenoiser, state: TrainState, grads, dtype: str, device):
+    """ldm_adamw_multi descriptors: fp32 masters + Adam moments, and the bf16 working copies
+    (both layouts) the next step's GEMMs read."""
+    work = denoiser.device_pack(dtype, device, with_tables=False)
+    return ops.adamw_table(
+        [(p, grads[n], *state.adam[n], work[n] if n.startswith("W") else None,
+          work.get(n + "_T")) for n, p in state.masters.items()])
+
+
 def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, *, steps: int,
           batch: Optional[int] = None, lr: float = 1e-4, weight_decay: float = 0.0,
           dtype: str = "bf16", generator: Optional[torch.Generator] = None,
-          state: Optional[TrainState] = None, group=None) -> TrainState:
+          state: Optional[TrainState] = None, group=None, fused_step: bool = True,
+          overlap: bool = False) -> TrainState:
     """Train the denoiser on latent codes ``[M, D]`` (DDPM Alg. 1, eps-prediction, AdamW).
 
     fp32 master weights; forward/backward GEMMs read ``dtype`` copies (bf16 by default).
     Data parallel over the group's ranks (each rank its shard of every batch; gradients
-    all-reduced in one bucket).
+    all-reduced in one bucket).  On one rank with the built-in AdamW (bf16) each step is ONE C
+    call, ``ldm_denoiser_train_step_adamw`` (``fused_step``); ``overlap`` forks its weight
+    updates onto a side stream beside the backward's tail (measured slower at config 2, so off
+    by default).  Neither switch changes the results.
     """
     capi.require_device(latents)
     device = latents.device
@@ -262,6 +275,8 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
     grads = state.adam_grads if state.adam_grads is not None else \
         {n: torch.empty_like(v) for n, v in state.masters.items()}
     T = schedule.T
+    # single rank, built-in AdamW: the fused C step (no gradient all-reduce to wait for)
+    fused = dtype == "bf16" and state.optimizer is None and world == 1 and fused_step
     for _ in range(steps):
         # full-batch steps (batch == M) take the latents as they are: no index, no gather
         idx = torch.randint(0, M, (batch,), device=device, generator=generator) \
@@ -271,6 +286,27 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         lo, hi = ldist.batch_shard(batch, rank, world)
         x0 = latents[idx[lo:hi]].contiguous() if idx is not None else \
             latents[lo:hi].float().contiguous()
+        if fused:
+            # one C call for the whole step: forward, backward and AdamW, the block / in / out
+            # weight updates overlapping the backward's tail on a side stream (same bits as
+            # train_step + adamw_multi)
+            if state.adam_table is None:
+                state.adam_table = _adam_table(denoiser, state, grads, dtype, device)
+                state.adam_grads = grads
+            if state.adam_grads is not grads:
+                raise RuntimeError("train: gradient buffers changed under the AdamW table")
+            dev = denoiser.device_pack(dtype, device, with_tables=False)
+            ws = denoiser.train_workspace(hi - lo, device)
+            loss = torch.empty(1, device=device, dtype=torch.float32)
+            ops.denoiser_train_step_adamw(
+                dev["desc"], schedule.device(device)["desc"], x0.float().contiguous(),
+                eps[lo:hi].contiguous(), t[lo:hi].contiguous(), ws,
+                denoiser.grads_struct(grads), loss, state.adam_table,
+                lr=state.hparams["lr"], weight_decay=state.hparams["weight_decay"],
+                step=state.step + 1, overlap=overlap)
+            state.step += 1
+            state.losses.append(loss)
+            continue
         loss, grads = train_step(denoiser, schedule, x0, t[lo:hi], eps[lo:hi], dtype=dtype,
                                  grads=grads, group=group)
         if state.optimizer is not None:          # caller-supplied torch optimizer
@@ -282,10 +318,7 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
             # one launch for every tensor: fp32 masters + Adam moments, and the bf16 working
             # copies (both layouts) the next step's GEMMs read
             if state.adam_table is None:
-                work = denoiser.device_pack(dtype, device, with_tables=False)
-                state.adam_table = ops.adamw_table(
-                    [(p, grads[n], *state.adam[n], work[n] if n.startswith("W") else None,
-                      work.get(n + "_T")) for n, p in state.masters.items()])
+                state.adam_table = _adam_table(denoiser, state, grads, dtype, device)
                 state.adam_grads = grads
             if state.adam_grads is not grads:
                 raise RuntimeError("train: gradient buffers changed under the AdamW table")

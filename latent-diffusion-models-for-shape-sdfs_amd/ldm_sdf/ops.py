@@ -622,6 +622,37 @@ def denoiser_train_step(desc: capi.Denoiser, sched_desc: capi.Sched, x0: torch.T
                "ldm_denoiser_train_step")
 
 
+_side_streams: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def side_stream(device: torch.device) -> "torch.cuda.Stream":
+    """The second stream ``denoiser_train_step_adamw`` forks the early AdamW updates onto."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _side_streams:
+        _side_streams[idx] = torch.cuda.Stream(device=torch.device("cuda", idx))
+    return _side_streams[idx]
+
+
+def denoiser_train_step_adamw(desc: capi.Denoiser, sched_desc: capi.Sched, x0: torch.Tensor,
+                              eps: torch.Tensor, t: torch.Tensor, ws: torch.Tensor,
+                              gstruct: capi.DenoiserGrads, loss: torch.Tensor, table, *,
+                              lr: float, betas=(0.9, 0.999), adam_eps: float = 1e-8,
+                              weight_decay: float = 0.0, step: int, overlap: bool = False) -> None:
+    """One single-rank step: ``denoiser_train_step`` + ``adamw_multi`` over ``table`` in one
+    call (``ldm_denoiser_train_step_adamw``); ``overlap`` forks the updates onto a side stream
+    as their gradients become final.  Same bits as the two calls in sequence."""
+    _f32(x0, eps, loss)
+    _contig(x0, eps, t)
+    if t.dtype != torch.int32:
+        raise capi.LdmError("t must be int32")
+    side = side_stream(x0.device).cuda_stream if overlap else None
+    capi.check(capi.load().ldm_denoiser_train_step_adamw(
+        C.byref(desc), C.byref(sched_desc), x0.data_ptr(), eps.data_ptr(), t.data_ptr(),
+        x0.shape[0], ws.data_ptr(), C.byref(gstruct), loss.data_ptr(), table, len(table),
+        float(lr), float(betas[0]), float(betas[1]), float(adam_eps), float(weight_decay),
+        int(step), capi.stream_handle(x0.device), side), "ldm_denoiser_train_step_adamw")
+
+
 def denoiser_fwd(desc: capi.Denoiser, x: torch.Tensor, t: torch.Tensor, ws: torch.Tensor,
                  eps_out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """Training forward with per-sample t (``ldm_denoiser_fwd``), activations saved in ws."""

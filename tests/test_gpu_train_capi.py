@@ -250,3 +250,37 @@ def test_train_bf16_loop_learns_and_matches_torch_adamw(dev, net):
     assert max(abs(a - b) for a, b in zip(la, lb)) <= 1e-3 * max(lb)
     for n in pa:
         assert (pa[n] - pb[n]).abs().max() <= 3e-3 * pb[n].abs().max() + 1e-6, n
+
+
+def test_train_step_adamw_fused_overlap_bitwise(dev, net):
+    """ldm_denoiser_train_step_adamw (early weight updates forked onto a side stream) ==
+    the same entry point serialised (side = NULL) == ldm_denoiser_train_step + ldm_adamw_multi,
+    bit for bit: losses, fp32 masters, Adam moments and both bf16 working copies."""
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser
+    _, p = net
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"], params[f"bblk{k}"] = p.Wblk[k], p.bblk[k]
+    lat = torch.randn(300, 256, generator=torch.Generator().manual_seed(5)).to(dev) * 0.5
+    sch = ldm_sdf.DDPMSchedule()
+    runs = []
+    for fused, overlap in ((True, True), (True, False), (False, False)):
+        model = MLPDenoiser(params={k: v.clone() for k, v in params.items()})
+        model.to_device(dev)
+        st = ldm_sdf.train(model, sch, lat, steps=6, batch=300, lr=1e-3, weight_decay=0.01,
+                           dtype="bf16", generator=torch.Generator(device=dev).manual_seed(3),
+                           fused_step=fused, overlap=overlap)
+        work = model.device_pack("bf16", dev, with_tables=False)
+        runs.append((list(st.losses), {n: t.clone() for n, t in model.params.items()},
+                     {n: (m.clone(), v.clone()) for n, (m, v) in st.adam.items()},
+                     {n: t.clone() for n, t in work.items() if isinstance(t, torch.Tensor)}))
+    torch.cuda.synchronize()
+    ref = runs[-1]
+    for r in runs[:-1]:
+        assert r[0] == ref[0]
+        for n in ref[1]:
+            assert torch.equal(r[1][n], ref[1][n]), n
+            assert torch.equal(r[2][n][0], ref[2][n][0]) and torch.equal(r[2][n][1], ref[2][n][1])
+        for n in ref[3]:
+            assert torch.equal(r[3][n], ref[3][n]), n
