@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--no-ddpm", action="store_true")
     ap.add_argument("--ddpm-batch", type=int, default=8)
     ap.add_argument("--no-train", action="store_true")
-    ap.add_argument("--train-steps", type=int, default=20)
+    ap.add_argument("--train-steps", type=int, default=100)
     ap.add_argument("--no-config5", action="store_true",
                     help="skip config 5 (1D-UNet sampling on 1024-d latents -> fp16 decode "
                          "of a 512^3 grid with the widen-skip decoder)")

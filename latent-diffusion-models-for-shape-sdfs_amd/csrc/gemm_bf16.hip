@@ -36,6 +36,21 @@ namespace {
 
 constexpr int kBK = 64;                 // k per ring stage (128 B per operand row)
 
+// A wave-uniform value made opaque in an SGPR (v_readfirstlane): the compiler can neither
+// re-materialise it as a kernarg load nor move it to a VGPR.
+template <typename T>
+__device__ __forceinline__ T pin_s(T v) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+    } else {
+        static_assert(sizeof(T) == 8, "pin_s: 4- or 8-byte values");
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+    }
+}
+
 __device__ __forceinline__ unsigned pack2_bf16(float a, float b) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const f32x2 v = {a, b};
@@ -293,7 +308,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                        unsigned short* Cbp, unsigned short* CbTp, float* csp, float* lpp,
                        float* wsp, const int64_t ldr, const int64_t ldpin, const int64_t ldrb,
                        const int64_t ldc, const int64_t ldp, const int64_t ldcb,
-                       const int64_t ldct) {
+                       const int64_t ldct) __attribute__((always_inline)) {
         const int rb = L.m0 + wr * (BM / 2) + i * 32;      // first row of this 32-row block
         float* sc = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + EPI_LDS_OFF) +
                     wave * 1024;
@@ -349,56 +364,56 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                 if constexpr (XB)
                     vb[p] = *reinterpret_cast<const u32x2*>(Rbp + (int64_t)bb * ldrb + n4);
             }
-            f32x4 out[4], pre_v[4], dh[4], dd[4];
+            // one row at a time from the batched operand loads: only the values the write-back
+            // needs (keep) live across rows (the 128 x 128 kernels spilled with all of it live)
+            f32x4 keep[4];
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
-                const bool live = rb + rl + 8 * p < Mv;
+                const int b = rb + rl + 8 * p;
+                const bool live = b < Mv;
+                f32x4 out, pre_v, dh, dd;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {      // epi()'s expressions, element for element
                     const float pre = cv[p][e] + bias4[e];
-                    pre_v[p][e] = pre;
+                    pre_v[e] = pre;
                     float o = pre;
-                    dh[p][e] = 0.f;
-                    dd[p][e] = 0.f;
+                    dh[e] = 0.f;
+                    dd[e] = 0.f;
                     if constexpr (MODE == LDM_GEMM_SILU) o = silu(pre);
                     if constexpr (MODE == LDM_GEMM_RESID_SILU) o = v1[p][e] + silu(pre);
                     if constexpr (MODE == LDM_GEMM_RELU) o = fmaxf(pre, 0.f);
                     if constexpr (MODE == LDM_GEMM_ACCUM || MODE == LDM_GEMM_ADD_R)
                         o = v1[p][e] + pre;
                     if constexpr (MODE == LDM_GEMM_DGRAD_SILU) {
-                        dh[p][e] = v1[p][e] + pre;
-                        o = dh[p][e] * silu_grad(v2[p][e]);
+                        dh[e] = v1[p][e] + pre;
+                        o = dh[e] * silu_grad(v2[p][e]);
                     }
                     if constexpr (LS) {
-                        dd[p][e] = pre - v2[p][e];
-                        o = scale * dd[p][e];
+                        dd[e] = pre - v2[p][e];
+                        o = scale * dd[e];
                     }
                     if constexpr (MODE == LDM_GEMM_RELU_BWD) {
                         const unsigned u = (vb[p][e >> 1] >> (16 * (e & 1))) & 0xffffu;
                         o = (u != 0 && (u & 0x8000u) == 0) ? pre : 0.f;
                     }
-                    out[p][e] = live ? o : 0.f;
+                    out[e] = live ? o : 0.f;
                 }
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int b = rb + rl + 8 * p;
-                if (Cp && b < Mv)
+                if (Cp && live)
                     *reinterpret_cast<f32x4*>(Cp + (int64_t)b * ldc + n4) =
-                        MODE == LDM_GEMM_DGRAD_SILU ? dh[p] : out[p];
+                        MODE == LDM_GEMM_DGRAD_SILU ? dh : out;
                 if constexpr (MODE == LDM_GEMM_SILU || MODE == LDM_GEMM_RESID_SILU) {
-                    if (Pp && b < Mv)
-                        *reinterpret_cast<f32x4*>(Pp + (int64_t)b * ldp + n4) = pre_v[p];
+                    if (Pp && live) *reinterpret_cast<f32x4*>(Pp + (int64_t)b * ldp + n4) = pre_v;
                 }
                 if (Cbp && b < Mr)
-                    *reinterpret_cast<u32x2*>(Cbp + (int64_t)b * ldcb + n4) = u32x2{
-                        pack2_bf16(out[p][0], out[p][1]), pack2_bf16(out[p][2], out[p][3])};
+                    *reinterpret_cast<u32x2*>(Cbp + (int64_t)b * ldcb + n4) =
+                        u32x2{pack2_bf16(out[0], out[1]), pack2_bf16(out[2], out[3])};
+                keep[p] = LS ? dd : out;
             }
             if (CbTp || csp || (LS && lpp)) {   // back to accumulator layout through the tile
                 asm volatile("" ::: "memory");
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
-                    *reinterpret_cast<f32x4*>(sc + (rl + 8 * p) * 32 + cq) = LS ? dd[p] : out[p];
+                    *reinterpret_cast<f32x4*>(sc + (rl + 8 * p) * 32 + cq) = keep[p];
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 float oa[16];
                 float lsum = 0.f;
@@ -471,7 +486,8 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     // and the mode is dispatched once per tile to a body specialised at compile time.  The
     // generic form re-read the argument block after every store and branched on the mode per
     // element: an s_load round trip per element, ~20 us per 128 x 128 tile (profiles/r02*).
-    auto epi = [&](const TileLoc& L, const f32x16& c, const int i, const int j) {
+    auto epi = [&](const TileLoc& L, const f32x16& c, const int i, const int j)
+                   __attribute__((always_inline)) {
         KProb& P = ka->prob[L.p];
         int mode = P.mode, Mv = P.M_valid, Mr = P.M, Nc = P.N, ksp = ka->ksplit[L.p];
         int kt = P.ct_blk;
@@ -489,18 +505,10 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         float* wsp = P.ws;
         int64_t ldr = P.ldr, ldpin = P.ldp_in, ldrb = P.ldrb, ldc = P.ldc, ldp = P.ldp,
                 ldcb = P.ldcb, ldct = P.ldct;
-        if constexpr (PERSIST) {
-            // (the non-persistent kernels take the LDS path below for every mode; there these
-            // pins broke the build: "illegal VGPR to SGPR copy")
-            asm volatile("" : "+s"(mode), "+s"(Mv), "+s"(Mr), "+s"(Nc), "+s"(ksp), "+s"(kt),
-                         "+s"(scale));
-            asm volatile("" : "+s"(bias_p), "+s"(Rp), "+s"(Pin), "+s"(Rbp), "+s"(Cp), "+s"(Pp));
-            asm volatile("" : "+s"(Cbp), "+s"(CbTp), "+s"(csp), "+s"(lpp), "+s"(wsp));
-            asm volatile("" : "+s"(ldr), "+s"(ldpin), "+s"(ldrb), "+s"(ldc), "+s"(ldp),
-                         "+s"(ldcb), "+s"(ldct));
-        }
         const int m0 = L.m0, n0 = L.n0;
-        if constexpr (!PERSIST) {
+        // (128 x 128 tiles keep the accumulator-layout stores: with the LDS path inlined four
+        // times the compiler put 460 B per lane in scratch)
+        if constexpr (!PERSIST && !(RM == 2 && RN == 2)) {
             // LDS-transposed path (see the note above epi): uniform eligibility test
             const int nb = n0 + wc * (BN / 2) + j * 32;        // first column of the block
             auto al = [](const void* p, int a) {
@@ -523,6 +531,14 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                 return;
             }
         }
+        // accumulator-layout path: pin every field in SGPRs (see above; readfirstlane rather
+        // than an empty "+s" asm, which the build rejected next to the LDS path)
+        mode = pin_s(mode); Mv = pin_s(Mv); Mr = pin_s(Mr); Nc = pin_s(Nc); ksp = pin_s(ksp);
+        kt = pin_s(kt); scale = pin_s(scale); bias_p = pin_s(bias_p); Rp = pin_s(Rp);
+        Pin = pin_s(Pin); Rbp = pin_s(Rbp); Cp = pin_s(Cp); Pp = pin_s(Pp); Cbp = pin_s(Cbp);
+        CbTp = pin_s(CbTp); csp = pin_s(csp); lpp = pin_s(lpp); wsp = pin_s(wsp);
+        ldr = pin_s(ldr); ldpin = pin_s(ldpin); ldrb = pin_s(ldrb); ldc = pin_s(ldc);
+        ldp = pin_s(ldp); ldcb = pin_s(ldcb); ldct = pin_s(ldct);
         const int rb = m0 + wr * (BM / 2) + i * 32;           // first row of this 32-row block
         const int n = n0 + wc * (BN / 2) + j * 32 + r32;
         const bool ncol = n < Nc;
