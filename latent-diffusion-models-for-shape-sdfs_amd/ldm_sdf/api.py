@@ -277,18 +277,26 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
     T = schedule.T
     # single rank, built-in AdamW: the fused C step (no gradient all-reduce to wait for)
     fused = dtype == "bf16" and state.optimizer is None and world == 1 and fused_step
-    for _ in range(steps):
-        # full-batch steps (batch == M) take the latents as they are: no index, no gather
-        idx = torch.randint(0, M, (batch,), device=device, generator=generator) \
-            if batch != M else None
-        t = torch.randint(0, T, (batch,), device=device, generator=generator, dtype=torch.int32)
-        eps = torch.randn(batch, D, device=device, generator=generator)
+    chunk = 32           # steps whose random draws are made in one launch each
+    for s in range(steps):
+        j = s % chunk
+        if j == 0:
+            # the draws of the next `chunk` steps (t, eps, and the batch indices when the batch
+            # is a sample of the latents) in three launches instead of two or three per step;
+            # full-batch steps (batch == M) take the latents as they are: no index, no gather
+            n = min(chunk, steps - s)
+            idx_all = torch.randint(0, M, (n, batch), device=device, generator=generator) \
+                if batch != M else None
+            t_all = torch.randint(0, T, (n, batch), device=device, generator=generator,
+                                  dtype=torch.int32)
+            eps_all = torch.randn(n, batch, D, device=device, generator=generator)
+        idx = idx_all[j] if idx_all is not None else None
+        t, eps = t_all[j], eps_all[j]
         lo, hi = ldist.batch_shard(batch, rank, world)
         x0 = latents[idx[lo:hi]].contiguous() if idx is not None else \
             latents[lo:hi].float().contiguous()
         if fused:
-            # one C call for the whole step: forward, backward and AdamW, the block / in / out
-            # weight updates overlapping the backward's tail on a side stream (same bits as
+            # one C call for the whole step: forward, backward and AdamW (same bits as
             # train_step + adamw_multi)
             if state.adam_table is None:
                 state.adam_table = _adam_table(denoiser, state, grads, dtype, device)
