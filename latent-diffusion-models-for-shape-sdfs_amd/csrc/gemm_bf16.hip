@@ -991,11 +991,13 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
         for (int p = 0; p < a.n_prob; ++p)
             for (int g = 0; g < a.prob[p].n_seg; ++g) k128 = k128 && a.prob[p].seg[g].K % 128 == 0;
         const int t64 = gemm_tiles(a, 64, 64);
-        // tuning knobs per launch size class (tile counts at 64 x 64): <= 256, <= 512, < 2048
-        static const int by_size[3] = {env_int("LDM_GEMM_TILE_SMALL"),
-                                       env_int("LDM_GEMM_TILE_MID"), env_int("LDM_GEMM_TILE_BIG")};
-        const int cls = t64 <= 256 ? 0 : t64 <= 512 ? 1 : 2;
-        tile = forced ? forced : t64 >= 2048 ? 15 : by_size[cls] ? by_size[cls]
+        // tuning knobs per launch size class (tile counts at 64 x 64): <= 256, <= 512, < 2048,
+        // >= 2048
+        static const int by_size[4] = {env_int("LDM_GEMM_TILE_SMALL"),
+                                       env_int("LDM_GEMM_TILE_MID"), env_int("LDM_GEMM_TILE_BIG"),
+                                       env_int("LDM_GEMM_TILE_HUGE")};
+        const int cls = t64 <= 256 ? 0 : t64 <= 512 ? 1 : t64 < 2048 ? 2 : 3;
+        tile = forced ? forced : by_size[cls] ? by_size[cls] : t64 >= 2048 ? 15
              : (k128 && t64 <= 256) ? 24 : 4;
     }
     if (tile >= 20) {                          // 128-deep stages: every K a multiple of 128
