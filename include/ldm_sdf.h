@@ -238,8 +238,16 @@ int ldm_denoiser_train_step_adamw(const ldm_denoiser_t* w, const ldm_sched_t* sc
                                   void* saved, const ldm_denoiser_grads_t* grads,
                                   float* loss_out, const ldm_adamw_tensor_t* tensors, int n,
                                   double lr, double beta1, double beta2, double eps_adam,
-                                  double weight_decay, int step, ldm_stream_t s,
-                                  ldm_stream_t side);
+                                  double weight_decay, int step, const float* d_hyper,
+                                  ldm_stream_t s, ldm_stream_t side);
+/* d_hyper (may be NULL): a DEVICE array of the 7 AdamW scalars ldm_adamw_hyper computes for
+ * (lr, beta1, beta2, eps_adam, weight_decay, step); the kernels read them from there instead
+ * of the arguments, so a hipGraph captured once replays every step (the caller refills it).
+ * ldm_adamw_hyper: host-only, the scalars exactly as the argument path derives them
+ * (double, rounded once): [1 - lr wd, 1 - beta1, beta2, 1 - beta2, eps, lr / (1 - beta1^step),
+ * sqrt(1 - beta2^step)]. */
+void ldm_adamw_hyper(double lr, double beta1, double beta2, double eps, double weight_decay,
+                     int step, float* out7);
 /* AdamW on fp32 masters p [n] with grads g, moments m, v (torch.optim.AdamW's order; step is
  * 1-based).  p_bf16 (may be NULL): bf16 [n] working copy of the updated p, written in the same
  * pass (RNE). */

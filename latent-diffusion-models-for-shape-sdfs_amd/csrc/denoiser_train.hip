@@ -480,6 +480,7 @@ struct AdamJobs {
     int first[LDM_ADAMW_MAX_TENSORS + 1];
     int n;
     float decay, omb1, b2, omb2, eps, step_size, bc2_sqrt;
+    const float* dh;    // non-null: the 7 scalars above are read from device memory instead
 };
 
 typedef const __attribute__((address_space(4))) AdamJobs KJobs;
@@ -509,8 +510,11 @@ __device__ __forceinline__ void adamw_tile(KJ* kj, unsigned short (&sT)[64][64 +
     const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
     const int tid = threadIdx.x;
     const int cq = (tid & 15) * 4;
-    const float decay = kj->decay, omb1 = kj->omb1, b2 = kj->b2, omb2 = kj->omb2;
-    const float eps = kj->eps, step_size = kj->step_size, bc2_sqrt = kj->bc2_sqrt;
+    const float* dh = kj->dh;
+    const float decay = dh ? dh[0] : kj->decay, omb1 = dh ? dh[1] : kj->omb1;
+    const float b2 = dh ? dh[2] : kj->b2, omb2 = dh ? dh[3] : kj->omb2;
+    const float eps = dh ? dh[4] : kj->eps, step_size = dh ? dh[5] : kj->step_size;
+    const float bc2_sqrt = dh ? dh[6] : kj->bc2_sqrt;
     float* __restrict__ P = T.p;
     const float* __restrict__ Gp = T.g;
     float* __restrict__ M = T.m;
@@ -601,9 +605,26 @@ __device__ __forceinline__ void adamw_tile(KJ* kj, unsigned short (&sT)[64][64 +
 namespace ldm {
 namespace {
 // One adamw_multi_kernel launch over the tensors list[0..n) (host descriptors).
+// The update's scalars, derived in double and rounded once, as ldm_adamw_step (and torch) do:
+// [decay, 1 - beta1, beta2, 1 - beta2, eps, lr / bc1, sqrt(bc2)].
+void adamw_hyper(double lr, double beta1, double beta2, double eps, double weight_decay,
+                 int step, float* o) {
+    const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
+    o[0] = (float)(1.0 - lr * weight_decay);
+    o[1] = (float)(1.0 - beta1);
+    o[2] = (float)beta2;
+    o[3] = (float)(1.0 - beta2);
+    o[4] = (float)eps;
+    o[5] = (float)(lr / bc1);
+    o[6] = (float)sqrt(bc2);
+}
+
+// One adamw_multi_kernel launch over the tensors list[0..n) (host descriptors); d_hyper
+// (optional): device copy of adamw_hyper's 7 scalars, read by the kernel instead (a captured
+// graph then replays with new step counts).
 int adamw_launch(const ldm_adamw_tensor_t* const* list, int n, double lr, double beta1,
                  double beta2, double eps, double weight_decay, int step, hipStream_t s,
-                 int grid_cap = 0) {
+                 int grid_cap = 0, const float* d_hyper = nullptr) {
     if (n == 0) return 0;
     AdamJobs J;
     memset(&J, 0, sizeof(J));
@@ -618,15 +639,11 @@ int adamw_launch(const ldm_adamw_tensor_t* const* list, int n, double lr, double
     }
     J.first[n] = tiles;
     J.n = n;
-    // scalars derived in double and rounded once, as ldm_adamw_step (and torch) do
-    const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
-    J.decay = (float)(1.0 - lr * weight_decay);
-    J.omb1 = (float)(1.0 - beta1);
-    J.b2 = (float)beta2;
-    J.omb2 = (float)(1.0 - beta2);
-    J.eps = (float)eps;
-    J.step_size = (float)(lr / bc1);
-    J.bc2_sqrt = (float)sqrt(bc2);
+    float h[7];
+    adamw_hyper(lr, beta1, beta2, eps, weight_decay, step, h);
+    J.decay = h[0]; J.omb1 = h[1]; J.b2 = h[2]; J.omb2 = h[3]; J.eps = h[4];
+    J.step_size = h[5]; J.bc2_sqrt = h[6];
+    J.dh = d_hyper;
     const int grid = grid_cap > 0 && grid_cap < tiles ? grid_cap : tiles;
     hipLaunchKernelGGL(adamw_multi_kernel, dim3(grid), dim3(256), 0, s, J);
     return launch_status("ldm_adamw_multi");
@@ -662,6 +679,7 @@ struct AdamSplit {
     int nb[kForks];
     double lr, beta1, beta2, eps, wd;
     int step, grid_cap;
+    const float* d_hyper;
     hipStream_t side;
     hipEvent_t ev[kForks + 1];
 };
@@ -676,7 +694,7 @@ int adam_batch(AdamSplit& A, int i, hipStream_t s) {
         q = A.side;
     }
     return adamw_launch(A.batch[i], A.nb[i], A.lr, A.beta1, A.beta2, A.eps, A.wd, A.step, q,
-                        A.side ? A.grid_cap : 0);
+                        A.side ? A.grid_cap : 0, A.d_hyper);
 }
 
 int adam_hook(void* ctx, int point, hipStream_t s) {
@@ -699,7 +717,8 @@ extern "C" int ldm_denoiser_train_step_adamw(
     const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, const float* eps,
     const int32_t* t, int B, void* saved, const ldm_denoiser_grads_t* grads, float* loss_out,
     const ldm_adamw_tensor_t* tensors, int n, double lr, double beta1, double beta2,
-    double eps_adam, double weight_decay, int step, ldm_stream_t s, ldm_stream_t side) {
+    double eps_adam, double weight_decay, int step, const float* d_hyper, ldm_stream_t s,
+    ldm_stream_t side) {
     LDM_TRY(check_desc(w, B, true));
     LDM_TRY(check_grads(w, grads));
     LDM_REQUIRE(sc && sc->abi_version == LDM_ABI_VERSION && sc->sqrt_ab && sc->sqrt_1mab,
@@ -714,6 +733,7 @@ extern "C" int ldm_denoiser_train_step_adamw(
     memset(&A, 0, sizeof(A));
     A.lr = lr; A.beta1 = beta1; A.beta2 = beta2; A.eps = eps_adam; A.wd = weight_decay;
     A.step = step;
+    A.d_hyper = d_hyper;
     A.side = side == s ? nullptr : (hipStream_t)side;
     if (A.side) {
         LDM_TRY(fork_events(A.ev));
@@ -747,4 +767,9 @@ extern "C" int ldm_denoiser_train_step_adamw(
                         hipStreamWaitEvent(st, A.ev[kForks], 0) == hipSuccess,
                     LDM_EINVAL, "train_step_adamw: join failed");
     return 0;
+}
+
+extern "C" void ldm_adamw_hyper(double lr, double beta1, double beta2, double eps,
+                                double weight_decay, int step, float* out7) {
+    ldm::adamw_hyper(lr, beta1, beta2, eps, weight_decay, step, out7);
 }

@@ -180,7 +180,10 @@ SIGNATURES = [
     ("ldm_denoiser_train_step_adamw", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _vp,
                                            _i, _vp, C.POINTER(DenoiserGrads), _fp,
                                            C.POINTER(AdamwTensor), _i, C.c_double, C.c_double,
-                                           C.c_double, C.c_double, C.c_double, _i, _vp, _vp]),
+                                           C.c_double, C.c_double, C.c_double, _i, _vp, _vp,
+                                           _vp]),
+    ("ldm_adamw_hyper", None, [C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, _i,
+                               _fp]),
     ("ldm_mc_workspace_bytes", _sz, [_i]),
     ("ldm_mc_count", _i, [_fp, _i, _f, _vp, _sz, _vp, _vp]),
     ("ldm_mc_emit", _i, [_fp, _i, _f, _f, _f, _vp, _sz, _fp, _vp, _vp]),

@@ -197,6 +197,8 @@ class TrainState:
     hparams: Dict[str, float] = field(default_factory=dict)
     adam_table: Optional[object] = None     # ldm_adamw_multi descriptors (bf16 path)
     adam_grads: Optional[Dict[str, torch.Tensor]] = None
+    adam_pack: Optional[Dict[str, object]] = None    # the device pack the table points into
+    graphs: Optional[Dict[str, object]] = None       # captured steps (train(graph=True))
 
 
 def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
@@ -246,7 +248,7 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
           batch: Optional[int] = None, lr: float = 1e-4, weight_decay: float = 0.0,
           dtype: str = "bf16", generator: Optional[torch.Generator] = None,
           state: Optional[TrainState] = None, group=None, fused_step: bool = True,
-          overlap: bool = False) -> TrainState:
+          overlap: bool = False, graph: bool = False) -> TrainState:
     """Train the denoiser on latent codes ``[M, D]`` (DDPM Alg. 1, eps-prediction, AdamW).
 
     fp32 master weights; forward/backward GEMMs read ``dtype`` copies (bf16 by default).
@@ -254,7 +256,11 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
     all-reduced in one bucket).  On one rank with the built-in AdamW (bf16) each step is ONE C
     call, ``ldm_denoiser_train_step_adamw`` (``fused_step``); ``overlap`` forks its weight
     updates onto a side stream beside the backward's tail (measured slower at config 2, so off
-    by default).  Neither switch changes the results.
+    by default).  ``graph``: full-batch single-rank steps replay hipGraphs of that call, one
+    per slot of a 32-step chunk (t, eps and the AdamW scalars in device buffers refilled per
+    chunk), captured once per state; measured 3% slower than the eager calls at config 2
+    (3030 vs 3115 steps/s, scripts/train_ab.py), so off by default.  No switch changes the
+    results.
     """
     capi.require_device(latents)
     device = latents.device
@@ -278,6 +284,15 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
     # single rank, built-in AdamW: the fused C step (no gradient all-reduce to wait for)
     fused = dtype == "bf16" and state.optimizer is None and world == 1 and fused_step
     chunk = 32           # steps whose random draws are made in one launch each
+    if dtype == "bf16" and state.optimizer is None:
+        pack = denoiser.device_pack(dtype, device, with_tables=False)
+        if state.adam_table is None or state.adam_pack is not pack:
+            # (re)build the AdamW table for this pack; graphs captured on the old one are void
+            state.adam_table = _adam_table(denoiser, state, grads, dtype, device)
+            state.adam_grads, state.adam_pack, state.graphs = grads, pack, None
+    if fused and graph and batch == M and not overlap:
+        _train_graphed(denoiser, schedule, latents, steps, state, grads, generator, chunk)
+        steps = 0
     for s in range(steps):
         j = s % chunk
         if j == 0:
@@ -298,9 +313,6 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         if fused:
             # one C call for the whole step: forward, backward and AdamW (same bits as
             # train_step + adamw_multi)
-            if state.adam_table is None:
-                state.adam_table = _adam_table(denoiser, state, grads, dtype, device)
-                state.adam_grads = grads
             if state.adam_grads is not grads:
                 raise RuntimeError("train: gradient buffers changed under the AdamW table")
             dev = denoiser.device_pack(dtype, device, with_tables=False)
@@ -324,10 +336,7 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
             denoiser.invalidate()
         elif dtype == "bf16":
             # one launch for every tensor: fp32 masters + Adam moments, and the bf16 working
-            # copies (both layouts) the next step's GEMMs read
-            if state.adam_table is None:
-                state.adam_table = _adam_table(denoiser, state, grads, dtype, device)
-                state.adam_grads = grads
+            # copies (both layouts) the next step's GEMMs read (table built above)
             if state.adam_grads is not grads:
                 raise RuntimeError("train: gradient buffers changed under the AdamW table")
             ops.adamw_multi(state.adam_table, lr=state.hparams["lr"],
@@ -346,8 +355,9 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         state.step += 1
         state.losses.append(loss)
     if state.optimizer is None:
-        denoiser.invalidate()    # E tables (sampling) are rebuilt from the trained masters
-        state.adam_table = None  # ... and so are the working copies the table pointed at
+        # the built-in AdamW kept every working copy current: only the E tables (sampling) are
+        # rebuilt from the trained weights, so the AdamW table and captured graphs stay valid
+        denoiser.invalidate_tables()
     # one device->host transfer for the whole run, not one per step
     pend = [i for i, l in enumerate(state.losses) if isinstance(l, torch.Tensor)]
     if pend:
@@ -355,3 +365,78 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         for i, v in zip(pend, vals):
             state.losses[i] = v
     return state
+
+
+def _train_graphed(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor,
+                   steps: int, state: TrainState, grads, generator, chunk: int) -> None:
+    """Full-batch single-rank bf16 steps as hipGraph replays of
+    ``ldm_denoiser_train_step_adamw``: one graph per slot j of a ``chunk``-step block reads
+    t / eps / the AdamW scalars of slot j from device buffers that are refilled once per block
+    (the same random draws, in the same order, as the eager loop; the scalars from
+    ``ldm_adamw_hyper``, the values the argument path uses), so results are bit-identical.
+    Slots run eagerly until their graph exists; every slot is captured after the first block."""
+    device = latents.device
+    M, D = latents.shape
+    T = schedule.T
+    dev = denoiser.device_pack("bf16", device, with_tables=False)
+    ws = denoiser.train_workspace(M, device)
+    sdesc = schedule.device(device)["desc"]
+    x0 = latents.float().contiguous()
+    key = (x0.data_ptr(), ws.data_ptr(), M, D, T, sdesc.sqrt_ab, chunk)
+    G = state.graphs
+    if G is None or G["key"] != key:
+        G = {"key": key, "x0": x0, "ws": ws,
+             "t": torch.empty(chunk, M, device=device, dtype=torch.int32),
+             "eps": torch.empty(chunk, M, D, device=device, dtype=torch.float32),
+             "hyper": torch.zeros(chunk, 8, device=device, dtype=torch.float32),
+             "loss": torch.zeros(chunk, device=device, dtype=torch.float32),
+             # two pinned host staging buffers for the scalars, each reused only after the
+             # event of its previous copy (a pageable copy would stall the host every block)
+             "hyper_host": [torch.zeros(chunk, 8, dtype=torch.float32).pin_memory()
+                            for _ in range(2)],
+             "hyper_ev": [None, None], "block": 0,
+             "g": [None] * chunk}
+        state.graphs = G
+    gstruct = denoiser.grads_struct(grads)
+    hp = state.hparams
+
+    def call(j: int, step: int) -> None:
+        ops.denoiser_train_step_adamw(
+            dev["desc"], sdesc, x0, G["eps"][j], G["t"][j], ws, gstruct, G["loss"][j:j + 1],
+            state.adam_table, lr=hp["lr"], weight_decay=hp["weight_decay"], step=step,
+            hyper=G["hyper"][j])
+
+    s = 0
+    while s < steps:
+        n = min(chunk, steps - s)
+        torch.randint(0, T, (n, M), generator=generator, out=G["t"][:n])
+        torch.randn((n, M, D), generator=generator, out=G["eps"][:n])
+        hb = G["block"] & 1
+        G["block"] += 1
+        if G["hyper_ev"][hb] is not None:
+            G["hyper_ev"][hb].synchronize()
+        host = G["hyper_host"][hb]
+        host[:n] = torch.tensor([ops.adamw_hyper(lr=hp["lr"], weight_decay=hp["weight_decay"],
+                                                 step=state.step + 1 + j) + [0.0]
+                                 for j in range(n)], dtype=torch.float32)
+        G["hyper"][:n].copy_(host[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        G["hyper_ev"][hb] = ev
+        for j in range(n):
+            if G["g"][j] is None:
+                call(j, state.step + 1 + j)
+            else:
+                G["g"][j].replay()
+        losses = G["loss"][:n].clone()
+        state.losses.extend(losses[j:j + 1] for j in range(n))
+        state.step += n
+        s += n
+        if any(g is None for g in G["g"]):
+            # capture executes nothing; the slots' next use replays
+            for j in range(chunk):
+                if G["g"][j] is None:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        call(j, 1)
+                    G["g"][j] = g

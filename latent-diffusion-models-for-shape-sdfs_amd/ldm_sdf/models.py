@@ -259,6 +259,16 @@ class MLPDenoiser:
         """Call after the fp32 masters changed (training): drops packed copies / E tables."""
         self._dev.clear()
 
+    def invalidate_tables(self) -> None:
+        """Call after training that kept the working copies current (the built-in AdamW
+        rewrites them every step): drops only the E tables, which the next sampling pack
+        rebuilds from the trained weights; the working copies (and graphs that captured their
+        addresses) stay valid."""
+        for dev in self._dev.values():
+            old = [dev.pop(f"etab{k}") for k in range(self.n_blocks) if f"etab{k}" in dev]
+            if old:             # kept alive: a descriptor handed out earlier still points there
+                dev["_stale_etab"] = old
+
     def make_stepper(self, n: int, dtype: str, device, sched_desc):
         """Callable ``step(x, z, t, x_out)``: one fused reverse step (``ldm_sample_step``)."""
         from . import ops
@@ -292,6 +302,14 @@ class MLPDenoiser:
         key = (dtype, device)
         if key in self._dev and ("etab0" in self._dev[key] or not with_tables):
             return self._dev[key]
+        if key in self._dev:                    # tables dropped by invalidate_tables
+            dev = self._dev[key]
+            from .ops import build_e_tables
+            tabs = build_e_tables(self, dev, dtype)
+            for k in range(self.n_blocks):
+                dev[f"etab{k}"] = tabs[k]
+                dev["desc"].e_tab[k] = tabs[k].data_ptr()
+            return dev
         wdt = {"fp32": torch.float32, "bf16": torch.bfloat16}[dtype]
         dev: Dict[str, object] = {}
         for n, v in self.params.items():

@@ -637,10 +637,13 @@ def denoiser_train_step_adamw(desc: capi.Denoiser, sched_desc: capi.Sched, x0: t
                               eps: torch.Tensor, t: torch.Tensor, ws: torch.Tensor,
                               gstruct: capi.DenoiserGrads, loss: torch.Tensor, table, *,
                               lr: float, betas=(0.9, 0.999), adam_eps: float = 1e-8,
-                              weight_decay: float = 0.0, step: int, overlap: bool = False) -> None:
+                              weight_decay: float = 0.0, step: int, overlap: bool = False,
+                              hyper: Optional[torch.Tensor] = None) -> None:
     """One single-rank step: ``denoiser_train_step`` + ``adamw_multi`` over ``table`` in one
     call (``ldm_denoiser_train_step_adamw``); ``overlap`` forks the updates onto a side stream
-    as their gradients become final.  Same bits as the two calls in sequence."""
+    as their gradients become final.  ``hyper``: device fp32 [7] AdamW scalars
+    (``adamw_hyper``) read by the kernels instead of lr / step (graph replays).  Same bits as
+    the two calls in sequence."""
     _f32(x0, eps, loss)
     _contig(x0, eps, t)
     if t.dtype != torch.int32:
@@ -650,7 +653,18 @@ def denoiser_train_step_adamw(desc: capi.Denoiser, sched_desc: capi.Sched, x0: t
         C.byref(desc), C.byref(sched_desc), x0.data_ptr(), eps.data_ptr(), t.data_ptr(),
         x0.shape[0], ws.data_ptr(), C.byref(gstruct), loss.data_ptr(), table, len(table),
         float(lr), float(betas[0]), float(betas[1]), float(adam_eps), float(weight_decay),
-        int(step), capi.stream_handle(x0.device), side), "ldm_denoiser_train_step_adamw")
+        int(step), capi.ptr(hyper), capi.stream_handle(x0.device), side),
+        "ldm_denoiser_train_step_adamw")
+
+
+def adamw_hyper(*, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                step: int) -> List[float]:
+    """The 7 AdamW scalars of one step exactly as the library derives them
+    (``ldm_adamw_hyper``), for a device ``hyper`` buffer."""
+    out = (C.c_float * 7)()
+    capi.load().ldm_adamw_hyper(float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                float(weight_decay), int(step), C.addressof(out))
+    return list(out)
 
 
 def denoiser_fwd(desc: capi.Denoiser, x: torch.Tensor, t: torch.Tensor, ws: torch.Tensor,

@@ -254,8 +254,9 @@ def test_train_bf16_loop_learns_and_matches_torch_adamw(dev, net):
 
 def test_train_step_adamw_fused_overlap_bitwise(dev, net):
     """ldm_denoiser_train_step_adamw (early weight updates forked onto a side stream) ==
-    the same entry point serialised (side = NULL) == ldm_denoiser_train_step + ldm_adamw_multi,
-    bit for bit: losses, fp32 masters, Adam moments and both bf16 working copies."""
+    its hipGraph replays (device AdamW scalars) == the entry point serialised (side = NULL) ==
+    ldm_denoiser_train_step + ldm_adamw_multi, bit for bit: losses, fp32 masters, Adam
+    moments and both bf16 working copies."""
     import ldm_sdf
     from ldm_sdf import MLPDenoiser
     _, p = net
@@ -265,12 +266,18 @@ def test_train_step_adamw_fused_overlap_bitwise(dev, net):
     lat = torch.randn(300, 256, generator=torch.Generator().manual_seed(5)).to(dev) * 0.5
     sch = ldm_sdf.DDPMSchedule()
     runs = []
-    for fused, overlap in ((True, True), (True, False), (False, False)):
+    for fused, overlap, graph in ((True, True, False), (True, False, True),
+                                  (True, False, False), (False, False, False)):
         model = MLPDenoiser(params={k: v.clone() for k, v in params.items()})
         model.to_device(dev)
-        st = ldm_sdf.train(model, sch, lat, steps=6, batch=300, lr=1e-3, weight_decay=0.01,
-                           dtype="bf16", generator=torch.Generator(device=dev).manual_seed(3),
-                           fused_step=fused, overlap=overlap)
+        gen = torch.Generator(device=dev).manual_seed(3)
+        # 40 steps in two calls: graph slots run eagerly in the first 32-step block, are
+        # captured, then replay (the second call reuses the state's graphs)
+        st = ldm_sdf.train(model, sch, lat, steps=30, batch=300, lr=1e-3, weight_decay=0.01,
+                           dtype="bf16", generator=gen, fused_step=fused, overlap=overlap,
+                           graph=graph)
+        st = ldm_sdf.train(model, sch, lat, steps=10, batch=300, dtype="bf16", generator=gen,
+                           state=st, fused_step=fused, overlap=overlap, graph=graph)
         work = model.device_pack("bf16", dev, with_tables=False)
         runs.append((list(st.losses), {n: t.clone() for n, t in model.params.items()},
                      {n: (m.clone(), v.clone()) for n, (m, v) in st.adam.items()},
