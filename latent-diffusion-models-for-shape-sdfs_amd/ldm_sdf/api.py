@@ -354,10 +354,13 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
                     w.copy_(p)                   # an fp32 working copy that is not the master
         state.step += 1
         state.losses.append(loss)
-    if state.optimizer is None:
-        # the built-in AdamW kept every working copy current: only the E tables (sampling) are
-        # rebuilt from the trained weights, so the AdamW table and captured graphs stay valid
+    if state.optimizer is None and dtype == "bf16":
+        # the built-in AdamW kept every working copy current (bf16 copies in both layouts; an
+        # fp32 pack holds the masters themselves): only the E tables (sampling) are rebuilt
+        # from the trained weights, so the AdamW table and captured graphs stay valid
         denoiser.invalidate_tables()
+    elif state.optimizer is None:
+        denoiser.invalidate()    # fp32 training updated the masters only: bf16 packs are stale
     # one device->host transfer for the whole run, not one per step
     pend = [i for i, l in enumerate(state.losses) if isinstance(l, torch.Tensor)]
     if pend:
