@@ -282,3 +282,58 @@ def test_gemm_blocked_transpose_and_sliced_split_k(dev):
     torch.cuda.synchronize()
     want = G.double() @ plain.double().T
     assert (out.double() - want).abs().max() < 2e-6 * math.sqrt(M) * 4 * 4
+
+
+@pytest.mark.parametrize("tile", [0, 4, 15, 20, 24])
+@pytest.mark.parametrize("mode", ["store", "silu", "resid_silu", "relu", "accum", "add_r",
+                                  "dgrad_silu", "loss", "relu_bwd"])
+def test_gemm_lds_epilogue_bitwise_vs_accumulator_layout(dev, mode, tile):
+    """The LDS-transposed epilogue (16-byte row-major stores) against the accumulator-layout
+    stores it replaced, on the same problem: row strides of N + 1 elements (not a multiple of
+    4) force every block onto the old path.  Every output must match bit for bit."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(hash(mode) % 997 + tile)
+    M, N, K = 200, 192, 384
+    Mv = 190
+    A = _rand((M, K), g, dev).bfloat16()
+    B = _rand((N, K), g, dev, 0.1).bfloat16()
+    bias = _rand((N,), g, dev)
+    R = _rand((M, N), g, dev)
+    Pin = _rand((M, N), g, dev)
+    Rb = _rand((M, N), g, dev).bfloat16()
+    Rb[::7] = 0.0
+    C0 = _rand((M, N), g, dev)
+
+    def run(pad):
+        def f32(src=None):
+            t = torch.zeros(M, N + pad, device=dev)
+            if src is not None:
+                t[:, :N] = src
+            return t[:, :N]
+        C = f32(C0)
+        P = f32()
+        Cb = torch.zeros(M, N + pad, device=dev, dtype=torch.bfloat16)[:, :N]
+        CbT = torch.zeros(N, M, device=dev, dtype=torch.bfloat16)
+        cs = torch.zeros((M + 31) // 32, N, device=dev)
+        lp = torch.zeros((M + 31) // 32, (N + 31) // 32, device=dev)
+        kw = dict(bias=bias, C=C, Cb=Cb, CbT=CbT, colsum=cs, M_valid=Mv)
+        if mode in ("silu", "resid_silu"):
+            kw["P"] = P
+        if mode in ("resid_silu", "add_r", "dgrad_silu"):
+            kw["R"] = f32(R)
+        if mode in ("dgrad_silu", "loss"):
+            kw["P_in"] = f32(Pin)
+        if mode == "loss":
+            kw["loss_part"] = lp
+            kw["scale"] = 0.37
+        if mode == "relu_bwd":
+            Rbp = torch.zeros(M, N + pad, device=dev, dtype=torch.bfloat16)
+            Rbp[:, :N] = Rb
+            kw["Rb"] = Rbp[:, :N]
+        ops.gemm([ops.gemm_problem([(A, B)], M, N, mode=mode, **kw)], tile=tile)
+        torch.cuda.synchronize()
+        return [x.contiguous() for x in (C, P, Cb, CbT, cs, lp)]
+
+    new, old = run(0), run(1)
+    for a, b, name in zip(new, old, ("C", "P", "Cb", "CbT", "colsum", "loss_part")):
+        assert torch.equal(a, b), (mode, tile, name)
