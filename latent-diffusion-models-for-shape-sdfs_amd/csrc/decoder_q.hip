@@ -128,7 +128,7 @@ __device__ __forceinline__ void qpipe_issue(QPipe& p, uint32_t voff) {
     glds2_saddr(p.isrc, voff, p.islot);
     p.islot = (p.islot + kStageBytes == p.ring_end) ? p.ring_beg : p.islot + kStageBytes;
     p.isrc += kStageBytes;
-    if (++p.is == p.inext) qpipe_boundary(p);
+    if (__builtin_expect(++p.is == p.inext, 0)) qpipe_boundary(p);   // 17 of 414 steps
 }
 
 __device__ __forceinline__ void qread_stage(const char* smem, int slot, int lane, u32x4 (&a)[8]) {
