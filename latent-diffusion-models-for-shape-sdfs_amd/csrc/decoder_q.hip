@@ -33,6 +33,10 @@ using namespace dec;
 #define QSTAMP 0
 #endif
 
+#ifndef QRELOAD_BRANCH
+#define QRELOAD_BRANCH 0
+#endif
+
 #define QRD(sl, i) ((QABL & 8) ? acur[i] : (sl)[(i) * 64 + c.lane])
 
 constexpr int QRING = 7;
@@ -339,6 +343,12 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
     // by the 4 steps above; it always lands in hb[24..31] (k-steps 24..31; a K=256 layer 4
     // reads its k-steps 8..15 from there, see qkloop_rest<8>), first read at pair j >= 4.
     // A predicated select (not a branch) keeps hb's register assignment stable.
+#if QRELOAD_BRANCH
+    if (q == 0) {         // uniform branch: the other 3 quarters skip the 8 KiB of LDS reads
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hb[24 + i] = c.tmp[i * 64 + c.lane];
+    }
+#else
     {
         const bool rl = (q == 0);
 #pragma unroll
@@ -347,6 +357,7 @@ __device__ __forceinline__ void run_quarter(QCtx& c, int qi, u32x4 (&acur)[8], u
             hb[24 + i] = rl ? v : hb[24 + i];
         }
     }
+#endif
     qkloop_rest<T, KP, PAR>(c, acur, hb, accX, accY);
     QSTS(4 + 3 * qi, accX);
     qstep_aux<T, false>(c, acur, bfrag, accX, PAR == 0);     // step KP (even)
