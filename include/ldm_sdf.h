@@ -178,6 +178,21 @@ size_t ldm_sample_loop_ws_bytes(int B, int H);
 int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, float* x, const float* noise,
                     int t_hi, int steps, int B, float* ws, size_t ws_bytes, ldm_stream_t s);
 int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* status_host, ldm_stream_t s);
+/* Loop forms.  AUTO (default): the XCD-replica loop when the shape has it (bf16, status 2 on a
+ * placement mismatch switches the device to XCD for good), else XCD. */
+#define LDM_LOOP_AUTO 0
+#define LDM_LOOP_REPLICA 1 /* one network copy per XCD, XCD-local tagged hand-offs */
+#define LDM_LOOP_XCD 2     /* chip-wide loop, XCD-hierarchical grid barrier */
+#define LDM_LOOP_DIRECT 3  /* chip-wide loop, hierarchical arrival, chip-wide polling */
+#define LDM_LOOP_FLAT 4    /* chip-wide loop, one flat counter */
+/* Explicit A/B and fault-injection control of ldm_sample_loop on the current device (the
+ * library reads no environment variable): form LDM_LOOP_*, spin_limit (0 = default; a tiny
+ * limit makes barriers give up, i.e. status 1), tagged (replica hand-offs: 1 = tagged
+ * granules, default; 0 = XCD-local barriers).  Defaults: (LDM_LOOP_AUTO, 0, 1). */
+int ldm_sample_loop_config(int form, unsigned spin_limit, int tagged);
+/* The form the last ldm_sample_loop launch on the current device took (LDM_LOOP_REPLICA ..
+ * LDM_LOOP_FLAT; 0 before any launch). */
+int ldm_sample_loop_last_form(void);
 
 /* ---- A6/A7/A9 training: denoiser forward with saved activations, backward, fused step ----
  * bf16 weights (w->dtype == LDM_BF16, the wt_* transposed copies set), matrix-core GEMMs

@@ -2,6 +2,7 @@
 // The compute entry points live next to their kernels (decoder.hip, denoiser.hip).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "ldm_internal.h"
 
@@ -16,6 +17,13 @@ void set_error(const char* fmt, ...) {
     vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
     va_end(ap);
 }
+
+#ifdef LDM_DEV_KNOBS
+int dev_knob_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
+#endif
 }  // namespace ldm
 
 extern "C" int ldm_abi_version(void) { return LDM_ABI_VERSION; }

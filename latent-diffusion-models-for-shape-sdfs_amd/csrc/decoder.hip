@@ -639,8 +639,8 @@ int check_decoder(const ldm_decoder_t* w) {
 
 // Schedule variant (development A/B knob; LDM_DECODER_SCHED=0|1, default 1).
 int decoder_sched() {
-    const char* e = getenv("LDM_DECODER_SCHED");   // read per launch: same-process A/B
-    return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 4;
+    const int v = dev_knob("LDM_DECODER_SCHED", 4);   // read per launch: same-process A/B
+    return (v >= 0 && v <= 4) ? v : 4;
 }
 
 template <typename T, int S, int SCHED>

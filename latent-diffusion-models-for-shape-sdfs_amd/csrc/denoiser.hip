@@ -522,8 +522,8 @@ void launch_small_v3(const SmallArgs& a, hipStream_t s) {
 }
 
 int small_version() {
-    const char* e = getenv("LDM_SMALL_LINEAR");   // development A/B knob: 1, 2, 3, 4 (default)
-    return (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 4;
+    const int v = dev_knob("LDM_SMALL_LINEAR", 4);   // development A/B knob: 1, 2, 3, 4 (default)
+    return (v >= 1 && v <= 4) ? v : 4;
 }
 
 template <typename TW, int EPI>

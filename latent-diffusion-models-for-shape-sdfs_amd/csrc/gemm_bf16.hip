@@ -24,6 +24,8 @@
 // Tiles: BM x BN per 4-wave workgroup (64 or 128 each), each wave (BM/2) x (BN/2) as
 // RM x RN v_mfma_f32_32x32x16_bf16 tiles; k-step 64.
 #include "ldm_internal.h"
+
+#include <mutex>
 #include "ddpm_common.h"
 
 #include <algorithm>
@@ -875,26 +877,33 @@ int launch_gemm(const ldm_gemm_args_t& a, hipStream_t s) {
     }
     ka.total = acc;
     constexpr int lds = STAGES * (BM + BN) * KB * 2;
-    static int grid_cap = 0;                  // persistent: resident workgroups on the device
-    if (grid_cap == 0) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_gemm_bf16: hipFuncSetAttribute: %s",
-                    hipGetErrorString(e));
-        int per_cu = 0, dev = 0, cus = 0;
-        if (PERSIST) {
-            LDM_REQUIRE(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                            &per_cu, reinterpret_cast<const void*>(k), 256 * KG, lds) ==
-                                hipSuccess &&
-                            hipGetDevice(&dev) == hipSuccess &&
-                            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
-                                                  dev) == hipSuccess &&
-                            per_cu >= 1,
-                        LDM_EINVAL, "ldm_gemm_bf16: persistent occupancy query failed");
+    // once per (template instance, device), thread-safe: the LDS attribute and, persistent,
+    // the resident-workgroup cap of THIS device (was once per process)
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static int grid_cap[kMaxDev];
+    static int init_err[kMaxDev];
+    int dev = 0;
+    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev, LDM_EINVAL,
+                "ldm_gemm_bf16: no current device");
+    std::call_once(once[dev], [&] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        int per_cu = 0, cus = 0;
+        if (e == hipSuccess && PERSIST) {
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(k), 256 * KG, lds);
+            if (e == hipSuccess)
+                e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess && per_cu < 1) e = hipErrorInvalidConfiguration;
         }
-        grid_cap = PERSIST ? per_cu * cus : 1;
-    }
-    const int grid = PERSIST ? std::min(acc, grid_cap) : acc;
+        init_err[dev] = (int)e;
+        grid_cap[dev] = PERSIST ? per_cu * cus : 1;
+    });
+    LDM_REQUIRE(init_err[dev] == 0, init_err[dev],
+                "ldm_gemm_bf16: kernel attribute / persistent occupancy query failed: %s",
+                hipGetErrorString((hipError_t)init_err[dev]));
+    const int grid = PERSIST ? std::min(acc, grid_cap[dev]) : acc;
     hipLaunchKernelGGL(k, dim3(grid), dim3(256 * KG), lds, s, ka);
     LDM_TRY(launch_status("ldm_gemm_bf16"));
     for (int p = 0; p < a.n_prob; ++p) {
@@ -918,10 +927,7 @@ int gemm_tiles(const ldm_gemm_args_t& a, int bm, int bn) {
     return total;
 }
 
-int env_int(const char* name) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : 0;
-}
+int env_int(const char* name) { return dev_knob(name, 0); }
 
 int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     LDM_REQUIRE(a.n_prob >= 1 && a.n_prob <= LDM_GEMM_MAX_PROBS, LDM_EINVAL,
@@ -981,10 +987,7 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     //    768-tile backward launches run in ONE wave of workgroups; the 128-deep 2-stage tile at
     //    2 per CU left half a wave: the step 0.348 -> 0.317-0.326 ms, scripts/train_tiles2.sh,
     //    profiles/r02h/train_tiles2.log).
-    static const int forced = [] {
-        const char* e = getenv("LDM_GEMM_TILE");
-        return e ? atoi(e) : 0;
-    }();
+    const int forced = dev_knob("LDM_GEMM_TILE", 0);
     int tile = a.tile;
     if (tile == 0) {
         bool k128 = true;
@@ -993,7 +996,7 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
         const int t64 = gemm_tiles(a, 64, 64);
         // tuning knobs per launch size class (tile counts at 64 x 64): <= 256, <= 512, < 2048,
         // >= 2048
-        static const int by_size[4] = {env_int("LDM_GEMM_TILE_SMALL"),
+        const int by_size[4] = {env_int("LDM_GEMM_TILE_SMALL"),
                                        env_int("LDM_GEMM_TILE_MID"), env_int("LDM_GEMM_TILE_BIG"),
                                        env_int("LDM_GEMM_TILE_HUGE")};
         const int cls = t64 <= 256 ? 0 : t64 <= 512 ? 1 : t64 < 2048 ? 2 : 3;

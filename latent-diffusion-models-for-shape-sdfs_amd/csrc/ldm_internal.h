@@ -35,6 +35,18 @@ inline int launch_status(const char* what) {
     return 0;
 }
 
+// ---- development A/B knobs --------------------------------------------------------------
+// The product library reads NO environment variable: every knob returns its default unless the
+// library was built with `make DEV=1` (-DLDM_DEV_KNOBS), the build scripts/ uses for same-
+// process A/B runs.  A stray variable at a caller's site can therefore never change which
+// kernel runs.
+#ifdef LDM_DEV_KNOBS
+int dev_knob_env(const char* name, int dflt);   // capi.cpp: getenv + atoi, per call
+inline int dev_knob(const char* name, int dflt) { return dev_knob_env(name, dflt); }
+#else
+inline int dev_knob(const char*, int dflt) { return dflt; }
+#endif
+
 // ---- fragment types ---------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

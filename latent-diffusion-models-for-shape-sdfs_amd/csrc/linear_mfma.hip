@@ -392,10 +392,7 @@ int launch_mfma3(const ldm_linear_args_t& a, bool xv, bool wv, hipStream_t s) {
 template <typename TW>
 int launch_mfma(const ldm_linear_args_t& a, bool xk, bool wk, hipStream_t s) {
     const int es = (int)sizeof(TW);
-    static const bool vec_on = [] {      // development A/B knob: LDM_LINEAR_VEC=0 -> scalar tiles
-        const char* e = getenv("LDM_LINEAR_VEC");
-        return !(e && e[0] == '0');
-    }();
+    const bool vec_on = dev_knob("LDM_LINEAR_VEC", 1) != 0;   // dev A/B: 0 -> scalar tiles
     bool xv = vec_on && vec_ok(a.X, a.sxb, a.sxk, a.Bn, a.K, 4);
     bool wv = vec_on && vec_ok(a.W, a.swm, a.swk, a.M, a.K, es);
     if (a.K2 > 0) {

@@ -23,6 +23,7 @@
 
 #include <stdlib.h>
 
+#include <atomic>
 #include <type_traits>
 
 #ifndef LDM_LOOP_SLEEP
@@ -33,7 +34,7 @@ namespace ldm {
 namespace {
 
 constexpr unsigned kSpinLimit = 1u << 22;   // x s_sleep(2) ~ 0.3 s per barrier, worst case
-// The limit travels in LoopArgs::spin_limit (default kSpinLimit).  LDM_SAMPLE_LOOP_SPIN_LIMIT
+// The limit travels in LoopArgs::spin_limit (default kSpinLimit).  ldm_sample_loop_config()
 // lowers it for the timeout test (tests/test_gpu_ddpm.py): a tiny limit makes barriers give up,
 // which must surface as status 1, never as silently wrong latents.
 
@@ -783,9 +784,26 @@ bool loop_resident_any(int dtype, int B, int D, int H) {
 }
 
 // The replica loop needs exactly H/4 = 256 workgroups resident, G/8 per XCD (checked in the
-// kernel: status 2 otherwise).  Once a launch has reported status 2 on this process, later
-// launches take the chip-wide loop.
-bool g_replica_off = false;
+// kernel: status 2 otherwise).  Once a launch has reported status 2 on a device, later
+// launches on that device take the chip-wide loop.  Per-device host state (device ordinals
+// < kMaxDev; the library is re-entrant per device, and these words are only ever flipped one
+// way or set by the explicit debug call ldm_sample_loop_config).
+constexpr int kMaxDev = 64;
+std::atomic<bool> g_replica_off[kMaxDev];
+// ldm_sample_loop_config (A/B and fault-injection tests only): form, spin limit, tagged
+struct LoopConfig {
+    std::atomic<int> form{LDM_LOOP_AUTO};
+    std::atomic<unsigned> spin_limit{0};
+    std::atomic<int> tagged{1};
+};
+LoopConfig g_cfg[kMaxDev];
+std::atomic<int> g_last_form[kMaxDev];
+
+int cur_dev() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) d = 0;
+    return d;
+}
 
 size_t replica_lds(int D, int MBX) {
     const int H = 1024, W = kRepWaves, R = H / (32 * W), RO = D / (32 * W);
@@ -807,7 +825,7 @@ bool replica_resident() {
 }
 
 bool replica_ok(const ldm_denoiser_t* w, int B) {
-    if (g_replica_off || w->dtype != LDM_BF16 || w->H != 1024 || w->n_blocks != 4) return false;
+    if (g_replica_off[cur_dev()].load() || w->dtype != LDM_BF16 || w->H != 1024 || w->n_blocks != 4) return false;
     if (w->D == 256) return B <= 8 ? replica_resident<256, 1>() : replica_resident<256, 2>();
     if (w->D == 512) return B <= 8 ? replica_resident<512, 1>() : replica_resident<512, 2>();
     return false;
@@ -879,29 +897,33 @@ extern "C" int ldm_sample_loop(const ldm_denoiser_t* w, const ldm_sched_t* sc, f
     a.h = ws;
     a.ctr = reinterpret_cast<unsigned*>(ws + act_floats(w->H));
     a.status = a.ctr + 32 * L_STATUS;
-    const char* bar = getenv("LDM_SAMPLE_LOOP_BARRIER");
-    // default / "replica": one network copy per XCD, XCD-local barriers (bf16 weights; else
-    // "xcd"); "xcd": chip-wide loop, XCD-hierarchical barrier with per-XCD generation words;
-    // "direct": hierarchical arrival, every workgroup polls the chip-wide word; "flat": one
-    // counter for everything
-    const bool replica = (!bar || bar[0] == 'r') && replica_ok(w, B);
-    a.hier = (bar && bar[0] == 'f') ? 0 : (bar && bar[0] == 'd') ? 2 : 1;
+    const int dev = cur_dev();
+    const LoopConfig& cfg = g_cfg[dev];
+    const int form = cfg.form.load();
+    // AUTO / REPLICA: one network copy per XCD, XCD-local hand-offs (bf16 weights; else the
+    // chip-wide loop with the XCD barrier); XCD: chip-wide loop, XCD-hierarchical barrier with
+    // per-XCD generation words; DIRECT: hierarchical arrival, every workgroup polls the
+    // chip-wide word; FLAT: one counter for everything
+    const bool replica = (form == LDM_LOOP_AUTO || form == LDM_LOOP_REPLICA) && replica_ok(w, B);
+    a.hier = form == LDM_LOOP_FLAT ? 0 : form == LDM_LOOP_DIRECT ? 2 : 1;
     a.B = B; a.D = w->D; a.H = w->H; a.t_hi = t_hi; a.steps = steps;
     a.spin_limit = kSpinLimit;
-    if (const char* lim = getenv("LDM_SAMPLE_LOOP_SPIN_LIMIT")) {
-        const long v = strtol(lim, nullptr, 10);
-        if (v >= 1 && v < (long)kSpinLimit) a.spin_limit = (unsigned)v;
+    {
+        const unsigned v = cfg.spin_limit.load();
+        if (v >= 1 && v < kSpinLimit) a.spin_limit = v;
     }
     for (int k = 0; k < 4; ++k)
         LDM_REQUIRE(a.w_blk[k] && a.e_tab[k], LDM_EINVAL, "sample_loop: block %d missing", k);
     a.hg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.ctr) + kSyncBytes);
     a.xg = a.hg + (size_t)8 * 2 * 2 * w->H;
-    // replica hand-offs: tagged granules (default) or XCD-local barriers ("0", A/B)
-    const char* tg = getenv("LDM_SAMPLE_LOOP_TAGGED");
-    a.tagged = (tg && tg[0] == '0') ? 0 : 1;
+    // replica hand-offs: tagged granules (default) or XCD-local barriers (tagged = 0, A/B)
+    a.tagged = cfg.tagged.load() ? 1 : 0;
     hipStream_t st = (hipStream_t)s;
     const size_t zero = kSyncBytes + (replica && a.tagged ? gran_bytes(w->H) : 0);
     if (hipMemsetAsync(a.ctr, 0, zero, st) != hipSuccess) return launch_status("sample_loop memset");
+    g_last_form[dev].store(replica ? LDM_LOOP_REPLICA
+                           : a.hier == 0 ? LDM_LOOP_FLAT : a.hier == 2 ? LDM_LOOP_DIRECT
+                                                                       : LDM_LOOP_XCD);
     if (replica) return launch_replica(a, st);
     if (w->dtype == LDM_BF16)
         return B <= 8 ? launch_loop<unsigned short, 8>(a, st) : launch_loop<unsigned short, 16>(a, st);
@@ -915,6 +937,19 @@ extern "C" int ldm_sample_loop_status(const float* ws, int B, int H, unsigned* s
     hipError_t e = hipMemcpyAsync(status_host, st, sizeof(unsigned), hipMemcpyDeviceToHost,
                                   (hipStream_t)s);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
-    if (e == hipSuccess && *status_host == 2) g_replica_off = true;   // placement: chip-wide loop
+    if (e == hipSuccess && *status_host == 2)
+        g_replica_off[cur_dev()].store(true);          // placement: chip-wide loop from now on
     return e == hipSuccess ? 0 : (int)e;
 }
+
+extern "C" int ldm_sample_loop_config(int form, unsigned spin_limit, int tagged) {
+    LDM_REQUIRE(form >= LDM_LOOP_AUTO && form <= LDM_LOOP_FLAT, LDM_EINVAL,
+                "sample_loop_config: form %d", form);
+    LoopConfig& c = g_cfg[cur_dev()];
+    c.form.store(form);
+    c.spin_limit.store(spin_limit);
+    c.tagged.store(tagged ? 1 : 0);
+    return 0;
+}
+
+extern "C" int ldm_sample_loop_last_form(void) { return g_last_form[cur_dev()].load(); }

@@ -155,6 +155,8 @@ SIGNATURES = [
     ("ldm_sample_loop", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _fp, _fp, _i, _i, _i, _fp,
                              _sz, _vp]),
     ("ldm_sample_loop_status", _i, [_fp, _i, _i, C.POINTER(C.c_uint), _vp]),
+    ("ldm_sample_loop_config", _i, [_i, C.c_uint, _i]),
+    ("ldm_sample_loop_last_form", _i, []),
     ("ldm_adamw_step", _i, [_fp, _fp, _fp, _fp, _vp, C.c_int64, C.c_double, C.c_double,
                             C.c_double, C.c_double, C.c_double, _i, _vp]),
     ("ldm_linear", _i, [C.POINTER(LinearArgs), _vp]),

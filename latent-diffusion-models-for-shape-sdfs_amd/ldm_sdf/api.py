@@ -90,6 +90,8 @@ class Sampler:
         if not (1 <= self.steps <= self.T):
             raise ValueError("steps must be in [1, T]")
         self.sd = schedule.device(self.device)
+        self.dtype = dtype
+        self._gen = getattr(denoiser, "table_gen", 0)
         D = denoiser.D
         self.x2 = torch.empty(2, n, D, device=self.device)
         self.x = [self.x2[0], self.x2[1]]
@@ -125,18 +127,36 @@ class Sampler:
 
         The persistent loop's grid barriers are bounded: if one gives up (status 1, e.g. when
         other work on the device kept part of the grid from being resident), the launch has
-        left partially updated latents.  With ``check`` (default) the status word is read back
+        left partially updated latents; status 2 (the XCD-replica loop found its workgroups
+        placed other than 32 per XCD) left them untouched and switched the device to the
+        chip-wide loop.  With ``check`` (default) the status word is read back
         (one stream synchronisation) and such a run is redone on the per-step path, which gives
         the same numbers bit for bit; ``loop_fallbacks`` counts these.  ``check=False`` keeps
         the call asynchronous: the caller then reads ``loop.status()`` itself."""
+        gen = getattr(self.model, "table_gen", 0)
+        if gen != self._gen:
+            # the denoiser was trained (or re-packed) since this sampler was built: re-pack its
+            # weights / E tables (descriptors are updated in place) and re-capture the graph,
+            # which baked the old table addresses in
+            self.model.device_pack(self.dtype, self.device)
+            self.step = self.model.make_stepper(self.n, self.dtype, self.device, self.sd["desc"])
+            if self.loop is not None:
+                self.loop = self.model.make_loop(self.n, self.dtype, self.device, self.sd["desc"])
+            self.graph = None
+            self._gen = gen
         self.x[0].copy_(x_T)
         self.noise[:noise.shape[0]].copy_(noise)
         if self.loop is not None:
             self.loop(self.x2, self.noise, self.T - 1, self.steps)
-            if not check or self.loop.status() == 0:
+            if not check:
+                return self.result
+            st = self.loop.status()
+            if st == 0:
                 return self.result
             self.loop_fallbacks += 1
-            warnings.warn("ldm_sample_loop: a grid barrier timed out (status 1); "
+            why = {1: "a grid barrier timed out",
+                   2: "replica placement mismatch (device switched to the chip-wide loop)"}
+            warnings.warn(f"ldm_sample_loop: status {st} ({why.get(st, 'unknown')}); "
                           "re-running this sample on the per-step path", RuntimeWarning)
             self.x[0].copy_(x_T)
             self._loop()

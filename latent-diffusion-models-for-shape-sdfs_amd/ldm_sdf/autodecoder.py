@@ -314,19 +314,23 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
     gb = {}
     ws_cache = {}
 
-    def ws_for(n):
-        t = ws_cache.get(n)
+    def ws_for(n, slot):
+        # keyed by (size, slot in the launch's problem list): two problems of ONE launch must
+        # never share partial slabs, even when their sizes agree (e.g. S == zw on the one-hot
+        # path); launches run in stream order, so reuse across launches is safe
+        t = ws_cache.get((n, slot))
         if t is None:
-            t = ws_cache[n] = torch.empty(n, **f32)
+            t = ws_cache[(n, slot)] = torch.empty(n, **f32)
         return t
 
-    def wgrad(gT, xT, M_, N_, out):
+    def wgrad(gT, xT, M_, N_, out, slot):
         """out [M_, N_] fp32 = sum over the samples of gT x xT^T; gT [nblk, M_, KT] and
-        xT [nblk, N_, KT] blocked: split-K with one slice per block."""
+        xT [nblk, N_, KT] blocked: split-K with one slice per block.  `slot` = the problem's
+        index within its launch (its own split-K workspace)."""
         if nblk == 1:
             return ops.gemm_problem([(gT[0], xT[0])], M_, N_, C=out)
         return ops.gemm_problem([(gT[0], xT[0])], M_, N_, C=out, k_split=nblk,
-                                ws=ws_for(nblk * M_ * N_),
+                                ws=ws_for(nblk * M_ * N_, slot),
                                 slices=(gT.shape[1] * KT, xT.shape[1] * KT))
 
     # layer 8: dW8 = g8^T h7, db8 = sum g8; g7 = (g8 w8) * [h7 > 0]
@@ -342,7 +346,7 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
     cs = torch.empty(nrow32, H, **f32)
     ops.gemm([ops.gemm_problem([(g8b, W8T)], Np, H, mode="relu_bwd", M_valid=N, Rb=h[7],
                                Cb=g_cur, CbT=gT_cur, colsum=cs, ct_blk=KT)])
-    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"])], tile=_WG_TILE)
+    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"], 0)], tile=_WG_TILE)
     colsums = {7: cs}
     gcs = {}                                       # g_l per 32-row block sums (bias / latent)
     Gs = {}                                        # per-shape column sums of g_skip and g_0
@@ -358,18 +362,18 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
         if l == skip:
             gw["W4h"] = torch.empty(H, hsp, **f32)
             gw["W4z"] = torch.empty(H, zw, **f32)
-            probs = [wgrad(gT_cur, hT[l - 1], H, hsp, gw["W4h"]),
-                     wgrad(gT_cur, ZxT, H, zw, gw["W4z"])]
+            probs = [wgrad(gT_cur, hT[l - 1], H, hsp, gw["W4h"], 0),
+                     wgrad(gT_cur, ZxT, H, zw, gw["W4z"], 1)]
         elif l == 0:
             gw["W0"] = torch.empty(H, zw, **f32)
-            probs = [wgrad(gT_cur, ZxT, H, zw, gw["W0"])]
+            probs = [wgrad(gT_cur, ZxT, H, zw, gw["W0"], 0)]
         else:
             win = h[l - 1].shape[1]
             gw[f"W{l}"] = torch.empty(wout, win, **f32)
-            probs = [wgrad(gT_cur, hT[l - 1], wout, win, gw[f"W{l}"])]
+            probs = [wgrad(gT_cur, hT[l - 1], wout, win, gw[f"W{l}"], 0)]
         if onehot is not None and l in (skip, 0):
             Gs[l] = torch.empty(S, H, **f32)
-            probs.append(wgrad(onehot, gT_cur, S, H, Gs[l]))
+            probs.append(wgrad(onehot, gT_cur, S, H, Gs[l], len(probs)))
         # weight gradients (long K per slice): larger tiles than the 1M-row G W product, so
         # their own launch
         ops.gemm(probs, tile=_WG_TILE)

@@ -228,6 +228,9 @@ class MLPDenoiser:
         self.params = {k: v.detach().to(torch.float32).contiguous() for k, v in params.items()}
         self.emb_table = torch.from_numpy(timestep_embedding_table(T, TE))
         self._dev: Dict[Tuple[str, torch.device], Dict[str, object]] = {}
+        # bumped whenever packed weights or E tables change under a descriptor handed out
+        # earlier: a Sampler compares it and re-packs / re-captures
+        self.table_gen = 0
 
     def names(self) -> List[str]:
         return list(self.PARAM_ORDER) + [f"Wblk{k}" for k in range(self.n_blocks)] + \
@@ -258,6 +261,7 @@ class MLPDenoiser:
     def invalidate(self) -> None:
         """Call after the fp32 masters changed (training): drops packed copies / E tables."""
         self._dev.clear()
+        self.table_gen += 1
 
     def invalidate_tables(self) -> None:
         """Call after training that kept the working copies current (the built-in AdamW
@@ -266,8 +270,9 @@ class MLPDenoiser:
         addresses) stay valid."""
         for dev in self._dev.values():
             old = [dev.pop(f"etab{k}") for k in range(self.n_blocks) if f"etab{k}" in dev]
-            if old:             # kept alive: a descriptor handed out earlier still points there
-                dev["_stale_etab"] = old
+            if old:             # kept alive (ALL generations): a descriptor or a graph captured
+                dev.setdefault("_stale_etab", []).append(old)   # earlier may still point there
+        self.table_gen += 1
 
     def make_stepper(self, n: int, dtype: str, device, sched_desc):
         """Callable ``step(x, z, t, x_out)``: one fused reverse step (``ldm_sample_step``)."""
@@ -293,6 +298,7 @@ class MLPDenoiser:
             ops.sample_loop(desc, sched_desc, x2, noise, t_hi, steps, ws)
             return ws
         loop.status = lambda: ops.sample_loop_status(desc, ws, n)
+        loop.form = ops.sample_loop_last_form     # which kernel the last launch ran
         return loop
 
     def device_pack(self, dtype: str, device, with_tables: bool = True) -> Dict[str, object]:

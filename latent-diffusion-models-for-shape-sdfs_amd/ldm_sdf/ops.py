@@ -213,6 +213,24 @@ def sample_loop_status(desc: capi.Denoiser, ws: torch.Tensor, B: int) -> int:
     return int(st.value)
 
 
+LOOP_FORMS = {"auto": 0, "replica": 1, "xcd": 2, "direct": 3, "flat": 4}
+LOOP_FORM_NAMES = {v: k for k, v in LOOP_FORMS.items()}
+
+
+def sample_loop_config(form: str = "auto", spin_limit: int = 0, tagged: bool = True) -> None:
+    """Explicit A/B / fault-injection control of the persistent sampling loop on the current
+    device (``ldm_sample_loop_config``): the library reads no environment variable."""
+    capi.check(capi.load().ldm_sample_loop_config(LOOP_FORMS[form], int(spin_limit),
+                                                  1 if tagged else 0),
+               "ldm_sample_loop_config")
+
+
+def sample_loop_last_form() -> str:
+    """Which loop kernel the last ``sample_loop`` on the current device ran ("replica", "xcd",
+    "direct", "flat"; "auto" before any launch)."""
+    return LOOP_FORM_NAMES[int(capi.load().ldm_sample_loop_last_form())]
+
+
 # ---------------------------------------------------------------------------------------- GEMM
 def linear(X: torch.Tensor, W: torch.Tensor, Y: torch.Tensor, *, epi: int = capi.EPI_BIAS,
            bias: Optional[torch.Tensor] = None, X2: Optional[torch.Tensor] = None,

@@ -126,6 +126,27 @@ def test_train_step_bf16_grads_close_to_fp64(dev, S, P):
         assert cos > 0.99, (k, cos)
 
 
+def test_train_step_bf16_split_k_workspaces_distinct(dev):
+    """S == zw (= 320 at L = 256) on the one-hot path (P % 32 != 0), nblk = 125 k-blocks: the
+    W0 gradient (H x zw) and the per-shape sums Gs[0] (S x H) share one split-K launch with
+    equal slab sizes.  Each must get its own workspace: compared with the fp64
+    oracle, every weight and the latent gradient at cosine > 0.99."""
+    from ldm_sdf import autodecoder_train_step
+    from oracle import ref_autodecoder as A
+    p, z, xyz, sdf = _problem(S=320, P=200, seed=11)
+    loss_ref, gref = A.autodecoder_grads(p, z.float().double(), xyz.float().double(),
+                                         sdf.float().double())
+    loss, grads, gz = autodecoder_train_step(_masters(p, dev), z.float().to(dev),
+                                             xyz.float().to(dev), sdf.float().to(dev),
+                                             dtype="bf16")
+    assert abs(float(loss) - loss_ref) < 2e-2 * abs(loss_ref)
+    for k in ["W0", "b0", "W4", "W8", "z"]:
+        got = (gz if k == "z" else grads[k]).cpu().double().flatten()
+        want = gref[k].flatten()
+        cos = float(got @ want / (got.norm() * want.norm()))
+        assert cos > 0.99, (k, cos)
+
+
 def test_fit_lowers_loss_on_spheres(dev):
     """4 spheres of different radii, 2048 samples each: 200 bf16 steps of the full loop
     (decoder Adam + latent Adam) cut the clamped-L1 loss by at least 2x, and the trained

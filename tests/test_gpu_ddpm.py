@@ -165,13 +165,15 @@ def test_sampling_graph_equals_eager_bf16(dev, den):
                           ("bf16", 8, 1000, "xcd"), ("bf16", 1, 40, "xcd"), ("bf16", 5, 40, "xcd"),
                           ("bf16", 16, 40, "xcd"), ("fp32", 8, 40, "xcd"), ("fp32", 13, 40, "xcd"),
                           ("bf16", 8, 200, "flat"), ("fp32", 3, 40, "flat")])
-def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps, barrier, monkeypatch):
+def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps, barrier, loop_form):
     """The one-launch loop (ldm_sample_loop) is bit-identical to the per-step launches: same
     k-to-lane mapping, fma order, shuffle reduce and epilogues; every barrier completed.  Every
     form is covered: the XCD-replica loop (bf16 default), the chip-wide loop with the
-    XCD-hierarchical barrier (fp32 default) and with the flat counter."""
+    XCD-hierarchical barrier (fp32 default) and with the flat counter; the form that actually
+    ran is asserted (ldm_sample_loop_last_form)."""
     import ldm_sdf
-    monkeypatch.setenv("LDM_SAMPLE_LOOP_BARRIER", barrier)
+    from ldm_sdf import ops
+    loop_form(barrier)
     model, _ = den
     gen = torch.Generator().manual_seed(11 + n)
     xT = torch.randn(n, 256, generator=gen).to(dev)
@@ -181,12 +183,26 @@ def test_sample_loop_persistent_matches_graph(dev, den, dtype, n, steps, barrier
     sg = ldm_sdf.Sampler(model, sch, n, steps=steps, dtype=dtype, device=dev, persistent=False)
     a = sp.run(xT, noise).clone()
     assert sp.loop.status() == 0
+    want_form = barrier if (barrier != "replica" or dtype == "bf16") else "xcd"
+    assert ops.sample_loop_last_form() == want_form, (ops.sample_loop_last_form(), want_form)
     b = sg.run(xT, noise).clone()
     assert torch.isfinite(a).all()
     assert torch.equal(a, b), float((a - b).abs().max())
     # replay: the counter/status words are re-zeroed per call, so a second run is identical
     c = sp.run(xT, noise).clone()
     assert sp.loop.status() == 0 and torch.equal(a, c)
+
+
+@pytest.fixture
+def loop_form():
+    """Set the persistent loop's form / spin limit through the explicit C call; restore the
+    defaults afterwards."""
+    from ldm_sdf import ops
+
+    def set_(form="auto", spin_limit=0, tagged=True):
+        ops.sample_loop_config(form, spin_limit, tagged)
+    yield set_
+    ops.sample_loop_config()
 
 
 def test_sample_loop_rejects_unsupported(dev):
@@ -477,7 +493,7 @@ def test_sampling_bf16_1000_steps_b8_vs_oracle_rounded(dev, den, path):
     assert loose <= 5e-2, loose
 
 
-def test_sample_loop_timeout_surfaces_and_falls_back(dev, den, monkeypatch):
+def test_sample_loop_timeout_surfaces_and_falls_back(dev, den, loop_form):
     """A persistent-loop barrier that gives up must not hand back partial latents silently:
     with a 1-poll spin limit the loop reports status 1, Sampler.run warns, re-runs the sample
     on the per-step path and returns that path's (bit-identical) result."""
@@ -489,7 +505,7 @@ def test_sample_loop_timeout_surfaces_and_falls_back(dev, den, monkeypatch):
     sch = ldm_sdf.DDPMSchedule()
     ref = ldm_sdf.Sampler(model, sch, 8, steps=40, dtype="bf16", device=dev,
                           persistent=False).run(xT, noise).clone()
-    monkeypatch.setenv("LDM_SAMPLE_LOOP_SPIN_LIMIT", "1")
+    loop_form("auto", spin_limit=1)
     sp = ldm_sdf.Sampler(model, sch, 8, steps=40, dtype="bf16", device=dev, persistent=True)
     sp.run(xT, noise, check=False)
     assert sp.loop.status() == 1
@@ -497,5 +513,34 @@ def test_sample_loop_timeout_surfaces_and_falls_back(dev, den, monkeypatch):
         got = sp.run(xT, noise).clone()
     assert sp.loop_fallbacks == 1
     assert torch.equal(got, ref)
-    monkeypatch.delenv("LDM_SAMPLE_LOOP_SPIN_LIMIT")
+    loop_form()
     assert torch.equal(sp.run(xT, noise), ref) and sp.loop_fallbacks == 1
+
+
+@pytest.mark.parametrize("persistent", [False, True])
+def test_sampler_repacks_after_training(dev, den, persistent):
+    """A Sampler built (and its graph captured) BEFORE train() must sample with the trained
+    weights AND their rebuilt E tables afterwards (the graph had baked the old
+    table addresses in): its result equals a fresh Sampler's, bit for bit."""
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser
+    _, p = den
+    params = {n: getattr(p, n) for n in ("Wt1", "bt1", "Wt2", "bt2", "Win", "bin", "Wout", "bout")}
+    for k in range(p.n_blocks):
+        params[f"Wblk{k}"], params[f"bblk{k}"] = p.Wblk[k], p.bblk[k]
+    model = MLPDenoiser(params={k: v.clone() for k, v in params.items()})
+    model.to_device(dev)
+    sch = ldm_sdf.DDPMSchedule()
+    gen = torch.Generator().manual_seed(31)
+    xT = torch.randn(8, 256, generator=gen).to(dev)
+    noise = torch.randn(1000, 8, 256, generator=gen).to(dev)
+    kw = dict(steps=30, dtype="bf16", device=dev, persistent=persistent)
+    old = ldm_sdf.Sampler(model, sch, 8, **kw)
+    before = old.run(xT, noise).clone()
+    lat = torch.randn(256, 256, generator=torch.Generator().manual_seed(3)).to(dev) * 0.5
+    ldm_sdf.train(model, sch, lat, steps=20, batch=256, lr=1e-3, dtype="bf16",
+                  generator=torch.Generator(device=dev).manual_seed(4))
+    after = old.run(xT, noise).clone()
+    fresh = ldm_sdf.Sampler(model, sch, 8, **kw).run(xT, noise).clone()
+    assert not torch.equal(before, fresh)          # training changed the network
+    assert torch.equal(after, fresh), float((after - fresh).abs().max())
