@@ -140,6 +140,42 @@ def cpu_baseline_sampling(budget_s: float, B: int):
             "sample": f"{steps} reverse steps, B={B}, fp32 torch-CPU oracle, {dt:.1f}s"}
 
 
+def cpu_baseline_train(budget_s: float, batch: int = 1000):
+    """Config 2 on the CPU: the fp32 oracle training step (q_sample -> denoiser -> eps-MSE ->
+    autograd backward, oracle/ref_cpu.py train_step's math) + torch AdamW on the fp32
+    parameters, batch ``batch`` on 1000 latents, this job's cores; steps until ``budget_s``."""
+    from oracle import ref_cpu as R
+    torch.set_num_threads(host_cores())
+    p = R.make_denoiser_params(seed=4321, dtype=torch.float32)
+    params = p.map(lambda w: w.detach().clone().requires_grad_(True))
+    leaves = [params.Wt1, params.bt1, params.Wt2, params.bt2, params.Win, params.bin,
+              params.Wout, params.bout] + list(params.Wblk) + list(params.bblk)
+    opt = torch.optim.AdamW(leaves, lr=1e-4, weight_decay=0.0)
+    tab = R.ddpm_tables()
+    emb = torch.from_numpy(R.timestep_embedding_table(1000, 128))
+    g = torch.Generator().manual_seed(0)
+    lat = torch.randn(1000, 256, generator=g) * 0.5
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        t = torch.randint(0, 1000, (batch,), generator=g)
+        eps = torch.randn(batch, 256, generator=g)
+        x0 = lat[:batch]
+        with torch.enable_grad():
+            xt = R.q_sample(tab, x0, eps, t)
+            loss = R.eps_mse_loss(R.denoiser_forward(params, xt, t, emb), eps)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+        opt.step()
+        steps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "steps/s", "kind": "port",
+            **cpu_fields(host_cores()),
+            "sample": f"{steps} fp32 torch-CPU oracle training steps (autograd + AdamW), "
+                      f"batch {batch}, {dt:.1f}s"}
+
+
 def cpu_baseline_unet(budget_s: float, B: int):
     """Config 5's sampler on the CPU: the fp32 oracle UNet (oracle/ref_unet.py) reverse steps."""
     from oracle import ref_cpu as R
@@ -341,6 +377,24 @@ def decoder_traffic(queries_per_launch: float):
     return per_q * queries_per_launch, j.get("source", tf)
 
 
+def handoff_latency():
+    """The same-XCD one-way latency of the sampler's 8-byte tagged hand-off, measured by
+    scripts/microbench/handoff_latency.hip on an MI355X (median of its reps), from the newest
+    profiles/*/handoff_latency.json; None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "handoff_latency.json")))
+    if not files:
+        return None
+    try:
+        rows = [json.loads(l) for l in open(files[-1]) if l.strip().startswith("{")]
+        same = sorted(r["one_way_ns"] for r in rows if r.get("pair") == "same-XCD" and r["ok"])
+    except (OSError, ValueError, KeyError):
+        return None
+    if not same:
+        return None
+    return {"one_way_ns": same[len(same) // 2], "source": os.path.relpath(files[-1], ROOT)}
+
+
 def config5(args, rank, world, dev, group, gen):
     """Config 5: 1000-step DDPM sampling of ``--c5-batch`` 1024-d latents with the 1D-UNet
     (bf16 weights, hipGraph) -> fp16 MFMA decode (widen-skip decoder, L=1024) of a 512^3
@@ -501,6 +555,18 @@ def main():
         if "ddpm" in res:
             res["ddpm"]["cpu_baseline"] = cpu_baseline_sampling(min(5.0, args.cpu_seconds),
                                                                 args.ddpm_batch)
+            if res["ddpm"].get("config3_sample_plus_decode128_s") is not None:
+                # config 3 end to end on the CPU, from the two bounded samples just timed: 1000
+                # oracle steps at B = 8 + the 8 x 128^3 decode at the oracle's q/s (flat in N)
+                sps_c = res["ddpm"]["cpu_baseline"]["value"]
+                qps_c = res["cpu_baseline"]["value"]
+                e2e_c = 1000.0 / sps_c + args.ddpm_batch * 128 ** 3 / qps_c
+                res["ddpm"]["config3_cpu_baseline"] = {
+                    "value": e2e_c, "unit": "s (sample + decode, extrapolated)", "kind": "port",
+                    "cores": res["cpu_baseline"]["cores"],
+                    "sample": "1000 / ddpm.cpu_baseline steps/s + 8 x 128^3 / "
+                              "cpu_baseline queries/s (both measured above on this host)",
+                    "gpu_over_cpu": e2e_c / res["ddpm"]["config3_sample_plus_decode128_s"]}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -540,10 +606,19 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
             el = float(tt)
         return 1000 * reps / el
 
-    # check=False inside the timed region (no per-run sync); the status is read right after
-    sps = timed(lambda: sampler.run(xT, noise, check=False))
+    # check=False (no host-side fallback inside the timed region), but the status word is read
+    # after EVERY rep (it is re-zeroed per launch): a rep that stopped early would otherwise
+    # shorten the time unseen.  One ~20 us read-back per 15-20 ms rep.
     persistent = sampler.loop is not None
-    loop_status = sampler.loop.status() if persistent else None
+    statuses = []
+
+    def one_rep():
+        sampler.run(xT, noise, check=False)
+        if persistent:
+            statuses.append(sampler.loop.status())
+    sps = timed(one_rep)
+    loop_status = max(statuses) if statuses else None
+    loop_form = ldm_sdf.ops.sample_loop_last_form() if persistent else None
     sampler_g = ldm_sdf.Sampler(den, sch, nl, dtype="bf16", device=dev, persistent=False)
     xg = sampler_g.run(xT, noise).clone()
     sps_graph = timed(lambda: sampler_g.run(xT, noise))
@@ -560,17 +635,34 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
         torch.cuda.synchronize()
         e2e = time.perf_counter() - t2
     wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nl * den.D * 4
-    return {"metric": "DDPM sample steps/sec", "value": sps, "unit": "steps/s",
+    valid = not loop_status
+    hand = handoff_latency()
+    if hand is not None:
+        # latency model: each reverse step is 6 dependent layer hand-offs (in-projection, 4
+        # blocks, out-projection + update), each at least one same-XCD publish -> poll latency
+        model_step = 6 * hand["one_way_ns"] * 1e-9
+        roof = {"bound": "handoff-latency", "achieved": sps,
+                "peak": 1.0 / model_step, "unit": "steps/s", "frac": sps * model_step,
+                "handoffs_per_step": 6, "one_way_handoff_ns": hand["one_way_ns"],
+                "source": hand["source"],
+                "note": "peak = 1 / (6 x measured same-XCD 8-byte tagged hand-off latency); "
+                        "frac = that model step time / the measured step time"}
+    else:
+        roof = None
+    return {"metric": "DDPM sample steps/sec", "value": sps if valid else None,
+            "valid": valid, "unit": "steps/s",
             "batch": nb, "batch_per_rank": nl, "T": 1000, "shape_steps_per_s": sps * nb,
             "path": ("one persistent launch for all 1000 steps "
                      "(weights in registers, XCD-hierarchical grid barrier per "
                      "layer)" if persistent
                      else "hipGraph of 1000 fused steps (6 kernels each)"),
-            "loop_status": loop_status,
+            "loop_status": loop_status, "loop_status_per_rep": statuses,
+            "loop_form": loop_form,
             "graph_path": {"steps_per_s": sps_graph,
                            "path": "hipGraph of 1000 fused steps (6 kernels each)",
                            "bit_identical": same},
-            "roofline": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
+            "roofline": roof,
+            "roofline_hbm": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
                          "peak": 8000.0, "unit": "GB/s",
                          "frac": sps * wbytes / 8e12,
                          "bytes_per_step": wbytes,
@@ -598,10 +690,20 @@ def bench_train(args, dev, gen):
     dtt = (time.perf_counter() - t3) / args.train_steps
     H, D, nb = den_t.H, den_t.D, den_t.n_blocks
     macs = 1000 * (H * 128 + H * H + H * D + nb * H * 2 * H + D * H)   # forward MACs
-    return {"metric": "DDPM training steps/sec (config 2)", "value": 1.0 / dtt,
-            "unit": "steps/s", "batch": 1000, "ms_per_step": dtt * 1e3,
-            "tflops_fwd_bwd": 3 * 2 * macs / dtt / 1e12,
-            "loss_first_last": [st.losses[0], st.losses[-1]]}
+    flops = 3 * 2 * macs          # forward + the two backward products (dX, dW) per layer
+    ach = flops / dtt / 1e12
+    res = {"metric": "DDPM training steps/sec (config 2)", "value": 1.0 / dtt,
+           "unit": "steps/s", "batch": 1000, "ms_per_step": dtt * 1e3,
+           "tflops_fwd_bwd": ach,
+           "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_TFLOPS["bf16"],
+                        "unit": "TFLOP/s", "frac": ach / PEAK_TFLOPS["bf16"],
+                        "flops_per_step": flops,
+                        "note": "3 x 2 x forward MACs per step (1000 samples) over the wall "
+                                "time of a step (every launch incl. AdamW, 100 timed steps)"},
+           "loss_first_last": [st.losses[0], st.losses[-1]]}
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_train(min(10.0, args.cpu_seconds))
+    return res
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@ for s in $STAGES; do
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 900 python bench.py ${BENCH_ARGS:-} ;;
+    micro)  run handoff_latency 120 scripts/microbench/handoff_latency ;;
     prof)   cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
             run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
                 --output-format csv -- python3 bench.py ${PROF_ARGS:-} ;;

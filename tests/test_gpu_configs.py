@@ -6,8 +6,9 @@
 * config 5 -- fp16 decode of a 512^3 grid with the widen-skip decoder, L = 1024
   (`BASELINE.json:11`; the UNet sampling half is pinned in test_gpu_unet.py).
 
-Config 4 (64 x 256^3 over 8 GPUs) is the bench's own step; its single-GPU numerics are the
-decoder tests', and its reassembly is covered by the gloo tests (test_dist_gloo.py).
+* config 4 -- the bench's own decode inputs at their own size: 64 shapes x 256^3, bf16
+  (`BASELINE.json:10`; its 8-GPU z-slab reassembly is covered by the gloo tests,
+  test_dist_gloo.py / test_bench_gloo.py);
 Full volumes are checked on random point subsets (the fp64 oracle on 134 M points would take
 hours); tolerances are SURVEY.md §8(c)'s.
 """
@@ -104,6 +105,51 @@ def test_config3_sample8_then_decode128(dev):
             assert err <= TOL["bf16"], (b, err)
 
 
+def _grid_xyz(idx: np.ndarray, N: int) -> torch.Tensor:
+    """A1's coordinates of flat grid indices (z slowest), without building the whole grid."""
+    from oracle import ref_cpu as R
+    line = (np.arange(N, dtype=np.float32) * R.grid_voxel_size(N)).astype(np.float32) \
+        + np.float32(-1.0)
+    return torch.from_numpy(np.stack([line[idx % N], line[(idx // N) % N], line[idx // (N * N)]],
+                                     axis=1).astype(np.float32)).double()
+
+
+def test_config4_decode_b64_256_bench_inputs(dev):
+    """Config 4 at its own size with the bench's exact inputs (bench.py main: decoder
+    SDFDecoder(256, seed=1234), latents = randn(64, 256, device generator seed 0) * 0.1, bf16,
+    256^3): 256 random points per shape plus every shape's 8 corners against the fp64 oracle at
+    the bf16 bound; and one shape decoded alone is bitwise the same shape inside the batch."""
+    import ldm_sdf
+    from oracle import ref_cpu as R
+    B, N = 64, 256
+    dec = ldm_sdf.SDFDecoder(256, seed=1234)
+    p = R.make_decoder_params(seed=1234)
+    for l in range(9):       # the bench's decoder IS the oracle's seed-1234 decoder
+        assert torch.equal(dec.weights[l], p.weights[l].float()), l
+    gen = torch.Generator(device=dev).manual_seed(0)
+    lat = torch.randn(B, 256, device=dev, generator=gen) * 0.1
+    vol = ldm_sdf.decode(dec, lat, N, dtype="bf16")
+    assert vol.shape == (B, N, N, N)
+    g = torch.Generator().manual_seed(404)
+    corners = torch.tensor([k * N * N + j * N + i for k in (0, N - 1) for j in (0, N - 1)
+                            for i in (0, N - 1)])
+    idx = torch.cat([torch.randint(0, N ** 3, (B, 256), generator=g),
+                     corners[None].expand(B, -1)], dim=1)
+    got = vol.reshape(B, -1)[torch.arange(B, device=dev)[:, None], idx.to(dev)].cpu().double()
+    zc = lat.cpu().double()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    worst = 0.0
+    for b in range(B):
+        want = R.decoder_forward(p, zc[b:b + 1], _grid_xyz(idx[b].numpy(), N))[0]
+        err = float((got[b] - want).abs().max())
+        worst = max(worst, err)
+        assert err <= TOL["bf16"], (b, err)
+    print(f"config4 64 x 256^3 bf16: max abs err {worst:.3e} over {idx.numel()} points")
+    assert bool(torch.isfinite(vol[:, 0]).all()) and bool(torch.isfinite(vol[:, -1]).all())
+    one = ldm_sdf.decode(dec, lat[37:38], N, dtype="bf16")
+    assert torch.equal(one[0], vol[37])
+
+
 def test_config5_decode_512_fp16_widen_skip(dev):
     """Config 5's decode: 1 latent (L = 1024, widen-skip decoder), fp16 matrix cores, the full
     512^3 grid (134 M queries, the size the bench runs), 2000 random points vs the fp64 oracle
@@ -124,12 +170,7 @@ def test_config5_decode_512_fp16_widen_skip(dev):
                             for i in (0, N - 1)])
     idx = torch.cat([idx, corners])
     got = vol.reshape(-1)[idx.to(dev)].cpu().double()
-    line = (np.arange(N, dtype=np.float32) * R.grid_voxel_size(N)).astype(np.float32) \
-        + np.float32(-1.0)                                  # A1's rule, without the 1.6 GB grid
-    ii = idx.numpy()
-    xyz = torch.from_numpy(np.stack([line[ii % N], line[(ii // N) % N], line[ii // (N * N)]],
-                                    axis=1).astype(np.float32)).double()
-    want = R.decoder_forward(p, z.double(), xyz)[0]
+    want = R.decoder_forward(p, z.double(), _grid_xyz(idx.numpy(), N))[0]
     err = float((got - want).abs().max())
     print(f"config5 512^3 fp16: max abs err {err:.3e} on {idx.numel()} points")
     assert err <= TOL["fp16"], err
