@@ -209,6 +209,50 @@ def decoder_forward_folded(p: DecoderParams, beta: torch.Tensor,
     return torch.stack(out, 0)
 
 
+def decoder_forward_lowp(p: DecoderParams, z: torch.Tensor, xyz: torch.Tensor,
+                         dt: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """A3 at the perf kernels' 16-bit precision contract (SURVEY.md §8(a) A3 "bf16/fp16 in,
+    fp32 acc"), evaluated in fp64: every weight matrix rounded to ``dt`` (RNE); every hidden
+    activation that feeds a matrix product rounded to ``dt`` after its layer (ReLU commutes
+    with the rounding); xyz and the folded biases beta (and the layer biases) enter as a ``dt``
+    hi + lo pair (~16 significant bits, DESIGN.md §3 'aux k-step'); the last hidden layer stays
+    unrounded (the 512 -> 1 layer is an fp32 dot with fp32 weights).  What is left between
+    this and the device is fp32 accumulation order only, so it pins the bf16/fp16 kernels far
+    tighter than the fp64 decoder can when the latents are large (their rounding error grows
+    with the activations' scale).  z: [B, L]; xyz: [P, 3] shared or [B, P, 3] -> [B, P]."""
+    def rd(t):
+        return t.to(torch.float32).to(dt).to(torch.float64)
+
+    def hilo(t):
+        hi = rd(t)
+        return hi + rd(t.to(torch.float64) - hi)
+
+    if z.dim() == 1:
+        z = z[None]
+    B = z.shape[0]
+    L = p.latent_dim
+    if xyz.dim() == 2:
+        xyz = xyz[None].expand(B, -1, -1)
+    beta = hilo(latent_fold(p, z.to(torch.float64)))
+    Ws = p.weights[p.skip]
+    hin = Ws.shape[1] - (L + 3)
+    out = []
+    for b in range(B):
+        x3 = hilo(xyz[b].to(torch.float64))
+        h = torch.relu(x3 @ rd(p.weights[0][:, L:L + 3]).T + beta[b, 0])
+        for l in range(1, p.n_linear):
+            if l == p.skip:
+                a = rd(h) @ rd(Ws[:, :hin]).T + x3 @ rd(Ws[:, hin + L:]).T + beta[b, 1]
+            elif l == p.n_linear - 1:
+                a = h @ p.weights[l].to(torch.float32).to(torch.float64).T \
+                    + p.biases[l].to(torch.float32).to(torch.float64)
+            else:
+                a = rd(h) @ rd(p.weights[l]).T + hilo(p.biases[l])
+            h = torch.relu(a) if l < p.n_linear - 1 else a
+        out.append(torch.tanh(h[:, 0]))
+    return torch.stack(out, 0)
+
+
 def decode_grid(p: DecoderParams, z: torch.Tensor, N: int, k0: int = 0,
                 k1: Optional[int] = None, chunk: int = 262144,
                 bbox: Tuple[float, float] = (-1.0, 1.0)) -> torch.Tensor:

@@ -81,3 +81,31 @@ def test_emulated_widen_skip_fp16():
     assert np.abs(emulate(packed, beta, xyz.numpy(), "fp16") - want).max() < 3e-3
     packed_q = pack.pack_decoder(p.weights, p.biases, 1024, "fp16", layout="quarter")
     assert np.abs(emulate_quarter(packed_q, beta, xyz.numpy(), "fp16") - want).max() < 3e-3
+
+
+@pytest.mark.parametrize("dtype,scale", [("bf16", 0.1), ("bf16", 0.5), ("fp16", 0.5)])
+def test_lowp_oracle_matches_emulated_kernel(dtype, scale):
+    """oracle decoder_forward_lowp (the 16-bit precision contract in fp64) against the
+    fragment-level kernel emulation (fp64 accumulation too): they agree far inside the 16-bit
+    rounding error itself, including at large latents where that error reaches 1e-2 -- which
+    is what lets the GPU tests pin the bf16 kernel tightly at any latent scale."""
+    p = R.make_decoder_params(seed=1234)
+    g = torch.Generator().manual_seed(3)
+    z = torch.randn(2, 256, generator=g, dtype=torch.float64) * scale
+    xyz = (torch.rand(2, 64, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    lowp = R.decoder_forward_lowp(p, z, xyz.double(), dt).numpy()
+    beta = R.latent_fold(p, z).float().numpy()
+    packed_q = pack.pack_decoder(p.weights, p.biases, 256, dtype, layout="quarter")
+    emu = emulate_quarter(packed_q, beta, xyz.numpy(), dtype)
+    full = R.decoder_forward(p, z, xyz.double()).numpy()
+    d = np.abs(emu - lowp)
+    err, med = d.max(), np.median(d)
+    rnd = np.abs(full - lowp).max()
+    print(f"{dtype} z*{scale}: |emu - lowp| max {err:.2e} median {med:.2e}, "
+          f"rounding error itself {rnd:.2e}")
+    # identical arithmetic up to summation order: most points agree to ~1e-8; a point whose
+    # pre-activation sits at a 16-bit rounding tie may round the other way (one ulp of one
+    # activation: <= ~5e-4 seen at z*0.5)
+    assert med < 1e-6, med
+    assert err < 1e-3, err
