@@ -65,12 +65,13 @@ typedef struct ldm_decoder {
     const float* wxyz;    /* fp32 [2][H][3]  xyz columns of layer 0 and layer 4 */
     const float* w_last;  /* fp32 [H] final 512->1 weights (bf16/f16: MFMA-row permuted) */
     float b_last;         /* final bias */
-    int32_t layout;       /* bf16/f16 stage-blob layout: LDM_LAYOUT_PASS8 or LDM_LAYOUT_QUARTER */
+    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_PASS8, _QUARTER or _SPLIT */
 } ldm_decoder_t;
 
 /* Stage-blob layouts of the MFMA decoder. */
 #define LDM_LAYOUT_PASS8 0   /* 8 m-chunks x 1 k-step per stage, 2 passes per layer */
 #define LDM_LAYOUT_QUARTER 1 /* 4 m-chunks x 2 k-steps per stage, 4 quarters per layer */
+#define LDM_LAYOUT_SPLIT 2   /* features split over the 4 waves, per-wave weight streams */
 
 /* DDPM tables, fp32 device arrays of length T. */
 typedef struct ldm_sched {

@@ -206,6 +206,116 @@ def pack_stage_blob_quarter(pieces: Dict[str, torch.Tensor], dt: torch.dtype) ->
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# "split" layout (csrc/decoder_fs.hip): the FEATURES of every layer are split
+# over the 4 waves of a workgroup, the 128 points of a tile are shared through an LDS activation
+# buffer.  Wave w owns output rows [128w, 128w+128) of every 512-wide layer, as two PARTS of
+# 64 rows (2 m-chunks); layer 3 at skip width 253 (padded 256) has one part of rows
+# [64w, 64w+64).  Each wave streams ITS OWN weight fragments (2 per k-step) from L2 straight
+# into registers: every weight byte still feeds the tile's 128 points, but each A fragment read
+# feeds 4 MFMAs (4 point chunks) instead of 1.
+# ------------------------------------------------------------------------------------------
+SPLIT_WAVES = 4
+
+
+def split_parts(skip_width: int) -> List[Tuple[int, int]]:
+    """(layer, part) in the kernel's order (csrc/decoder_fs.hip)."""
+    S = skip_pad(skip_width)
+    parts = [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0), (2, 1)]
+    parts += [(3, 0)] if S == 256 else [(3, 0), (3, 1)]
+    parts += [(l, p) for l in (4, 5, 6, 7) for p in (0, 1)]
+    return parts
+
+
+def split_nk(layer: int, skip_width: int) -> int:
+    """Ring k-steps (16 features each) of one part of ``layer`` (the aux step not counted)."""
+    return 0 if layer == 0 else (skip_pad(skip_width) // 16 if layer == 4 else 32)
+
+
+def split_kidx(layer: int, skip_width: int) -> np.ndarray:
+    """Input k-step consumed at ring step j of ``layer``.  The previous layer's activations sit
+    in LDS as 32 k-steps of 16 features; when it was 512 wide (two parts per wave) its part 0
+    ("early", k-steps 8w..8w+3) is written at the layer boundary and its part 1 ("late",
+    8w+4..8w+7) during this layer's first steps, so early k-steps are consumed first:
+    step j = 16u + 4g + r reads k-step 8g + 4u + r.  After the one-part layer 3 (skip 253) the
+    16 k-steps are read in order."""
+    nk = split_nk(layer, skip_width)
+    j = np.arange(nk)
+    if layer == 4 and skip_pad(skip_width) == 256:
+        return j
+    return 8 * ((j >> 2) & 3) + 4 * (j >> 4) + (j & 3)
+
+
+def split_row_base(layer: int, part: int, wave: int, skip_width: int) -> int:
+    if layer == 3 and skip_pad(skip_width) == 256:
+        return 64 * wave
+    return 128 * wave + 64 * part
+
+
+def split_stream_steps(skip_width: int) -> int:
+    return sum(split_nk(l, skip_width) for (l, _) in split_parts(skip_width))
+
+
+def pack_split(pieces: Dict[str, torch.Tensor], dt: torch.dtype) -> Tuple[torch.Tensor, int]:
+    """Split-layout blob: ``stream [4 waves][n_steps][2 frags][64 lanes][8]`` then
+    ``bias_aux [4 waves][n_parts][2 frags][64 lanes][8]``.  Stream element (wave w, step s of
+    part (l, p) at ring step j, m-chunk i, lane ln, elem e) =
+    ``W_l[row_base + 32 i + (ln & 31), 16 kidx_l(j) + PERM[8 (ln >> 5) + e]]``.  The bias aux
+    fragment of a part (lanes < 32, row ``row_base + 32 i + ln``) is
+    ``[0,0,0,0,0,0,b_hi,b_lo]``; the parts of layers 0 and 4 are per shape (workspace, filled
+    by the kernel's aux pack) and stay zero here.  Returns (flat blob, n_steps)."""
+    sw = pieces["skip_width"]
+    S = skip_pad(sw)
+    parts = split_parts(sw)
+    nsteps = split_stream_steps(sw)
+    lanes = np.arange(64)
+    rows_l = torch.from_numpy(lanes & 31)
+    kcols = torch.from_numpy(np.array([[PERM[8 * (l >> 5) + j] for j in range(8)]
+                                       for l in lanes]))                          # [64, 8]
+    padded = {}
+    for l in range(1, 8):
+        w = pieces["main"][l]
+        M = S if l == 3 else H
+        K = S if l == 4 else H
+        wp = torch.zeros(M, K, dtype=torch.float64)
+        wp[:w.shape[0], :w.shape[1]] = w
+        padded[l] = _round(wp, dt)
+    stream = torch.zeros(SPLIT_WAVES, nsteps, 2, 64, 8, dtype=dt)
+    aux = torch.zeros(SPLIT_WAVES, len(parts), 2, 64, 8, dtype=dt)
+    for w in range(SPLIT_WAVES):
+        s0 = 0
+        for pi, (l, p) in enumerate(parts):
+            rb = split_row_base(l, p, w, sw)
+            rows = (rb + 32 * torch.arange(2))[:, None] + rows_l[None, :]           # [2, 64]
+            if l not in (0, 4):
+                b = pieces["bias"][l]
+                bp = torch.zeros(S if l == 3 else H, dtype=torch.float64)
+                bp[:b.shape[0]] = b
+                hi, lo = _hi_lo(bp, dt)
+                aux[w, pi, :, :32, 6] = hi[rows[:, :32]]
+                aux[w, pi, :, :32, 7] = lo[rows[:, :32]]
+            if l == 0:
+                continue
+            kidx = torch.from_numpy(split_kidx(l, sw))
+            nk = kidx.numel()
+            cols = kidx[:, None, None] * 16 + kcols[None]                           # [nk, 64, 8]
+            wp = padded[l]
+            # [nk, 2, 64, 8]: W[rows[i, ln], cols[j, ln, e]]
+            stream[w, s0:s0 + nk] = wp[rows[None, :, :, None], cols[:, None, :, :]]
+            s0 += nk
+        assert s0 == nsteps
+    return torch.cat([stream.reshape(-1), aux.reshape(-1)]), nsteps
+
+
+def permute_w_last_split(w_last: torch.Tensor) -> torch.Tensor:
+    """Final-layer weights in the split kernel's accumulator order:
+    ``wl[w][p][i][h][v] = w8[128 w + 64 p + 32 i + (v & 3) + 8 (v >> 2) + 4 h]``."""
+    idx = [128 * w + 64 * p + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * h
+           for w in range(4) for p in range(2) for i in range(2) for h in range(2)
+           for v in range(16)]
+    return w_last.to(torch.float32)[torch.tensor(idx)]
+
+
 def permute_w_last(w_last: torch.Tensor) -> torch.Tensor:
     """``wl[(mc*2 + h)*16 + r] = w8[32 mc + (r&3) + 8 (r>>2) + 4 h]`` (accumulator row order)."""
     idx = [32 * mc + (r & 3) + 8 * (r >> 2) + 4 * h
@@ -227,7 +337,8 @@ def pack_f32_blob(pieces: Dict[str, torch.Tensor]) -> torch.Tensor:
 def pack_decoder(weights, biases, latent_dim: int, dtype: str,
                  layout: str = "quarter") -> Dict[str, object]:
     """All host-side arrays of an ``ldm_decoder_t`` for ``dtype`` in {fp32, bf16, fp16}; the
-    16-bit stage blob in ``layout`` ("quarter": csrc/decoder_q.hip, "pass8": decoder.hip)."""
+    16-bit weights in ``layout`` ("split": csrc/decoder_fs.hip, "quarter": decoder_q.hip,
+    "pass8": decoder.hip)."""
     pieces = canonical_pieces(weights, biases, latent_dim)
     out = {
         "skip_width": pieces["skip_width"],
@@ -242,6 +353,12 @@ def pack_decoder(weights, biases, latent_dim: int, dtype: str,
         out["weights"] = pack_f32_blob(pieces)
         out["w_last"] = pieces["w_last"].to(torch.float32).contiguous()
         out["n_stages"] = 0
+    elif dtype in ("bf16", "fp16") and layout == "split":
+        dt = torch.bfloat16 if dtype == "bf16" else torch.float16
+        blob, nst = pack_split(pieces, dt)
+        out["weights"] = blob.contiguous()
+        out["w_last"] = permute_w_last_split(pieces["w_last"]).contiguous()
+        out["n_stages"] = nst
     elif dtype in ("bf16", "fp16"):
         dt = torch.bfloat16 if dtype == "bf16" else torch.float16
         blob = (pack_stage_blob_quarter(pieces, dt) if layout == "quarter"

@@ -67,7 +67,7 @@ def test_fold_matches_oracle(dev, decoder, small):
     assert (beta - want).abs().max() < 1e-5
 
 
-@pytest.mark.parametrize("layout", ["quarter", "pass8"])
+@pytest.mark.parametrize("layout", ["split", "quarter", "pass8"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
 def test_decode_grid_32_vs_golden(dev, decoder, small, dtype, layout):
     import ldm_sdf
@@ -83,7 +83,7 @@ def test_decode_grid_32_vs_golden(dev, decoder, small, dtype, layout):
     assert np.isfinite(sdf).all()
 
 
-@pytest.mark.parametrize("layout", ["quarter", "pass8"])
+@pytest.mark.parametrize("layout", ["split", "quarter", "pass8"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
 def test_decode_points_ragged_vs_golden(dev, decoder, small, dtype, layout):
     import ldm_sdf
@@ -120,14 +120,20 @@ def test_widen_skip_fp16(dev):
     assert dec.widen_skip and dec.skip_width == 512
     z = torch.from_numpy(g["z"]).to(dev)
     pts = torch.from_numpy(g["pts"]).to(dev)
-    for dt, lay in (("fp16", "quarter"), ("fp16", "pass8"), ("fp32", "quarter")):
+    for dt, lay in (("fp16", "split"), ("fp16", "quarter"), ("fp16", "pass8"),
+                    ("bf16", "split"), ("fp32", "quarter")):
         dec.DEFAULT_LAYOUT = lay
         got = ldm_sdf.decode_points(dec, z, pts, dtype=dt).cpu().double().numpy()
         assert np.abs(got - g["sdf_pts"]).max() <= TOL[dt], (dt, lay)
+        lowp = R.decoder_forward_lowp(p, z.cpu().double(), pts.cpu().double(),
+                                      torch.bfloat16 if dt == "bf16" else torch.float16)
+        if dt != "fp32":        # the 16-bit precision contract itself
+            assert np.abs(got - lowp.numpy()).max() <= 2e-3, (dt, lay)
 
 
 @pytest.mark.parametrize("dtype,layout", [("fp32", "quarter"), ("bf16", "quarter"),
-                                          ("bf16", "pass8")])
+                                          ("bf16", "pass8"), ("bf16", "split"),
+                                          ("fp16", "split")])
 def test_slab_equals_slice_bitwise(dev, decoder, small, dtype, layout):
     """Each point's value is independent of its tile/slab: slabs are bitwise slices."""
     from ldm_sdf import ops
@@ -144,7 +150,7 @@ def test_slab_equals_slice_bitwise(dev, decoder, small, dtype, layout):
     assert torch.equal(one[0], full[1])
 
 
-@pytest.mark.parametrize("layout", ["quarter", "pass8"])
+@pytest.mark.parametrize("layout", ["split", "quarter", "pass8"])
 def test_many_tiles_persistent_loop_subset(dev, decoder, layout):
     """64^3 x 3 shapes = 6144 tiles (> 1 per CU): spot-check vs the oracle on a subset."""
     import ldm_sdf
@@ -181,3 +187,32 @@ def test_errors_are_loud(dev, decoder):
         ldm_sdf.decode(decoder, torch.zeros(1, 256), 8)      # CPU tensor -> no fallback
     with pytest.raises(ValueError):
         ldm_sdf.decode(decoder, torch.zeros(1, 256, device=dev), 1)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("scale", [0.1, 0.5])
+def test_split_vs_lowp_oracle_and_quarter(dev, decoder, dtype, scale):
+    """The feature-split kernel (decoder_fs.hip) on 3 shapes x 1000 random points (8 tiles per
+    shape, ragged): within 2e-3 of the 16-bit precision-contract oracle (fp32 summation order
+    and rounding-tie flips only) and of the quarter kernel (which sums the k-steps in another
+    order), at the synthetic latent scale and at 5x it."""
+    import ldm_sdf
+    from oracle import ref_cpu as R
+    g = torch.Generator().manual_seed(17)
+    z = torch.randn(3, 256, generator=g) * scale
+    pts = torch.rand(3, 1000, 3, generator=g) * 2 - 1
+    p = R.make_decoder_params(seed=1234)
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float16
+    out = {}
+    for lay in ("split", "quarter"):
+        decoder.DEFAULT_LAYOUT = lay
+        try:
+            out[lay] = ldm_sdf.decode_points(decoder, z.to(dev), pts.to(dev),
+                                             dtype=dtype).cpu().double()
+        finally:
+            del decoder.DEFAULT_LAYOUT
+    lowp = R.decoder_forward_lowp(p, z.double(), pts.double(), dt)
+    e_lo = float((out["split"] - lowp).abs().max())
+    e_q = float((out["split"] - out["quarter"]).abs().max())
+    print(f"split {dtype} z*{scale}: vs lowp {e_lo:.2e}, vs quarter {e_q:.2e}")
+    assert e_lo <= 2e-3 and e_q <= 2e-3, (e_lo, e_q)

@@ -109,3 +109,24 @@ def test_lowp_oracle_matches_emulated_kernel(dtype, scale):
     # activation: <= ~5e-4 seen at z*0.5)
     assert med < 1e-6, med
     assert err < 1e-3, err
+
+
+@pytest.mark.parametrize("dtype,sw", [("bf16", 253), ("fp16", 253), ("fp16", 512)])
+def test_split_layout_emulation_matches_lowp_oracle(dtype, sw):
+    """The split layout (csrc/decoder_fs.hip) replayed on the CPU from the packed blob: same
+    numbers as the 16-bit precision-contract oracle (fp64 sums), for DeepSDF (skip 253) and the
+    widen-skip decoder (L = 1024); the stream length matches the kernel's constant."""
+    from tests.mfma_emulator import emulate_split
+    L = 256 if sw == 253 else 1024
+    p = R.make_decoder_params(L=L, widen_skip=(sw == 512), seed=1234)
+    g = torch.Generator().manual_seed(5)
+    z = torch.randn(2, L, generator=g, dtype=torch.float64) * 0.1
+    xyz = (torch.rand(2, 128, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    packed = pack.pack_decoder(p.weights, p.biases, L, dtype, layout="split")
+    assert packed["n_stages"] == (384 if sw == 253 else 448)
+    beta = R.latent_fold(p, z).float().numpy()
+    emu = emulate_split(packed, beta, xyz.numpy(), dtype)
+    lowp = R.decoder_forward_lowp(p, z, xyz.double(), dt).numpy()
+    d = np.abs(emu - lowp)
+    assert np.median(d) < 1e-6 and d.max() < 1e-3, (np.median(d), d.max())
