@@ -138,23 +138,30 @@ __device__ __forceinline__ void fs_bar() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// B fragments of input k-step kk for the 4 point chunks
-__device__ __forceinline__ void read_b(const FCtx& c, int kk, u32x4 (&b)[4]) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(c.smem + kk * 4096 + c.voff);
+// The activation buffer is kept in CONSUMPTION order: position j (4 KiB: 4 point chunks x
+// 1 KiB) holds the k-step that ring step j of the next layer reads (pack.split_kidx): after a
+// 512-wide layer, k-step 8w + 4u + 2i + s sits at position 16u + 4w + 2i + s (u = 0: part 0,
+// written at the layer boundary; u = 1: part 1, written during the next layer's first steps);
+// after layer 3 at skip 253, k-step 4w + 2i + s at position 4w + 2i + s.  So step j reads
+// position j: the addresses are immediates from one group base.
+__device__ __forceinline__ void read_b(const FCtx& c, int pos, u32x4 (&b)[4]) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(c.smem + pos * 4096 + c.voff);
 #pragma unroll
     for (int n = 0; n < 4; ++n) b[n] = p[n * 64];
 }
 
-// k order of a part: el (previous layer 512 wide): step j = 16u + 4g + r reads k-step
-// 8g + 4u + r (early k-steps first); else k-step j.
-__device__ __forceinline__ int kidx(int j, bool el) {
-    return el ? 8 * ((j >> 2) & 3) + 4 * (j >> 4) + (j & 3) : j;
+// Stream step r (0..3) of the 4-step stream group at c.s_iss into ring slot `slot`: the
+// (r & 1) * 2 KiB + fragment offset folds into the load's immediate, the (r >> 1) * 4 KiB into
+// the scalar offset, so a group costs one wrap test instead of one per step.
+__device__ __forceinline__ void issue(FCtx& c, int slot, int r) {
+    const uint32_t so = c.s_iss + (uint32_t)(r >> 1) * 2u * kFsStep;
+    const uint32_t vo = c.voff + (uint32_t)(r & 1) * kFsStep;
+    c.ring[slot][0] = bld(c.rw, vo, so);
+    c.ring[slot][1] = bld(c.rw, vo + 1024u, so);
 }
 
-__device__ __forceinline__ void issue(FCtx& c, int r) {
-    c.ring[r][0] = bld(c.rw, c.voff, c.s_iss);
-    c.ring[r][1] = bld(c.rw, c.voff + 1024u, c.s_iss);
-    c.s_iss += kFsStep;
+__device__ __forceinline__ void next_group(FCtx& c) {
+    c.s_iss += 4u * kFsStep;
     if (c.s_iss == c.s_end) c.s_iss = c.s_beg;
 }
 
@@ -162,11 +169,11 @@ __device__ __forceinline__ void issue(FCtx& c, int r) {
 template <typename T, int EK>
 __device__ __forceinline__ void epi_tile(FCtx& c, const f32x16 (&accY)[2][4], int t, int fin_p) {
     const int i = t >> 2, n = t & 3;
-    if (EK == FE_LDS) {          // last part of the previous layer -> its "late" k-steps
+    if (EK == FE_LDS) {          // last part of the previous layer -> its "late" positions
         u32x4 f0, f1;
         acc_to_frags<T>(accY[i][n], f0, f1);
-        const int kk = 8 * c.wave + 4 + 2 * i;
-        u32x4* p = reinterpret_cast<u32x4*>(c.smem + (kk * 4 + n) * 1024 + c.voff);
+        const int pos = 16 + 4 * c.wave + 2 * i;
+        u32x4* p = reinterpret_cast<u32x4*>(c.smem + (pos * 4 + n) * 1024 + c.voff);
         p[0] = f0;
         p[4 * 64] = f1;            // k-step kk + 1
     } else if (EK == FE_PARK) {
@@ -198,18 +205,44 @@ __device__ __forceinline__ void mfma8(f32x16 (&acc)[2][4], const u32x4 a0, const
 // Four k-steps j0..j0+3 (ring slots RO..RO+3).  E work: tiles T0..T0+3 of the other set
 // (EK != FE_NONE).  The next step's B fragments are read unconditionally (no selects in the
 // loop): at the mid barrier and at a part's end that read is stale or unused and the caller
-// reads again (kidx(nk) stays inside the LDS allocation).
+// reads again (position 32 is still inside the LDS allocation).  A scheduling barrier closes
+// every step: left free, the scheduler sank all of a group's weight loads to its end, which
+// left one step of latency cover instead of FS_D.
 template <typename T, int EK, int T0, int RO>
 __device__ __forceinline__ void group4(FCtx& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
-                                       u32x4 (&b)[4], int j0, bool el, int fin_p) {
+                                       u32x4 (&b)[4], int j0, int fin_p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int j = j0 + r;
-        mfma8<T>(acc, c.ring[RO + r][0], c.ring[RO + r][1], b);
-        issue(c, RO + r);
-        read_b(c, kidx(j + 1, el), b);
+        // rolling B fragments: chunk n of step j+1 is read as soon as step j's two MFMAs on
+        // chunk n are issued, ~6 MFMAs (~190 cycles) before it is needed (a read after the
+        // step's last MFMA left ~32 cycles of cover: an LDS round trip exposed per step)
+        const u32x4* nb = reinterpret_cast<const u32x4*>(c.smem + (j0 + r + 1) * 4096 + c.voff);
+        const u32x4 a0 = c.ring[RO + r][0], a1 = c.ring[RO + r][1];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            acc[0][n] = Elem<T>::mfma(a0, b[n], acc[0][n]);
+            acc[1][n] = Elem<T>::mfma(a1, b[n], acc[1][n]);
+            b[n] = nb[n * 64];
+        }
+        issue(c, RO + r, r);
         if (EK != FE_NONE) epi_tile<T, EK>(c, accY, T0 + r, fin_p);
+        // pin the step's order for the scheduler (it otherwise sinks the B reads and weight
+        // loads below the last MFMA): per point chunk n, MFMA, [VALU], MFMA, B read, [VALU];
+        // then the 2 weight loads.  E steps spread their VALU (AGPR reads, cvt, ReLU) 4 per
+        // MFMA gap (the guide: <= 5 fillers per 32x32x16 gap hide).
+        constexpr int V = EK == FE_NONE ? 0 : 4;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (V) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if (V) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
+    next_group(c);
 }
 
 // One part: aux step (zero-initialises acc), then nk ring steps; the other set's epilogue
@@ -217,10 +250,10 @@ __device__ __forceinline__ void group4(FCtx& c, f32x16 (&acc)[2][4], const f32x1
 // every wave during steps 0..7).  `naux`: aux fragments of the NEXT part (loaded here).
 template <typename T, int EK>
 __device__ __forceinline__ void run_part(FCtx& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
-                                         int nk, bool el, bool mid, FSrc naux, int fin_p) {
+                                         int nk, bool mid, FSrc naux, int fin_p) {
     const f32x16 zero = {};
     u32x4 b[4];
-    if (nk > 0) read_b(c, kidx(0, el), b);
+    if (nk > 0) read_b(c, 0, b);
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         acc[0][n] = Elem<T>::mfma(c.auxn[0], c.xyzf[n], zero);
@@ -229,20 +262,20 @@ __device__ __forceinline__ void run_part(FCtx& c, f32x16 (&acc)[2][4], const f32
     load_aux(c, naux);
     if (nk == 0) return;
     // steps 0..7 carry the epilogue of the other set (ring slots 0..7)
-    group4<T, EK, 0, 0>(c, acc, accY, b, 0, el, fin_p);
-    group4<T, EK, 4, (FS_D == 8 ? 4 : 0)>(c, acc, accY, b, 4, el, fin_p);
+    group4<T, EK, 0, 0>(c, acc, accY, b, 0, fin_p);
+    group4<T, EK, 4, (FS_D == 8 ? 4 : 0)>(c, acc, accY, b, 4, fin_p);
 #pragma unroll 1
     for (int j0 = 8; j0 < nk; j0 += FS_D) {
         if (mid && j0 == 16) {
             fs_bar();
-            read_b(c, kidx(16, el), b);      // the late k-steps, now written by every wave
+            read_b(c, 16, b);                // the late positions, now written by every wave
         }
-        group4<T, FE_NONE, 0, 0>(c, acc, accY, b, j0, el, 0);
-        if (FS_D == 8) group4<T, FE_NONE, 0, 4>(c, acc, accY, b, j0 + 4, el, 0);
+        group4<T, FE_NONE, 0, 0>(c, acc, accY, b, j0, 0);
+        if (FS_D == 8) group4<T, FE_NONE, 0, 4>(c, acc, accY, b, j0 + 4, 0);
     }
 }
 
-// serial epilogue of a whole set into LDS k-steps kbase + 2i + s
+// serial epilogue of a whole set into LDS positions kbase + 2i + s
 template <typename T>
 __device__ __forceinline__ void acc_to_lds(FCtx& c, const f32x16 (&acc)[2][4], int kbase) {
 #pragma unroll
@@ -257,14 +290,14 @@ __device__ __forceinline__ void acc_to_lds(FCtx& c, const f32x16 (&acc)[2][4], i
         }
 }
 
-// layer boundary after a two-part layer: park -> early k-steps 8w + 2i + s
+// layer boundary after a two-part layer: park -> "early" positions 4w + 2i + s
 __device__ __forceinline__ void park_to_lds(FCtx& c) {
     fs_bar();                      // every wave is done reading this layer's inputs
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            u32x4* p = reinterpret_cast<u32x4*>(c.smem + ((8 * c.wave + 2 * i) * 4 + n) * 1024 +
+            u32x4* p = reinterpret_cast<u32x4*>(c.smem + ((4 * c.wave + 2 * i) * 4 + n) * 1024 +
                                                 c.voff);
             p[0] = c.park[i][n][0];
             p[4 * 64] = c.park[i][n][1];
@@ -303,7 +336,10 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
     auto shp = [&](int slot) -> FSrc { return FSrc{true, c.aux_w + (uint32_t)slot * kFsStep}; };
     c.aux_w = shape_aux(blockIdx.x);
 #pragma unroll
-    for (int r = 0; r < FS_D; ++r) issue(c, r);
+    for (int r = 0; r < FS_D; ++r) {
+        issue(c, r, r & 3);
+        if ((r & 3) == 3) next_group(c);
+    }
     load_aux(c, shp(0));                                // layer 0 part 0 of the first tile
 
     f32x16 accA[2][4], accB[2][4];
@@ -341,8 +377,8 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
         for (int n = 0; n < 4; ++n) c.part[n] = 0.f;
 
         // ---- layer 0 (aux only): part 0 -> A, part 1 -> B; A parked, B deferred into L1
-        run_part<T, FE_NONE>(c, accA, accB, 0, false, false, shp(1), 0);
-        run_part<T, FE_NONE>(c, accB, accA, 0, false, false, bias(2), 0);
+        run_part<T, FE_NONE>(c, accA, accB, 0, false, shp(1), 0);
+        run_part<T, FE_NONE>(c, accB, accA, 0, false, bias(2), 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -356,37 +392,37 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
         for (int l = 1; l < L2P; ++l, pi += 2) {
             // the part after layer 3 (512 wide) is layer 4's: per-shape aux
             const FSrc nx = (S == 512 && l == 3) ? shp(2) : bias(pi + 2);
-            run_part<T, FE_LDS>(c, accA, accB, 32, true, true, bias(pi + 1), 0);
-            run_part<T, FE_PARK>(c, accB, accA, 32, true, false, nx, 0);
+            run_part<T, FE_LDS>(c, accA, accB, 32, true, bias(pi + 1), 0);
+            run_part<T, FE_PARK>(c, accB, accA, 32, false, nx, 0);
             park_to_lds(c);
         }
         if (S == 256) {
             // layer 3, one part of rows 64w..64w+63 -> LDS k-steps 4w..4w+3 (serial)
-            run_part<T, FE_LDS>(c, accA, accB, 32, true, true, shp(2), 0);
+            run_part<T, FE_LDS>(c, accA, accB, 32, true, shp(2), 0);
             fs_bar();
             acc_to_lds<T>(c, accA, 4 * c.wave);
             fs_bar();
             // layer 4 (K = 256 in order)
-            run_part<T, FE_NONE>(c, accA, accB, 16, false, false, shp(3), 0);
-            run_part<T, FE_PARK>(c, accB, accA, 16, false, false, bias(pi + 3), 0);
+            run_part<T, FE_NONE>(c, accA, accB, 16, false, shp(3), 0);
+            run_part<T, FE_PARK>(c, accB, accA, 16, false, bias(pi + 3), 0);
             park_to_lds(c);
             pi += 3;
         } else {
-            run_part<T, FE_LDS>(c, accA, accB, 32, true, true, shp(3), 0);
-            run_part<T, FE_PARK>(c, accB, accA, 32, true, false, bias(pi + 2), 0);
+            run_part<T, FE_LDS>(c, accA, accB, 32, true, shp(3), 0);
+            run_part<T, FE_PARK>(c, accB, accA, 32, false, bias(pi + 2), 0);
             park_to_lds(c);
             pi += 2;
         }
         // ---- layers 5, 6
 #pragma unroll 1
         for (int l = 5; l < 7; ++l, pi += 2) {
-            run_part<T, FE_LDS>(c, accA, accB, 32, true, true, bias(pi + 1), 0);
-            run_part<T, FE_PARK>(c, accB, accA, 32, true, false, bias(pi + 2), 0);
+            run_part<T, FE_LDS>(c, accA, accB, 32, true, bias(pi + 1), 0);
+            run_part<T, FE_PARK>(c, accB, accA, 32, false, bias(pi + 2), 0);
             park_to_lds(c);
         }
         // ---- layer 7: part 0 folds into the dot product during part 1; part 1 after it
-        run_part<T, FE_LDS>(c, accA, accB, 32, true, true, bias(pi + 1), 0);
-        run_part<T, FE_FIN>(c, accB, accA, 32, true, false, FSrc{true, c.aux_next}, 0);
+        run_part<T, FE_LDS>(c, accA, accB, 32, true, bias(pi + 1), 0);
+        run_part<T, FE_FIN>(c, accB, accA, 32, false, FSrc{true, c.aux_next}, 0);
 #pragma unroll
         for (int t = 0; t < 8; ++t) epi_tile<T, FE_FIN>(c, accB, t, 1);
         // ---- final layer across waves: lanes l and l^32 hold the same point

@@ -14,7 +14,7 @@ R = int(os.environ.get("DEC_R", "3"))
 dtype = os.environ.get("DEC_DTYPE", "bf16")
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)
-pk = dec.device_pack(dtype, dev)
+pk = dec.device_pack(dtype, dev, layout=os.environ.get("DEC_LAYOUT") or None)
 z = torch.randn(B, 256, device=dev) * 0.1
 beta = ops.decoder_fold(pk["desc"], z)
 out = torch.empty(B, N, N, N, device=dev)

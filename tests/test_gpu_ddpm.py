@@ -606,8 +606,9 @@ def test_config3_bounded_sample8_then_decode128_unscaled(dev, den):
     """Config 3 on bounded latents: sample(8) through the default loop, then the bf16 128^3
     decode of those latents AS SAMPLED (no rescaling; they are ~5x the synthetic-latent scale),
     600 random points per shape against (a) the oracle at the bf16 precision contract
-    (decoder_forward_lowp: 16-bit operands, fp64 sums) within 2e-3 -- fp32 summation order and
-    rare rounding-tie flips -- and (b) the fp64 decoder within 2.5e-2: the bf16 rounding error
+    (decoder_forward_lowp: 16-bit operands, fp64 sums): median within 2e-5 (fp32 summation
+    order), max within 6e-3 (rare 16-bit rounding-tie flips at these larger activations) -- and
+    (b) the fp64 decoder within 2.5e-2: the bf16 rounding error
     grows with the activations' scale (1.2e-2 measured here, 1.5e-2 on CPU at z*0.5, vs 3e-3 at
     the 0.1 scale SURVEY §8(c)'s 1e-2 was set for).  The SDFs are not saturated."""
     import ldm_sdf
@@ -637,6 +638,9 @@ def test_config3_bounded_sample8_then_decode128_unscaled(dev, den):
         full = R.decoder_forward(pd, zc[b:b + 1], grid[idx[b]])[0]
         e_lo = float((got[b] - lowp).abs().max())
         e_64 = float((got[b] - full).abs().max())
-        print(f"config3 bounded shape {b}: vs bf16-contract oracle {e_lo:.2e}, vs fp64 {e_64:.2e}")
-        assert e_lo <= 2e-3, (b, e_lo)
+        m_lo = float((got[b] - lowp).abs().median())
+        print(f"config3 bounded shape {b}: vs bf16-contract oracle {e_lo:.2e} (median "
+              f"{m_lo:.1e}), vs fp64 {e_64:.2e}")
+        assert m_lo <= 2e-5, (b, m_lo)          # fp32 summation noise at most points
+        assert e_lo <= 6e-3, (b, e_lo)          # + rare 16-bit rounding-tie flips
         assert e_64 <= 2.5e-2, (b, e_64)

@@ -212,7 +212,15 @@ def test_split_vs_lowp_oracle_and_quarter(dev, decoder, dtype, scale):
         finally:
             del decoder.DEFAULT_LAYOUT
     lowp = R.decoder_forward_lowp(p, z.double(), pts.double(), dt)
-    e_lo = float((out["split"] - lowp).abs().max())
-    e_q = float((out["split"] - out["quarter"]).abs().max())
-    print(f"split {dtype} z*{scale}: vs lowp {e_lo:.2e}, vs quarter {e_q:.2e}")
-    assert e_lo <= 2e-3 and e_q <= 2e-3, (e_lo, e_q)
+    d_lo = (out["split"] - lowp).abs()
+    d_q = (out["split"] - out["quarter"]).abs()
+    e_lo, e_q = float(d_lo.max()), float(d_q.max())
+    m_lo = float(d_lo.median())
+    print(f"split {dtype} z*{scale}: vs lowp max {e_lo:.2e} median {m_lo:.2e}, "
+          f"vs quarter {e_q:.2e}")
+    # fp32 sums in another order + a rare activation rounding the other way at a 16-bit tie
+    # (one ulp of one activation, ~1e-3 downstream; more such ties at larger latents):
+    # the median stays at fp32 noise, the max within a third of the rounding error itself
+    bound = 3e-3 if scale <= 0.1 else 6e-3
+    assert m_lo <= 2e-5, m_lo
+    assert e_lo <= bound and e_q <= bound, (e_lo, e_q)
