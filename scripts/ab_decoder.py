@@ -16,7 +16,7 @@ R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 # variants: "p<sched>" = pass8 layout with LDM_DECODER_SCHED=<sched> (needs the `make DEV=1`
 # library for sched != 4), "q" = quarter layout, "s" = split layout
 VARIANTS = os.environ.get("AB_VARIANTS", "s,q").split(",")
-LAYOUT = {"q": "quarter", "s": "split"}
+LAYOUT = {"q": "quarter", "s": "split", "s4": "split", "s8": "split"}
 FLOPS = 3146752
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)
@@ -31,6 +31,8 @@ for dtype in os.environ.get("AB_DTYPES", "bf16").split(","):
         for v in VARIANTS:
             if v.startswith("p"):
                 os.environ["LDM_DECODER_SCHED"] = v[1:]
+            if v in ("s4", "s8"):                  # split ring depth (dev build)
+                os.environ["LDM_FS_D"] = v[1:]
             e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
             e0.record()
             ops.decoder_grid_fwd(pks[v]["desc"], beta, N, 0, N, out=out)
