@@ -7,23 +7,28 @@
 //     64 rows (2 m-chunks of 32); the one-part layer 3 of DeepSDF (253 -> 256) gives each wave
 //     rows [64w, 64w+64);
 //   * the tile's activations live once, in LDS, as B fragments (128 KiB, 32 positions of 4
-//     point chunks x 1 KiB); every wave reads every position's 4 B fragments;
+//     point chunks x 1 KiB; position 32 = the tile's xyz fragments of the aux steps); every
+//     wave reads every position's 4 B fragments;
 //   * each wave streams ITS OWN weight fragments (2 per k-step, 2 KiB) from L2 straight into a
-//     register ring (raw buffer loads, FS_D k-steps ahead): no LDS ring, no DMA barrier.
+//     register ring (raw buffer loads, kFsD k-steps ahead): no LDS ring, no DMA barrier.
 //     Per k-step a wave reads 2 A fragments (L2) + 4 B fragments (LDS) for 8 MFMAs: each
 //     fragment feeds 4 (A) or 2 (B) MFMAs, where the quarter kernel read one LDS fragment per
 //     MFMA; the weight bytes per point are unchanged (each feeds the tile's 128 points).
 //   * a part's accumulators (2 m x 4 n tiles = 128 fp32) alternate between two sets A and B,
-//     and a finished set is converted (16-bit + ReLU) straight into LDS inside 8 k-steps of a
-//     LATER part, one tile per step, between its MFMAs:
+//     and a finished set is converted (16-bit + ReLU) straight into LDS inside a 16-step
+//     window of a LATER part, half a tile per step, between its MFMAs:
 //       - a layer's part 1 (set B) -> the "late" positions 16..31, during the next layer's
-//         part 0 steps 0-7; that part meets a barrier at its step 16 before reading them;
+//         part 0 steps 0-14; a barrier inside its step 15 publishes them;
 //       - a layer's part 0 (set A) -> the "early" positions 0..15, during the SAME layer's
-//         part 1 steps 16-23: part 1 reads the early positions in steps 0-15, so after a
-//         barrier at its step 16 no wave reads them any more; the next layer's part 0
-//         publishes them with a barrier after its aux step;
-//       - layer 7's parts fold into the final 512 -> 1 dot product instead (fp32, w_last).
-//     No activation is parked in registers and no layer boundary writes LDS serially.
+//         part 1 steps 16-30: part 1 reads the early positions in steps 0-15, so after the
+//         barrier inside its step 15 no wave reads them any more; the barrier inside its
+//         step 31 publishes them to the next layer;
+//       - layer 7's parts fold into the final 512 -> 1 dot product instead (fp32, w_last):
+//         part 0 during part 1, part 1 during the NEXT tile's layer 1 part 0 (which also
+//         stores the previous tile's outputs).
+//     The barriers sit INSIDE a step, after its first MFMA pair, so the next position's reads
+//     after them stay covered by the step's remaining MFMAs.  Serial LDS writes: layer 0
+//     (both parts) and layer 3 of DeepSDF.
 //   * the bias (and, for layers 0 and 4, xyz + the folded latent) enters as one aux MFMA step
 //     at the START of each part (A = [wx,wy,wz,wx,wy,wz,b_hi,b_lo], B = [x_hi,y_hi,z_hi,x_lo,
 //     y_lo,z_lo,1,1]), which also zero-initialises the accumulators.
@@ -34,15 +39,18 @@ namespace ldm {
 namespace {
 using namespace dec;
 
-// FS_D: k-steps of A fragments in flight per wave (register ring depth), 4 or 8; the product
-// uses kFsDefaultD, the other depth is instantiated for A/B runs of the dev build
-constexpr int kFsDefaultD = 4;
+// k-steps of A fragments in flight per wave (register ring depth = one 4-step stream group)
+constexpr int kFsD = 4;
+// FV (kernel variant, template): bit 0 = an in-stream barrier sits after the step's SECOND
+// MFMA pair instead of its first (dev-build A/B: LDM_FS_BP=1)
+constexpr int kFsDefaultV = 0;
 
 constexpr int kFsStep = 2048;                       // one wave's A fragments of one k-step
-constexpr int kFsAct = 32 * 4 * 1024;               // 128 KiB activation buffer
-constexpr int kFsRed = 4 * 4 * 32 * 4;              // final partials [wave][n][32] fp32
+// activation buffer: 32 positions of 4 KiB + position 32 = the tile's aux B fragments
+// [x_hi,y_hi,z_hi,x_lo,y_lo,z_lo,1,1] (every part's last step reads it for the next aux step)
+constexpr int kFsAct = 33 * 4 * 1024;
+constexpr int kFsRed = 4 * 4 * 64 * 4;              // final partials [wave][n][64 lanes] fp32
 constexpr int kFsWl = 512 * 4;                      // permuted final-layer weights
-constexpr int kFsXyz = 4 * 4 * 1024;                // per-wave aux B fragments [wave][n][64]
 // Diagnostic build only (-DFS_STAMP=1, scripts/stamp_split.py; results are wrong): wave 0 of
 // every workgroup stamps s_memtime at part and layer boundaries of its second tile, dumped over
 // the output at the end.
@@ -50,7 +58,7 @@ constexpr int kFsXyz = 4 * 4 * 1024;                // per-wave aux B fragments 
 #define FS_STAMP 0
 #endif
 constexpr int kFsStamp = FS_STAMP ? 128 * 8 : 0;
-constexpr int kFsLds = kFsAct + kFsRed + kFsWl + kFsXyz + kFsStamp;
+constexpr int kFsLds = kFsAct + kFsRed + kFsWl + kFsStamp;
 static_assert(kFsLds <= 160 * 1024, "LDS");
 
 __host__ __device__ constexpr int fs_nparts(int S) { return S == 256 ? 15 : 16; }
@@ -101,7 +109,11 @@ struct FArgs {
 };
 
 // Epilogue kinds run inside 8 k-steps of a part (on the OTHER accumulator set)
-enum FsEpi { FE_NONE = 0, FE_LATE = 1, FE_EARLY = 2, FE_FIN = 3 };
+//   FE_FIN0: layer 7 part 0 (set A) -> the final dot product, during layer 7 part 1;
+//   FE_FIN1: layer 7 part 1 of the PREVIOUS tile (set B) -> the dot product, during layer 1 part
+//            0 of this one; its step 14 publishes the partials (the mid barrier) and the part
+//            sums them and stores the previous tile's outputs after that barrier
+enum FsEpi { FE_NONE = 0, FE_LATE = 1, FE_EARLY = 2, FE_FIN0 = 3, FE_FIN1 = 4 };
 
 // A fragment source: a buffer resource (SGPRs) + a byte offset (SGPR); the lane's 16 bytes at
 // voffset lane*16 (+1024: the second fragment, an immediate).  Raw buffer loads keep every
@@ -110,9 +122,10 @@ enum FsEpi { FE_NONE = 0, FE_LATE = 1, FE_EARLY = 2, FE_FIN = 3 };
 struct FSrc {
     bool shape;               // per-shape aux (workspace) or the weight blob
     uint32_t off;             // byte offset in that buffer
+    bool none = false;        // nothing to prefetch (the tile's last part)
 };
 
-template <int FS_D>
+template <int FV>
 struct FCtx {
     int lane, wave, h;
     uint32_t voff;            // lane * 16
@@ -125,15 +138,19 @@ struct FCtx {
     uint32_t aux_w;           // this tile's per-shape aux of this wave [4 slots][2 KiB] in ra
     uint32_t aux_next;        // ... of the next tile
     u32x4 auxn[2];            // aux A fragments of the part about to start
-    u32x4 ring[FS_D][2];
-    float part[4];
+    u32x4 ring[kFsD][2];
+    u32x4 b[4];               // the B fragments of the step about to run (rolling)
+    float part[4];            // final-layer partial sums of point chunk n
+    float* out;               // the previous tile's outputs (FE_FIN1): [shape][npts]
+    int npts, prev_shape, prev_local;   // prev_local < 0: no previous tile
+    float b_last;
     unsigned long long* st;   // FS_STAMP
     int st_i;
     bool st_on;
 };
 
-template <int FS_D>
-__device__ __forceinline__ void stamp(FCtx<FS_D>& c) {
+template <int FV>
+__device__ __forceinline__ void stamp(FCtx<FV>& c) {
     if (FS_STAMP) {
         if (c.st_on && c.lane == 0 && c.st_i < 128) c.st[c.st_i] = __builtin_readcyclecounter();
         ++c.st_i;
@@ -144,23 +161,52 @@ __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, ui
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-template <int FS_D>
-__device__ __forceinline__ void load_aux(FCtx<FS_D>& c, FSrc s) {
+template <int FV>
+__device__ __forceinline__ void load_aux(FCtx<FV>& c, FSrc s) {
+    if (s.none) return;
     const __amdgpu_buffer_rsrc_t r = s.shape ? c.ra : c.rw;
     c.auxn[0] = bld(r, c.voff, s.off);
     c.auxn[1] = bld(r, c.voff + 1024u, s.off);
 }
 
-// A lane's LDS byte address `voff + off` (off wave-uniform) as an OPAQUE VGPR: LDS immediates
-// are 16 bits, so positions past 64 KiB need a register base; left to itself the compiler
-// materialised one VGPR per (position, chunk) constant, hoisted them out of the tile loop and
-// spilled them.  The empty volatile asm is neither folded nor hoisted: one v_add per use site,
-// and every per-tile offset below it fits the immediate.
-template <int FS_D>
-__device__ __forceinline__ char* lds_at(const FCtx<FS_D>& c, uint32_t off) {
-    uint32_t v = c.voff + off;
+// A lane's LDS byte address `voff + off` (off wave-uniform: one v_add).
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
     asm volatile("" : "+v"(v));
-    return c.smem + v;
+    return v;
+}
+
+__device__ __forceinline__ int opaque_s(int v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+
+// LDS addressing.  Immediates are 16 bits, so most accesses need a register base past 64 KiB;
+// left to itself the compiler materialised one VGPR per constant address, hoisted them out of
+// the tile loop and spilled them -- and every spill reload waits vmcnt(0), i.e. for the whole
+// weight ring in flight.  So every address is formed AT ITS USE from an opaque copy of voff
+// (a volatile asm is neither hoisted nor folded): one or two VALU per use, nothing long-lived
+// but voff itself.
+template <int FV>
+__device__ __forceinline__ char* lds_at(const FCtx<FV>& c, uint32_t off) {
+    return c.smem + (opaque(c.voff) + off);
+}
+// this wave's early (0) / late (16) positions: + (2i + s) * 4 KiB + n * 1 KiB immediates
+template <int FV>
+__device__ __forceinline__ u32x4* act_w(const FCtx<FV>& c, int late) {
+    return reinterpret_cast<u32x4*>(lds_at(c, (uint32_t)(late + 4 * c.wave) * 4096u));
+}
+// final-layer weights of (this wave, part p, m-chunk i, this lane half)
+template <int FV>
+__device__ __forceinline__ const f32x4* wl_at(const FCtx<FV>& c, int p, int i) {
+    const uint32_t h = opaque(c.voff) >> 9;           // lane >> 5
+    return reinterpret_cast<const f32x4*>(
+        c.smem + kFsAct + kFsRed + (((c.wave * 2 + p) * 2 + i) * 2) * 64 + h * 64);
+}
+
+// this lane's final partials red[wave][n][lane] (+ n * 64 floats)
+template <int FV>
+__device__ __forceinline__ float* red_w(const FCtx<FV>& c) {
+    return reinterpret_cast<float*>(c.smem + kFsAct + c.wave * 4 * 64 * 4 + (opaque(c.voff) >> 2));
 }
 
 // LDS barrier: LDS writes done (lgkmcnt), then s_barrier.  The weight loads in flight
@@ -175,100 +221,182 @@ __device__ __forceinline__ void fs_bar() {
 // the "early" positions; u = 1: part 1, the "late" ones); after layer 3 at skip 253, k-step
 // 4w + 2i + s at position 16 + 4w + 2i + s (layer 4 reads positions 16 + j).  Step j reads
 // position pos0 + j: the addresses are immediates from one group base.
-template <int FS_D>
-__device__ __forceinline__ void read_b(const FCtx<FS_D>& c, int pos, u32x4 (&b)[4]) {
+template <int FV>
+__device__ __forceinline__ void read_b(FCtx<FV>& c, int pos) {
     const u32x4* p = reinterpret_cast<const u32x4*>(lds_at(c, pos * 4096));
 #pragma unroll
-    for (int n = 0; n < 4; ++n) b[n] = p[n * 64];
+    for (int n = 0; n < 4; ++n) c.b[n] = p[n * 64];
 }
 
-// Stream step r (0..3) of the 4-step stream group at c.s_iss into ring slot `slot`: the
+// Stream step r (0..3) of the 4-step stream group at c.s_iss into ring slot r: the
 // (r & 1) * 2 KiB + fragment offset folds into the load's immediate, the (r >> 1) * 4 KiB into
 // the scalar offset, so a group costs one wrap test instead of one per step.
-template <int FS_D>
-__device__ __forceinline__ void issue(FCtx<FS_D>& c, int slot, int r) {
+template <int FV>
+__device__ __forceinline__ void issue(FCtx<FV>& c, int r) {
     const uint32_t so = c.s_iss + (uint32_t)(r >> 1) * 2u * kFsStep;
     const uint32_t vo = c.voff + (uint32_t)(r & 1) * kFsStep;
-    c.ring[slot][0] = bld(c.rw, vo, so);
-    c.ring[slot][1] = bld(c.rw, vo + 1024u, so);
+    c.ring[r][0] = bld(c.rw, vo, so);
+    c.ring[r][1] = bld(c.rw, vo + 1024u, so);
 }
 
-template <int FS_D>
-__device__ __forceinline__ void next_group(FCtx<FS_D>& c) {
+template <int FV>
+__device__ __forceinline__ void next_group(FCtx<FV>& c) {
     c.s_iss += 4u * kFsStep;
     if (c.s_iss == c.s_end) c.s_iss = c.s_beg;
 }
 
-// one accumulator tile -> its two B fragments at LDS position pos, pos + 1 (point chunk n)
-template <typename T, int FS_D>
-__device__ __forceinline__ void tile_to_lds(FCtx<FS_D>& c, const f32x16& acc, int pos, int n) {
-    u32x4 f0, f1;
-    acc_to_frags<T>(acc, f0, f1);
-    u32x4* p = reinterpret_cast<u32x4*>(lds_at(c, (pos * 4 + n) * 1024));
-    p[0] = f0;
-    p[4 * 64] = f1;
+// ReLU of an fp32 value as ONE integer max: a negative float is a negative int32 (sign bit),
+// so max(bits, 0) is +0 for it and the value itself otherwise (fmaxf costs a NaN-quieting
+// v_max plus the max under IEEE mode: two instructions per element)
+__device__ __forceinline__ float relu_f(float x) {
+    return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
 }
 
-// One tile t = 4i + n of the other accumulator set's epilogue.
-template <typename T, int EK, int FS_D>
-__device__ __forceinline__ void epi_tile(FCtx<FS_D>& c, const f32x16 (&accY)[2][4], int t) {
+// One epilogue unit u = 2t + s of the other accumulator set: HALF of tile t = 4i + n (its
+// accumulator registers 8s..8s+7 = the B fragment of k-step 2i + s).
+template <typename T, int EK, int FV>
+__device__ __forceinline__ void epi_unit(FCtx<FV>& c, const f32x16 (&accY)[2][4], int u) {
+    const int t = u >> 1, s = u & 1;
     const int i = t >> 2, n = t & 3;
     if (EK == FE_LATE || EK == FE_EARLY) {   // part 1 of the previous layer / part 0 of this
-        u32x4 f0, f1;
-        acc_to_frags<T>(accY[i][n], f0, f1);
-        u32x4* p = reinterpret_cast<u32x4*>(
-            lds_at(c, (uint32_t)((EK == FE_LATE ? 16 : 0) + 4 * c.wave) * 4096u));
-        p[(2 * i * 4 + n) * 64] = f0;
-        p[((2 * i + 1) * 4 + n) * 64] = f1;
-    } else if (EK == FE_FIN) {     // part 0 of layer 7 -> the final dot product
-        const f32x4* w = reinterpret_cast<const f32x4*>(
-            c.smem + kFsAct + kFsRed + (((c.wave * 2 * 2 + i) * 2 + c.h) * 16) * 4);
+        u32x4 f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            f[q] = relu2(Elem<T>::pack(accY[i][n][8 * s + 2 * q], accY[i][n][8 * s + 2 * q + 1]));
+        u32x4* p = act_w(c, EK == FE_LATE ? 16 : 0);
+        p[((2 * i + s) * 4 + n) * 64] = f;
+    } else if (EK == FE_FIN0 || EK == FE_FIN1) {     // layer 7 -> the final dot product
+        const f32x4* w = wl_at(c, EK == FE_FIN0 ? 0 : 1, i);
         float part = c.part[n];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 2 * s; q < 2 * s + 2; ++q) {
             const f32x4 wv = w[q];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) part = fmaf(fmaxf(accY[i][n][4 * q + e], 0.f), wv[e], part);
+            for (int e = 0; e < 4; ++e) part = fmaf(relu_f(accY[i][n][4 * q + e]), wv[e], part);
         }
         c.part[n] = part;
     }
 }
 
-// Four k-steps reading positions p0..p0+3 (ring slots RO..RO+3).  E work: tiles T0..T0+3 of the
-// other set (EK != FE_NONE).  The next position's B fragments are read unconditionally (no
-// selects in the loop): at a barrier and at a part's end that read is stale or unused and the
-// caller reads again (position 32 is still inside the LDS allocation).
-template <typename T, int EK, int T0, int RO, int FS_D>
-__device__ __forceinline__ void group4(FCtx<FS_D>& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
-                                       u32x4 (&b)[4], int p0) {
+// The 16 units of an epilogue window of 16 steps k = 0..15: unit k in step k < 14, units 14
+// and 15 in step 14, none in step 15 -- so the window's LDS writes are all issued before the
+// barrier that closes it (inside step 15, see group4).
+template <typename T, int EK, int FV>
+__device__ __forceinline__ void epi_step(FCtx<FV>& c, const f32x16 (&accY)[2][4], int k) {
+    if (EK == FE_NONE || k == 15) return;
+    epi_unit<T, EK>(c, accY, k);
+    if (k == 14) epi_unit<T, EK>(c, accY, 15);
+    if (EK == FE_FIN1 && k == 14) {         // the partials -> red[wave][n][lane], published by
+        float* rw = red_w(c);               // the barrier inside step 15
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            rw[n * 64] = c.part[n];
+            c.part[n] = 0.f;
+        }
+    }
+}
+
+// the final layer across waves and lane halves (lanes l and l^32 hold the same point): lanes
+// < 32 of wave w sum point chunk w's 8 partials (after the barrier that published them), add
+// the bias, tanh, store
+template <int FV>
+__device__ __forceinline__ void fin_store(const FCtx<FV>& c, int shape, int local) {
+    const int lane = (int)(opaque(c.voff) >> 4);     // formed here: nothing kept live (spills)
+    if (local < 0 || lane >= 32) return;
+    const float* rr = reinterpret_cast<const float*>(
+        c.smem + kFsAct + c.wave * 64 * 4 + (opaque(c.voff) >> 2));
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += rr[w * 4 * 64] + rr[w * 4 * 64 + 32];
+    const int pt = local * kTilePoints + 32 * c.wave + lane;
+    if (pt < c.npts) {
+        // a buffer store off the shape's row (scalar base, 32-bit lane offset): a 64-bit VGPR
+        // address here was kept live across the tile loop and spilled
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(c.out + (size_t)shape * c.npts), (short)0, 0x7ffffff0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, tanhf(s + c.b_last)),
+                                              ro, (uint32_t)pt * 4u, 0, 2 /* nt */);
+    }
+}
+
+// scheduling slot of v VALU instructions (0, 2 or 4; v is a constant once unrolled)
+__device__ __forceinline__ void valu_slot(int v) {
+    if (v == 2) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    else if (v == 4) __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+}
+
+// MFMA pair of point chunk n of one step (both m-chunks of the wave's part)
+template <typename T>
+__device__ __forceinline__ void mfma_pair(f32x16 (&acc)[2][4], const u32x4& a0, const u32x4& a1,
+                                          const u32x4& b, int n) {
+    acc[0][n] = Elem<T>::mfma(a0, b, acc[0][n]);
+    acc[1][n] = Elem<T>::mfma(a1, b, acc[1][n]);
+}
+
+// Four k-steps reading positions p0..p0+3 (ring slots 0..3), epilogue window steps K0..K0+3.
+// Rolling B fragments: chunk n of step j+1 is read as soon as step j's two MFMAs on chunk n are
+// issued (~6 MFMAs, ~190 cycles, before it is needed).  BAR = r: an LDS barrier INSIDE step r,
+// after its first (FV & 1: second) MFMA pair and before its first read of the next position:
+// the waves wait on each other with the step's remaining MFMAs still to issue and the next
+// position's reads still covered by them (a barrier between steps exposed one LDS round trip
+// plus the pipeline drain, ~500-750 cycles per barrier).
+template <typename T, int EK, int K0, int BAR, int FV>
+__device__ __forceinline__ void group4(FCtx<FV>& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
+                                       int p0) {
+    constexpr int BP = (FV & 1) ? 2 : 1;     // MFMA pairs before the in-stream barrier
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        // rolling B fragments: chunk n of step j+1 is read as soon as step j's two MFMAs on
-        // chunk n are issued, ~6 MFMAs (~190 cycles) before it is needed (a read after the
-        // step's last MFMA left ~32 cycles of cover: an LDS round trip exposed per step)
         const u32x4* nb = reinterpret_cast<const u32x4*>(lds_at(c, (p0 + r + 1) * 4096));
-        const u32x4 a0 = c.ring[RO + r][0], a1 = c.ring[RO + r][1];
+        const u32x4 a0 = c.ring[r][0], a1 = c.ring[r][1];
+        const int k = K0 + r;
+        // the step's VALU (epilogue: AGPR reads, cvt, ReLU, LDS address) 2 per MFMA gap, 4 in
+        // the double-unit step 14 (the guide: <= 5 fillers per 32x32x16 gap hide)
+        const int V = (EK == FE_NONE || k == 15) ? 0 : (k == 14 ? 4 : 2);
+        if (r == BAR) {
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            acc[0][n] = Elem<T>::mfma(a0, b[n], acc[0][n]);
-            acc[1][n] = Elem<T>::mfma(a1, b[n], acc[1][n]);
-            b[n] = nb[n * 64];
-        }
-        issue(c, RO + r, r);
-        if (EK != FE_NONE) epi_tile<T, EK>(c, accY, T0 + r);
-        // pin the step's order for the scheduler (left free it sank the B reads and weight
-        // loads below the last MFMA: one step of latency cover instead of FS_D): per point
-        // chunk n, MFMA, [VALU], MFMA, B read, [VALU]; then the 2 weight loads.  E steps
-        // spread their VALU (AGPR reads, cvt, ReLU) 4 per MFMA gap (the guide: <= 5 fillers
-        // per 32x32x16 gap hide).
-        constexpr int V = EK == FE_NONE ? 0 : 4;
+            for (int n = 0; n < BP; ++n) mfma_pair<T>(acc, a0, a1, c.b[n], n);
+            for (int n = 0; n < BP; ++n) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            fs_bar();
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            if (V) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            if (V) __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+            for (int n = 0; n < BP; ++n) c.b[n] = nb[n * 64];
+#pragma unroll
+            for (int n = BP; n < 4; ++n) {
+                mfma_pair<T>(acc, a0, a1, c.b[n], n);
+                c.b[n] = nb[n * 64];
+            }
+            issue(c, r);
+            epi_step<T, EK>(c, accY, k);
+            for (int n = 0; n < BP; ++n) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            for (int n = BP; n < 4; ++n) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                valu_slot(V);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                valu_slot(V);
+            }
+        } else {
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                mfma_pair<T>(acc, a0, a1, c.b[n], n);
+                c.b[n] = nb[n * 64];
+            }
+            issue(c, r);
+            epi_step<T, EK>(c, accY, k);
+            // pin the step's order for the scheduler (left free it sank the B reads and weight
+            // loads below the last MFMA): per point chunk n, MFMA, [VALU], MFMA, B read,
+            // [VALU]; then the 2 weight loads
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                valu_slot(V);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                valu_slot(V);
+            }
         }
         __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         __builtin_amdgcn_sched_barrier(0);
@@ -276,125 +404,141 @@ __device__ __forceinline__ void group4(FCtx<FS_D>& c, f32x16 (&acc)[2][4], const
     next_group(c);
 }
 
-// 8 k-steps from position p0 (ring slots 0..7 mod FS_D); E work (tiles 0..7) when EK != NONE
-template <typename T, int EK, int FS_D>
-__device__ __forceinline__ void steps8(FCtx<FS_D>& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
-                                       u32x4 (&b)[4], int p0) {
-    group4<T, EK, 0, 0, FS_D>(c, acc, accY, b, p0);
-    group4<T, EK, 4, (FS_D == 8 ? 4 : 0), FS_D>(c, acc, accY, b, p0 + 4);
+// 16 k-steps from position p0 carrying the 16 epilogue units of the other set; BAR: the
+// window's closing barrier inside its step 15
+template <typename T, int EK, bool BAR, int FV>
+__device__ __forceinline__ void steps16e(FCtx<FV>& c, f32x16 (&acc)[2][4],
+                                         const f32x16 (&accY)[2][4], int p0) {
+    group4<T, EK, 0, -1, FV>(c, acc, accY, p0);
+    group4<T, EK, 4, -1, FV>(c, acc, accY, p0 + 4);
+    group4<T, EK, 8, -1, FV>(c, acc, accY, p0 + 8);
+    group4<T, EK, 12, BAR ? 3 : -1, FV>(c, acc, accY, p0 + 12);
 }
 
-// One part: the aux step (zero-initialises acc; loads the NEXT part's aux fragments), then nk
-// ring steps reading positions pos0 + j.  E work (the other set, EK) in steps 0-7 (E16 false)
-// or 16-23 (E16 true).  `mid`: a barrier before step 16 (the late positions were written
-// during steps 0-7 by every wave / no wave reads the early positions any more).  `bar0`: the
-// part follows LDS writes of the previous layer still to be published: the barrier comes after
-// its aux step (which reads only the wave's own xyz fragments).
-template <typename T, int EK, bool E16, int FS_D>
-__device__ __forceinline__ void run_part(FCtx<FS_D>& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
-                                         int nk, bool mid, FSrc naux, int pos0, bool bar0) {
+// plain k-steps [j0, j1) from position pos0 as ONE runtime loop of 4-step groups (code size:
+// the kernel must stay well inside the instruction cache)
+template <typename T, int FV>
+__device__ __forceinline__ void steps_plain(FCtx<FV>& c, f32x16 (&acc)[2][4],
+                                            const f32x16 (&accY)[2][4], int pos0, int j0, int j1) {
+#pragma unroll 1
+    for (int j = j0; j < j1; j += 4) group4<T, FE_NONE, 0, -1, FV>(c, acc, accY, pos0 + j);
+}
+
+// One part: the aux step, then nk ring steps reading positions pos0 .. pos0 + nk - 1 = 31
+// (the last one reads position 32, the tile's aux B fragments, for the next part's aux step).
+//   * aux step: zero-initialises acc with [wx,wy,wz,wx,wy,wz,b_hi,b_lo] x xyz (c.b on entry)
+//     and, per point chunk, reads the first position's B fragment behind its MFMA pair -- or,
+//     `bar0`, after a barrier (the part follows serial LDS writes: layers 1 and 4 at skip 253);
+//     then it loads the NEXT part's aux A fragments (naux).
+//   * E work (the other set, EK) in steps 0-15 (E16 false) or 16-31 (E16 true).
+//   * `mid`: the barrier inside step 15 (the late positions written during steps 0-14 by
+//     every wave / no wave reads the early positions any more before E16 writes them);
+//     `endbar` (E work parts): the barrier inside the part's last step, publishing the window's
+//     writes to the next part, whose aux step then reads on without a barrier.
+template <typename T, int EK, bool E16, int FV>
+__device__ __forceinline__ void run_part(FCtx<FV>& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
+                                         int nk, bool mid, bool endbar, FSrc naux, int pos0,
+                                         bool bar0) {
     const f32x16 zero = {};
-    u32x4 b[4];
-    // the aux B fragments (xyz of the tile's points) sit in this wave's LDS copy
-    const u32x4* xb = reinterpret_cast<const u32x4*>(
-        lds_at(c, kFsAct + kFsRed + kFsWl + c.wave * 4096));
+    const u32x4 a0 = c.auxn[0], a1 = c.auxn[1];
+    if (nk == 0) {             // layer 0: the aux step only, c.b stays the xyz fragments
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const u32x4 x = xb[n * 64];
-        acc[0][n] = Elem<T>::mfma(c.auxn[0], x, zero);
-        acc[1][n] = Elem<T>::mfma(c.auxn[1], x, zero);
-    }
-    load_aux(c, naux);
-    if (bar0) fs_bar();
-    stamp(c);
-    if (nk == 0) return;
-    read_b(c, pos0, b);
-    // code size: the E steps are unrolled per kind, the plain steps run as ONE runtime loop of
-    // 4-step groups (the kernel must stay well inside the instruction cache)
-    int j = 0;
-    if (!E16) {
-        steps8<T, EK, FS_D>(c, acc, accY, b, pos0);
-        j = 8;
-    }
-    stamp(c);
-#pragma unroll 1
-    for (; j < nk; j += FS_D) {
-        if (j == 16) {
-            if (E16) break;
-            if (mid) {
-                stamp(c);
-                fs_bar();
-                read_b(c, pos0 + 16, b);
-            }
+        for (int n = 0; n < 4; ++n) {
+            acc[0][n] = Elem<T>::mfma(a0, c.b[n], zero);
+            acc[1][n] = Elem<T>::mfma(a1, c.b[n], zero);
         }
-        group4<T, FE_NONE, 0, 0, FS_D>(c, acc, accY, b, pos0 + j);
-        if (FS_D == 8) group4<T, FE_NONE, 0, 4, FS_D>(c, acc, accY, b, pos0 + j + 4);
-    }
-    if (E16) {               // j == 16 here (E16 parts have nk = 32 and a mid barrier)
+        load_aux(c, naux);
         stamp(c);
+        return;
+    }
+    if (bar0) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            acc[0][n] = Elem<T>::mfma(a0, c.b[n], zero);
+            acc[1][n] = Elem<T>::mfma(a1, c.b[n], zero);
+        }
+        load_aux(c, naux);
         fs_bar();
-        read_b(c, pos0 + 16, b);
-        steps8<T, EK, FS_D>(c, acc, accY, b, pos0 + 16);
-        stamp(c);
-#pragma unroll 1
-        for (j = 24; j < nk; j += FS_D) {
-            group4<T, FE_NONE, 0, 0, FS_D>(c, acc, accY, b, pos0 + j);
-            if (FS_D == 8) group4<T, FE_NONE, 0, 4, FS_D>(c, acc, accY, b, pos0 + j + 4);
+        read_b(c, pos0);
+    } else {
+        const u32x4* p = reinterpret_cast<const u32x4*>(lds_at(c, pos0 * 4096));
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            acc[0][n] = Elem<T>::mfma(a0, c.b[n], zero);
+            acc[1][n] = Elem<T>::mfma(a1, c.b[n], zero);
+            c.b[n] = p[n * 64];
         }
+        load_aux(c, naux);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    stamp(c);
+    if (!E16 && EK != FE_NONE) {        // E work in steps 0-15
+        // the barrier inside step 15: mid (nk 32), or the end barrier of a 16-step part
+        if (mid || (endbar && nk == 16)) steps16e<T, EK, true>(c, acc, accY, pos0);
+        else steps16e<T, EK, false>(c, acc, accY, pos0);
+        if (EK == FE_FIN1) fin_store(c, c.prev_shape, c.prev_local);
+        stamp(c);
+        if (endbar && nk == 32) {       // the end barrier inside step 31
+            steps_plain<T>(c, acc, accY, pos0, 16, 28);
+            group4<T, FE_NONE, 0, 3, FV>(c, acc, accY, pos0 + 28);
+        } else {
+            steps_plain<T>(c, acc, accY, pos0, 16, nk);
+        }
+    } else if (E16) {                   // nk 32, mid
+        steps_plain<T>(c, acc, accY, pos0, 0, 12);
+        group4<T, FE_NONE, 0, 3, FV>(c, acc, accY, pos0 + 12);
+        stamp(c);
+        if (endbar) steps16e<T, EK, true>(c, acc, accY, pos0 + 16);
+        else steps16e<T, EK, false>(c, acc, accY, pos0 + 16);
+    } else {                            // plain part, no barrier (layer 4 part 0 at skip 253)
+        steps_plain<T>(c, acc, accY, pos0, 0, nk < 16 ? nk : 16);
+        stamp(c);
+        steps_plain<T>(c, acc, accY, pos0, 16, nk);
     }
     stamp(c);
 }
 
-// a whole set into LDS positions kbase + 2i + s (serial: layer 0, layer 3 at skip 253)
-template <typename T, int FS_D>
-__device__ __forceinline__ void acc_to_lds(FCtx<FS_D>& c, const f32x16 (&acc)[2][4], int kbase) {
+// a whole set into this wave's early (LATE = false) or late positions 16u + 4w + 2i + s
+// (serial: layer 0, layer 3 at skip 253); the per-wave base and immediates per tile
+template <typename T, bool LATE, int FV>
+__device__ __forceinline__ void acc_to_lds(FCtx<FV>& c, const f32x16 (&acc)[2][4]) {
+    u32x4* p = act_w(c, LATE ? 16 : 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) tile_to_lds<T>(c, acc[i][n], kbase + 2 * i, n);
-}
-
-// final layer of part 1 of layer 7 (after its MFMAs): w read once per m-chunk, shared by the 4
-// point chunks; four independent fma chains per tile, summed in fixed order
-template <int FS_D>
-__device__ __forceinline__ void fin_serial(FCtx<FS_D>& c, const f32x16 (&acc)[2][4]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const f32x4* wp = reinterpret_cast<const f32x4*>(
-            c.smem + kFsAct + kFsRed + ((((c.wave * 2 + 1) * 2 + i) * 2 + c.h) * 16) * 4);
-        f32x4 w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = wp[q];
-#pragma unroll
         for (int n = 0; n < 4; ++n) {
-            float s[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                s[q] = fmaxf(acc[i][n][4 * q], 0.f) * w[q][0];
-#pragma unroll
-                for (int e = 1; e < 4; ++e) s[q] = fmaf(fmaxf(acc[i][n][4 * q + e], 0.f), w[q][e], s[q]);
-            }
-            c.part[n] += (s[0] + s[1]) + (s[2] + s[3]);
+            u32x4 f0, f1;
+            acc_to_frags<T>(acc[i][n], f0, f1);
+            p[(2 * i * 4 + n) * 64] = f0;
+            p[((2 * i + 1) * 4 + n) * 64] = f1;
         }
-    }
 }
 
-template <typename T, int S, bool POINTS, int FS_D>
+template <typename T, int S, bool POINTS, int FV>
 __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[kFsLds];
-    FCtx<FS_D> c;
+    FCtx<FV> c;
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c.h = c.lane >> 5;
     c.voff = (uint32_t)c.lane * 16u;
     c.smem = smem;
-    c.st = reinterpret_cast<unsigned long long*>(smem + kFsAct + kFsRed + kFsWl + kFsXyz);
+    c.out = a.out;
+    c.npts = a.npts;
+    c.b_last = a.b_last;
+    c.prev_shape = 0;
+    c.prev_local = -1;
+    c.st = reinterpret_cast<unsigned long long*>(smem + kFsAct + kFsRed + kFsWl);
     c.st_i = 0;
     c.st_on = false;
     float* wl = reinterpret_cast<float*>(smem + kFsAct + kFsRed);
-    float* red = reinterpret_cast<float*>(smem + kFsAct);
-    u32x4* xyz_l = reinterpret_cast<u32x4*>(smem + kFsAct + kFsRed + kFsWl + c.wave * 4096 +
-                                            c.voff);
+
     for (int i = threadIdx.x; i < 512; i += 256) wl[i] = a.w_last[i];
     __syncthreads();
     if ((int)blockIdx.x >= a.n_tiles) return;
@@ -415,13 +559,16 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
     auto shp = [&](int slot) -> FSrc { return FSrc{true, c.aux_w + (uint32_t)slot * kFsStep}; };
     c.aux_w = shape_aux(blockIdx.x);
 #pragma unroll
-    for (int r = 0; r < FS_D; ++r) {
-        issue(c, r, r & 3);
-        if ((r & 3) == 3) next_group(c);
-    }
-    load_aux(c, shp(0));                                // layer 0 part 0 of the first tile
+    for (int r = 0; r < kFsD; ++r) issue(c, r);
+    next_group(c);
 
     f32x16 accA[2][4], accB[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) accB[i][n] = f32x16{};    // the first tile's FE_FIN1 input
+#pragma unroll
+    for (int n = 0; n < 4; ++n) c.part[n] = 0.f;
 #pragma unroll 1
     for (int tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         const int shape = tile / a.tiles_per_shape;
@@ -433,11 +580,18 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
         c.st_on = FS_STAMP && c.wave == 0 && tile == (int)blockIdx.x + (int)gridDim.x;
         c.st_i = 0;
         stamp(c);
-        // ---- aux B fragments [x_hi,y_hi,z_hi,x_lo,y_lo,z_lo,1,1] of point 32n + (lane&31),
-        // into this wave's LDS copy
+        load_aux(c, shp(0));            // L0p0's aux fragments (latency under the xyz setup)
+        // ---- aux B fragments [x_hi,y_hi,z_hi,x_lo,y_lo,z_lo,1,1] of point 32n + (lane&31) at
+        // position 32.  Every wave writes the same bytes (no barrier: a wave reads back its own
+        // writes, the others only ever replace them with equal values; every read of the
+        // previous tile's position 32 came before its final barrier)
+        // lane values formed here from an opaque voff (kept live across the tile loop, they
+        // were spilled and reloaded behind the whole weight ring)
+        const uint32_t lv = opaque(c.voff);
+        const bool hi = lv >= 512u;                       // lane >= 32
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            int pt = local * kTilePoints + 32 * n + (c.lane & 31);
+            int pt = local * kTilePoints + 32 * n + (int)((lv >> 4) & 31u);
             if (pt >= a.npts) pt = a.npts - 1;
             float x, y, z;
             if (POINTS) {
@@ -446,82 +600,89 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
                 y = qq[1];
                 z = qq[2];
             } else {
-                grid_point(pt, a.N, a.k0, a.vs, a.origin, x, y, z);
+                // N through an opaque SGPR: the divisions' reciprocals are formed per tile
+                // instead of hoisted out of the loop (and spilled)
+                grid_point(pt, opaque_s(a.N), a.k0, a.vs, a.origin, x, y, z);
             }
             const float xh = Elem<T>::round(x), yh = Elem<T>::round(y), zh = Elem<T>::round(z);
             u32x4 f;
-            f[0] = c.h ? 0u : Elem<T>::pack(xh, yh);
-            f[1] = c.h ? 0u : Elem<T>::pack(zh, x - xh);
-            f[2] = c.h ? 0u : Elem<T>::pack(y - yh, z - zh);
-            f[3] = c.h ? 0u : Elem<T>::pack(1.f, 1.f);
-            xyz_l[n * 64] = f;
+            f[0] = hi ? 0u : Elem<T>::pack(xh, yh);
+            f[1] = hi ? 0u : Elem<T>::pack(zh, x - xh);
+            f[2] = hi ? 0u : Elem<T>::pack(y - yh, z - zh);
+            f[3] = hi ? 0u : Elem<T>::pack(1.f, 1.f);
+            reinterpret_cast<u32x4*>(lds_at(c, 32u * 4096u))[n * 64] = f;
         }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) c.part[n] = 0.f;
+        read_b(c, 32);
 
-        // ---- layer 0 (aux only): part 0 -> A -> early positions now (the previous tile's
-        // readers all passed its final barrier), part 1 -> B -> late positions during L1p0
-        run_part<T, FE_NONE, false, FS_D>(c, accA, accB, 0, false, shp(1), 0, false);
-        run_part<T, FE_NONE, false, FS_D>(c, accB, accA, 0, false, bias(2), 0, false);
-        acc_to_lds<T, FS_D>(c, accA, 4 * c.wave);
+        // ---- layer 0 (aux only), both parts through set A into LDS serially (set B still
+        // holds the previous tile's layer 7 part 1, folded into the output during L1p0); the
+        // previous tile's readers all passed the end barrier of its layer 7
+        run_part<T, FE_NONE, false, FV>(c, accA, accB, 0, false, false, shp(1), 0, false);
+        acc_to_lds<T, false, FV>(c, accA);
+        stamp(c);
+        run_part<T, FE_NONE, false, FV>(c, accA, accB, 0, false, false, bias(2), 0, false);
+        acc_to_lds<T, true, FV>(c, accA);
         stamp(c);
 
-        // ---- two-part layers 1, 2 (and 3 when 512 wide)
+        // ---- two-part layers 1, 2 (and 3 when 512 wide).  L1p0 folds the previous tile's
+        // layer 7 part 1 into its outputs (FE_FIN1); p1 of layer l publishes with its end barrier
         constexpr int L2P = S == 256 ? 3 : 4;
         int pi = 2;
+        run_part<T, FE_FIN1, false, FV>(c, accA, accB, 32, true, false, bias(pi + 1), 0, true);
+        run_part<T, FE_EARLY, true, FV>(c, accB, accA, 32, true, true, bias(pi + 2), 0, false);
+        pi += 2;
 #pragma unroll 1
-        for (int l = 1; l < L2P; ++l, pi += 2) {
+        for (int l = 2; l < L2P; ++l, pi += 2) {
             // the part after layer 3 (512 wide) is layer 4's: per-shape aux
             const FSrc nx = (S == 512 && l == 3) ? shp(2) : bias(pi + 2);
-            run_part<T, FE_LATE, false, FS_D>(c, accA, accB, 32, true, bias(pi + 1), 0, true);
-            run_part<T, FE_EARLY, true, FS_D>(c, accB, accA, 32, true, nx, 0, false);
+            run_part<T, FE_LATE, false, FV>(c, accA, accB, 32, true, false, bias(pi + 1), 0, false);
+            run_part<T, FE_EARLY, true, FV>(c, accB, accA, 32, true, true, nx, 0, false);
         }
         if (S == 256) {
             // layer 3: one part of rows 64w..64w+63 -> positions 16 + 4w + 2i + s (serial,
             // once every wave is done reading layer 3's inputs)
-            run_part<T, FE_LATE, false, FS_D>(c, accA, accB, 32, true, shp(2), 0, true);
+            run_part<T, FE_LATE, false, FV>(c, accA, accB, 32, true, false, shp(2), 0, false);
             fs_bar();
-            acc_to_lds<T, FS_D>(c, accA, 16 + 4 * c.wave);
+            acc_to_lds<T, true, FV>(c, accA);
             stamp(c);
             // layer 4 (K = 256, positions 16..31); part 0 -> early positions during part 1
-            run_part<T, FE_NONE, false, FS_D>(c, accA, accB, 16, false, shp(3), 16, true);
-            run_part<T, FE_EARLY, false, FS_D>(c, accB, accA, 16, false, bias(pi + 3), 16, false);
+            run_part<T, FE_NONE, false, FV>(c, accA, accB, 16, false, false, shp(3), 16, true);
+            run_part<T, FE_EARLY, false, FV>(c, accB, accA, 16, false, true, bias(pi + 3), 16,
+                                             false);
             pi += 3;
         } else {
-            run_part<T, FE_LATE, false, FS_D>(c, accA, accB, 32, true, shp(3), 0, true);
-            run_part<T, FE_EARLY, true, FS_D>(c, accB, accA, 32, true, bias(pi + 2), 0, false);
+            run_part<T, FE_LATE, false, FV>(c, accA, accB, 32, true, false, shp(3), 0, false);
+            run_part<T, FE_EARLY, true, FV>(c, accB, accA, 32, true, true, bias(pi + 2), 0, false);
             pi += 2;
         }
         // ---- layers 5, 6
 #pragma unroll 1
         for (int l = 5; l < 7; ++l, pi += 2) {
-            run_part<T, FE_LATE, false, FS_D>(c, accA, accB, 32, true, bias(pi + 1), 0, true);
-            run_part<T, FE_EARLY, true, FS_D>(c, accB, accA, 32, true, bias(pi + 2), 0, false);
+            run_part<T, FE_LATE, false, FV>(c, accA, accB, 32, true, false, bias(pi + 1), 0, false);
+            run_part<T, FE_EARLY, true, FV>(c, accB, accA, 32, true, true, bias(pi + 2), 0, false);
         }
-        // ---- layer 7: part 0 folds into the dot product during part 1; part 1 after it
-        run_part<T, FE_LATE, false, FS_D>(c, accA, accB, 32, true, bias(pi + 1), 0, true);
-        run_part<T, FE_FIN, false, FS_D>(c, accB, accA, 32, false, FSrc{true, c.aux_next}, 0,
-                                         false);
-        fin_serial(c, accB);
-        // ---- final layer across waves: lanes l and l^32 hold the same point
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const float tot = c.part[n] + __shfl_xor(c.part[n], 32);
-            if (c.h == 0) red[(c.wave * 4 + n) * 32 + c.lane] = tot;
-        }
-        stamp(c);
-        fs_bar();
-        if (c.h == 0) {
-            float s = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) s += red[(w * 4 + c.wave) * 32 + c.lane];
-            const int pt = local * kTilePoints + 32 * c.wave + c.lane;
-            if (pt < a.npts)
-                __builtin_nontemporal_store(tanhf(s + a.b_last), a.out + (size_t)shape * a.npts + pt);
-        }
-        stamp(c);
+        // ---- layer 7: part 0 folds into the dot product during part 1, part 1 during the
+        // next tile's L1p0 (its end barrier lets the next tile overwrite every position)
+        run_part<T, FE_LATE, false, FV>(c, accA, accB, 32, true, false, bias(pi + 1), 0, false);
+        // (no prefetch of the next tile's first aux fragments here: live across the whole
+        // part they were spilled, each spill waiting for the whole ring)
+        run_part<T, FE_FIN0, false, FV>(c, accB, accA, 32, false, true, FSrc{true, 0, true}, 0,
+                                        false);
+        c.prev_shape = shape;
+        c.prev_local = local;
         c.aux_w = c.aux_next;
     }
+    // the last tile's layer 7 part 1: the FE_FIN1 units in their window order (a point's
+    // value must not depend on whether its tile was its workgroup's last)
+#pragma unroll
+    for (int u = 0; u < 16; ++u) epi_unit<T, FE_FIN1>(c, accB, u);
+    {
+        float* rw = red_w(c);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) rw[n * 64] = c.part[n];
+    }
+    fs_bar();
+    fin_store(c, c.prev_shape, c.prev_local);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (FS_STAMP && c.wave == 0) {
         __builtin_amdgcn_s_waitcnt(0);
@@ -541,10 +702,9 @@ void launch_fs_d(const FArgs& a, bool points, hipStream_t s, int grid) {
 template <typename T, int S>
 void launch_fs(const FArgs& a, bool points, hipStream_t s, int grid) {
 #ifdef LDM_DEV_KNOBS
-    if (dev_knob("LDM_FS_D", kFsDefaultD) == 8) return launch_fs_d<T, S, 8>(a, points, s, grid);
-    if (dev_knob("LDM_FS_D", kFsDefaultD) == 4) return launch_fs_d<T, S, 4>(a, points, s, grid);
+    if (dev_knob("LDM_FS_BP", 0) == 1) return launch_fs_d<T, S, 1>(a, points, s, grid);
 #endif
-    launch_fs_d<T, S, kFsDefaultD>(a, points, s, grid);
+    launch_fs_d<T, S, kFsDefaultV>(a, points, s, grid);
 }
 
 }  // namespace

@@ -14,9 +14,10 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 # variants: "p<sched>" = pass8 layout with LDM_DECODER_SCHED=<sched> (needs the `make DEV=1`
-# library for sched != 4), "q" = quarter layout, "s" = split layout
+# library for sched != 4), "q" = quarter layout, "s" = split layout, "sb" = split with its
+# in-stream barriers after the second MFMA pair (LDM_FS_BP=1, dev build)
 VARIANTS = os.environ.get("AB_VARIANTS", "s,q").split(",")
-LAYOUT = {"q": "quarter", "s": "split", "s4": "split", "s8": "split"}
+LAYOUT = {"q": "quarter", "s": "split", "sb": "split"}
 FLOPS = 3146752
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)
@@ -31,8 +32,8 @@ for dtype in os.environ.get("AB_DTYPES", "bf16").split(","):
         for v in VARIANTS:
             if v.startswith("p"):
                 os.environ["LDM_DECODER_SCHED"] = v[1:]
-            if v in ("s4", "s8"):                  # split ring depth (dev build)
-                os.environ["LDM_FS_D"] = v[1:]
+            if v in ("s", "sb"):
+                os.environ["LDM_FS_BP"] = "1" if v == "sb" else "0"
             e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
             e0.record()
             ops.decoder_grid_fwd(pks[v]["desc"], beta, N, 0, N, out=out)

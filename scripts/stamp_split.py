@@ -31,29 +31,28 @@ labels = []
 
 
 def part(name, kind):
-    """stamps of one run_part (csrc/decoder_fs.hip): E0 = epilogue in steps 0-7, E16 = in steps
-    16-23 (after the part's own barrier), mid = barrier before step 16."""
+    """stamps of one run_part (csrc/decoder_fs.hip): after its aux step (plus the first read,
+    after a barrier for bar0 parts), after steps 0-15, at its end.  BAR = the in-stream barrier
+    inside step 15, END = the one inside the part's last step."""
     if kind == "aux":
         return [f"{name} aux"]
-    if kind == "E0mid":
-        return [f"{name} aux", f"{name} E-steps 0-7", f"{name} steps 8-15",
-                f"{name} MID BAR + steps 16-31"]
-    if kind == "E0":
-        return [f"{name} aux", f"{name} E-steps 0-7", f"{name} steps 8-end"]
-    if kind == "E16":
-        return [f"{name} aux", f"{name} (none)", f"{name} steps 0-15",
-                f"{name} MID BAR + E-steps 16-23", f"{name} steps 24-31"]
-    raise ValueError(kind)
+    segs = {"E0mid": ("E 0-15 + BAR", "steps 16-31"),
+            "E16": ("steps 0-15 + BAR", "E 16-31 + END"),
+            "plain16": ("steps 0-15", "(none)"),
+            "E0end16": ("E 0-15 + END", "(none)"),
+            "FIN1": ("E(prev L7p1) 0-15 + BAR + store", "steps 16-31"),
+            "FIN0": ("E 0-15", "steps 16-31 + END")}[kind]
+    return [f"{name} aux"] + [f"{name} {x}" for x in segs]
 
 
-labels += part("L0p0", "aux") + part("L0p1", "aux") + ["L0 serial write"]
-for l in (1, 2):
-    labels += part(f"L{l}p0", "E0mid") + part(f"L{l}p1", "E16")
+labels += part("L0p0", "aux") + ["L0 serial A"] + part("L0p1", "aux") + ["L0 serial B"]
+labels += part("L1p0", "FIN1") + part("L1p1", "E16")
+labels += part("L2p0", "E0mid") + part("L2p1", "E16")
 labels += part("L3p0", "E0mid") + ["L3 bar + serial write"]
-labels += part("L4p0", "E0") + part("L4p1", "E0")
+labels += part("L4p0", "plain16") + part("L4p1", "E0end16")
 for l in (5, 6):
     labels += part(f"L{l}p0", "E0mid") + part(f"L{l}p1", "E16")
-labels += part("L7p0", "E0mid") + part("L7p1", "E0") + ["FIN serial", "red bar+store"]
+labels += part("L7p0", "E0mid") + part("L7p1", "FIN0")
 n = len(labels) + 1
 t = st[:, :n]
 d = np.diff(t, axis=1)
