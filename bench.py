@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--ad-steps", type=int, default=5)
     ap.add_argument("--no-config3", action="store_true",
                     help="skip config 3 (sample(8) -> decode 128^3, timed end to end; its "
-                         "decode is a dec_q_kernel launch of another size in a profile)")
+                         "decode is a dec_fs_kernel launch of another size in a profile)")
     ap.add_argument("--shapes-per-group", type=int, default=0,
                     help="multi-GPU decode: shapes per gather group (0: ceil(B/8))")
     return ap.parse_args()
@@ -531,7 +531,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
                          "frac": ach / peak, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "dec_q_kernel (+qaux_pack, <0.1%)",
+                         "kernel": "dec_fs_kernel (+fs_aux_pack, <0.1%)",
                          "flops_per_query": FLOPS_PER_QUERY,
                          "queries_per_launch": qpl, "avg_launch_ms": kms,
                          "launches_per_step": len(slab.events) // max(1, args.steps)},

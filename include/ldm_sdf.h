@@ -42,7 +42,8 @@ extern "C" {
 /* workspace ops for ldm_workspace_bytes() */
 #define LDM_OP_DECODER_GRID 1
 #define LDM_OP_DECODER_POINTS 2
-/* workspace for the quarter layout is 64 KiB per shape; query with ldm_workspace_bytes_layout */
+/* ldm_workspace_bytes() returns the quarter layout's 64 KiB per shape, enough for every layout
+   (split: 32 KiB, pass8: 32 KiB); ldm_workspace_bytes_layout() gives the layout's own size */
 
 typedef void* ldm_stream_t; /* hipStream_t; NULL = the null stream */
 
@@ -65,13 +66,14 @@ typedef struct ldm_decoder {
     const float* wxyz;    /* fp32 [2][H][3]  xyz columns of layer 0 and layer 4 */
     const float* w_last;  /* fp32 [H] final 512->1 weights (bf16/f16: MFMA-row permuted) */
     float b_last;         /* final bias */
-    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_PASS8, _QUARTER or _SPLIT */
+    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_PASS8, _QUARTER, _SPLIT, _SPLIT16 */
 } ldm_decoder_t;
 
 /* Stage-blob layouts of the MFMA decoder. */
 #define LDM_LAYOUT_PASS8 0   /* 8 m-chunks x 1 k-step per stage, 2 passes per layer */
 #define LDM_LAYOUT_QUARTER 1 /* 4 m-chunks x 2 k-steps per stage, 4 quarters per layer */
 #define LDM_LAYOUT_SPLIT 2   /* features split over the 4 waves, per-wave weight streams */
+#define LDM_LAYOUT_SPLIT16 3 /* the split work division on 16x16x32 MFMAs, fp32 biases */
 
 /* DDPM tables, fp32 device arrays of length T. */
 typedef struct ldm_sched {

@@ -627,12 +627,13 @@ int check_decoder(const ldm_decoder_t* w) {
                 "decoder weights must be 16-byte aligned");
     if (w->dtype != LDM_F32) {
         LDM_REQUIRE(w->layout == LDM_LAYOUT_PASS8 || w->layout == LDM_LAYOUT_QUARTER ||
-                        w->layout == LDM_LAYOUT_SPLIT,
+                        w->layout == LDM_LAYOUT_SPLIT || w->layout == LDM_LAYOUT_SPLIT16,
                     LDM_EINVAL, "bad decoder layout %d", w->layout);
         const int S = w->skip_width == 253 ? 256 : 512;
         const int want = w->layout == LDM_LAYOUT_PASS8     ? dec_n_stages(S)
                          : w->layout == LDM_LAYOUT_QUARTER ? decoder_q_n_stages(w->skip_width)
-                                                           : decoder_fs_n_stages(w->skip_width);
+                         : w->layout == LDM_LAYOUT_SPLIT   ? decoder_fs_n_stages(w->skip_width)
+                                                           : decoder_fs16_n_stages(w->skip_width);
         LDM_REQUIRE(w->n_stages == want, LDM_EINVAL, "n_stages %d != %d for skip width %d",
                     w->n_stages, want, w->skip_width);
     }
@@ -699,6 +700,9 @@ int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int
                            points ? 1 : 0);
         return launch_status("ldm_decoder_fwd(f32)");
     }
+    if (w->layout == LDM_LAYOUT_SPLIT16)
+        return decoder_fs16_fwd(w, beta, xyz, B, npts, N, k0, vs, origin, out, ws, ws_bytes, s,
+                                num_cus());
     if (w->layout == LDM_LAYOUT_SPLIT)
         return decoder_fs_fwd(w, beta, xyz, B, npts, N, k0, vs, origin, out, ws, ws_bytes, s,
                               num_cus());
@@ -750,6 +754,7 @@ size_t decoder_workspace_bytes(int B, int dtype, int layout) {
     if (dtype == LDM_F32) return 0;
     return layout == LDM_LAYOUT_PASS8    ? aux_bytes(B)
            : layout == LDM_LAYOUT_SPLIT ? decoder_fs_aux_bytes(B)
+           : layout == LDM_LAYOUT_SPLIT16 ? decoder_fs16_aux_bytes(B)
                                         : decoder_q_aux_bytes(B);
 }
 

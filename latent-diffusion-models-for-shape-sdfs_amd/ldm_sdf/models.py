@@ -80,7 +80,8 @@ class SDFDecoder:
         return (self.hidden == 512 and self.n_hidden == 8 and self.skip == 4
                 and self.skip_width in (253, 512))
 
-    DEFAULT_LAYOUT = "quarter"
+    # the feature-split kernel (csrc/decoder_fs.hip); "quarter" / "pass8" stay selectable
+    DEFAULT_LAYOUT = "split"
 
     def invalidate(self) -> None:
         """Call after the weights changed (auto-decoder training): drops the packed copies."""

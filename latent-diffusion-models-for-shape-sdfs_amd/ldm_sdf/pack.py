@@ -70,7 +70,10 @@ def stage_plan(skip_width: int) -> List[StageRef]:
     return plan
 
 
-def n_stages(skip_width: int, layout: str = "pass8") -> int:
+def n_stages(skip_width: int, layout: str = "split") -> int:
+    """``ldm_decoder_t.n_stages`` of a 16-bit blob in ``layout`` (split: k-steps per wave)."""
+    if layout == "split":
+        return split_stream_steps(skip_width)
     return len(stage_plan_quarter(skip_width) if layout == "quarter" else stage_plan(skip_width))
 
 
@@ -335,7 +338,7 @@ def pack_f32_blob(pieces: Dict[str, torch.Tensor]) -> torch.Tensor:
 
 
 def pack_decoder(weights, biases, latent_dim: int, dtype: str,
-                 layout: str = "quarter") -> Dict[str, object]:
+                 layout: str = "split") -> Dict[str, object]:
     """All host-side arrays of an ``ldm_decoder_t`` for ``dtype`` in {fp32, bf16, fp16}; the
     16-bit weights in ``layout`` ("split": csrc/decoder_fs.hip, "quarter": decoder_q.hip,
     "pass8": decoder.hip)."""
