@@ -405,17 +405,26 @@ def config5(args, rank, world, dev, group, gen):
     sch = ldm_sdf.DDPMSchedule()
     lo, hi = ldm_sdf.dist.batch_shard(nb, rank, world)
     nl = max(1, hi - lo)
-    sampler = ldm_sdf.Sampler(unet, sch, nl, dtype="bf16", device=dev)
     xT = torch.randn(nl, 1024, device=dev, generator=gen)
     noise = torch.randn(1000, nl, 1024, device=dev, generator=gen)
-    sampler.run(xT, noise)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    reps = 2
-    for _ in range(reps):
-        lat = sampler.run(xT, noise)
-    torch.cuda.synchronize()
-    sps = 1000 * reps / (time.perf_counter() - t0)
+
+    def timed_sampler(persistent):
+        smp = ldm_sdf.Sampler(unet, sch, nl, dtype="bf16", device=dev, persistent=persistent)
+        smp.run(xT, noise)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps, status = 3, []
+        for _ in range(reps):
+            lat = smp.run(xT, noise, check=False).clone()
+            if smp.loop is not None:
+                status.append(smp.loop.status())      # outside the kernel, read per rep
+        torch.cuda.synchronize()
+        return 1000 * reps / (time.perf_counter() - t0), lat, smp, status
+
+    # default Sampler path: the one-launch persistent loop when the batch has it (ldm_unet_loop)
+    sps, lat, sampler, loop_status = timed_sampler(None)
+    sps_graph, lat_graph, _, _ = timed_sampler(False)
+    loop_ok = all(v == 0 for v in loop_status)
     latents = ldm_sdf.dist.all_gather_rows(lat[:hi - lo].clone(), nb, group=group) \
         if world > 1 else lat[:nb].clone()
     dec = ldm_sdf.SDFDecoder(1024, seed=1235)            # widen-skip (L + 3 >= H)
@@ -441,8 +450,15 @@ def config5(args, rank, world, dev, group, gen):
                                "unit": "TFLOP/s", "frac": ach / PEAK_TFLOPS["fp16"],
                                "flops_per_query": FLOPS_PER_QUERY_WIDEN,
                                "queries_per_launch": qpl, "avg_launch_ms": kms},
-           "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
-           "unet_graph": "hipGraph of 1000 steps x 18 ldm_conv1d launches",
+           "unet_sample_steps_per_s": sps if loop_ok else None, "unet_batch_per_rank": nl,
+           "unet_path": ("one persistent launch for all 1000 steps (ldm_unet_loop: one replica "
+                         "of the 18-conv step per XCD, XCD-local barriers)"
+                         if sampler.loop is not None else
+                         "hipGraph of 1000 steps x 18 ldm_conv1d launches"),
+           "unet_loop_status_per_rep": loop_status,
+           "unet_graph_path": {"steps_per_s": sps_graph,
+                               "path": "hipGraph of 1000 steps x 18 ldm_conv1d launches",
+                               "bit_identical": bool(torch.equal(lat, lat_graph))},
            "unet_conv_weight_bytes_per_step": wbytes}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)

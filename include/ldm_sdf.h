@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define LDM_ABI_VERSION 3
+#define LDM_ABI_VERSION 4
 
 /* dtypes */
 #define LDM_F32 0
@@ -472,6 +472,38 @@ typedef struct ldm_conv1d_args {
     const float* c1; const float* c2; const float* sigma; int32_t t;   /* A4 device tables */
 } ldm_conv1d_args_t;
 int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s);
+
+/* ---- C17 sampling loop: the whole T-step UNet reverse loop as ONE launch -- */
+/* A "program" is the n_phase ldm_conv1d calls of one reverse step (the UNet: 18), as
+ * ldm_conv1d would take them, plus which fields follow the step: with x2 [2][B][D] and
+ * cur = step & 1, t = t_hi - step,
+ *   LDM_UNET_PATCH_X      seg[0].X = x2[cur]                                (the input conv)
+ *   LDM_UNET_PATCH_STEP   Y = x2[cur ^ 1], xlat = x2[cur], z = noise[t], t  (the DDPM conv)
+ *   LDM_UNET_PATCH_CBIAS  cbias = cbias + t * cb_tstride   (a [T][Cout] table's base: E_i[t])
+ * ldm_unet_loop_prepare checks the program (every conv must be an ldm_conv1d-valid call with
+ * batch-uniform cbias, w_dtype equal across phases, LDS plan at 64-position tiles <= 160 KiB)
+ * and uploads it into ws (synchronises the stream).  ldm_unet_loop then runs `steps` reverse
+ * steps from t_hi in one launch: one replica of the program per XCD (shapes b = xcd mod 8),
+ * an XCD-local barrier between dependent convs; the convs' arithmetic is ldm_conv1d's, so the
+ * result is bit-identical to n_phase * steps ldm_conv1d calls.  Result in x2[steps & 1].
+ * LDM_ENOSYS when the device has no 8 x 32-CU replica geometry (not an MI355X) or B > 16.
+ * ldm_unet_loop_status: 0 completed, 1 a barrier timed out (partial latents), 2 workgroups
+ * were not placed 32 per XCD (nothing computed); synchronises the stream. */
+#define LDM_UNET_PATCH_X 1
+#define LDM_UNET_PATCH_STEP 2
+#define LDM_UNET_PATCH_CBIAS 4
+#define LDM_UNET_MAX_PHASES 32
+typedef struct ldm_unet_phase {
+    ldm_conv1d_args_t conv;
+    int32_t patch, reserved;
+    int64_t cb_tstride;
+} ldm_unet_phase_t;
+size_t ldm_unet_loop_ws_bytes(int n_phase);
+int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, void* ws, size_t ws_bytes,
+                          ldm_stream_t s);
+int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* noise, int B, int D,
+                  int t_hi, int steps, void* ws, size_t ws_bytes, ldm_stream_t s);
+int ldm_unet_loop_status(const void* ws, unsigned* status_host, ldm_stream_t s);
 
 /* ---- C18 marching cubes on a decoded volume ---------------------------- */
 /* vol: fp32 [N][N][N] (z slowest, as decode writes it); a corner is inside when v < level.

@@ -20,18 +20,20 @@
 // sees LDM_ETIMEOUT-style failure through the status word instead of a hung GPU.
 #include "ldm_internal.h"
 #include "ddpm_common.h"
+#include "loop_sync.h"
 
 #include <stdlib.h>
 
 #include <atomic>
 #include <type_traits>
 
-#ifndef LDM_LOOP_SLEEP
-#define LDM_LOOP_SLEEP 1     // s_sleep units (64 clocks) between polls of the XCD barrier
-#endif
-
 namespace ldm {
 namespace {
+using lsync::kSyncBytes;
+using lsync::spin_until;
+using lsync::replica_sync;
+using lsync::replica_census;
+using namespace lsync;   // ReplicaLine
 
 constexpr unsigned kSpinLimit = 1u << 22;   // x s_sleep(2) ~ 0.3 s per barrier, worst case
 // The limit travels in LoopArgs::spin_limit (default kSpinLimit).  ldm_sample_loop_config()
@@ -210,26 +212,8 @@ __device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned* status, unsig
 // add, sc1 loads after the last poll).
 enum SyncLine { L_TOP = 0, L_STATUS = 1, L_START = 2, L_CNT = 3, L_ARR = 11, L_GEN = 19,
                 L_COUNT = 27 };
-constexpr size_t kSyncBytes = 4096;
 static_assert(L_COUNT * 128 <= (int)kSyncBytes, "sync words overflow");
 
-__device__ __forceinline__ bool spin_until(const unsigned* w, unsigned target, unsigned* status,
-                                           unsigned limit) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        if ((spins & 63) == 63 &&
-            __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-            return false;
-        if (++spins > limit) {
-            __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
-        }
-#if LDM_LOOP_SLEEP > 0
-        __builtin_amdgcn_s_sleep(LDM_LOOP_SLEEP);
-#endif
-    }
-    return true;
-}
 
 struct XcdState { unsigned xcc, n_local, n_active; };
 
@@ -394,8 +378,6 @@ __global__ __launch_bounds__(256) void sample_loop_kernel(LoopArgs a) {
 // Placement: workgroups learn their XCD from HW_REG_XCC_ID; if an XCD holds other than G/8 of
 // them the launch reports status 2 and returns before any compute (the host then uses the
 // chip-wide loop), so correctness never rests on the dispatch order.
-enum ReplicaLine { R_START = 0, R_STATUS = 1, R_CNT = 2, R_ARR = 10, R_GEN = 18, R_COUNT = 26 };
-static_assert(R_COUNT * 128 <= (int)kSyncBytes, "replica sync words overflow");
 
 template <int NR, int NJ>
 __device__ __forceinline__ void load_rows_bf16(u32x4 (&w)[NR][NJ], const void* W, int row0,
@@ -480,28 +462,6 @@ __device__ __forceinline__ float reduce_scatter(float (&acc)[NV], int lane) {
     return acc[0];
 }
 
-// XCD-local barrier of the nloc workgroups of replica xcc (every storing wave drained its sc1
-// stores; one lane adds; the last arriver of the phase publishes the generation word).
-__device__ __forceinline__ bool replica_sync(unsigned* sync, unsigned xcc, unsigned nloc,
-                                            unsigned phase, int* ok, unsigned limit) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned* status = sync + 32 * R_STATUS;
-        unsigned* gen = sync + 32 * (R_GEN + xcc);
-        const unsigned t = __hip_atomic_fetch_add(sync + 32 * (R_ARR + xcc), 1u,
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool good = true;
-        if (t + 1 == phase * nloc)
-            __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            good = spin_until(gen, phase, status, limit);
-        *ok = good;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __syncthreads();
-    return *ok != 0;
-}
 
 // Data-tagged granule hand-off (MI355X guide: handoff-1to1 / allgather rows, "keep 8-byte
 // granules, flat sweep").  A producer stores {value, tag} as ONE 8-byte agent-scope store
@@ -586,22 +546,10 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     // ---- census: XCD id, local rank, equal split check -----------------------------------
     __shared__ unsigned s_xcc, s_rank, s_nloc;
     if (threadIdx.x == 0) {
-        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
-        const unsigned rank = __hip_atomic_fetch_add(sync + 32 * (R_CNT + xcc), 1u,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(sync + 32 * R_START, 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        bool good = spin_until(sync + 32 * R_START, G, sync + 32 * R_STATUS, a.spin_limit);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        bool even = true;
-        for (unsigned x = 0; x < 8; ++x)
-            even = even && __hip_atomic_load(sync + 32 * (R_CNT + x), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) == G / 8;
-        if (good && !even)          // placement other than G/8 per XCD: leave it to the host
-            __hip_atomic_store(sync + 32 * R_STATUS, 2u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        unsigned xcc, rank;
+        const bool good = replica_census(sync, G, a.spin_limit, &xcc, &rank);
         s_xcc = xcc; s_rank = rank; s_nloc = G / 8;
-        *ok = good && even;
+        *ok = good;
     }
     __syncthreads();
     if (!*ok) return;

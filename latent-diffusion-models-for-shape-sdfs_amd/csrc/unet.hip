@@ -28,6 +28,19 @@
 //     arrive already permuted from the host packing (ldm_sdf/ops.py pack_conv_weight).
 #include "ldm_internal.h"
 #include "ddpm_common.h"
+#include "loop_sync.h"
+
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+// Diagnostic build only (-DUNET_STAMP=1, scripts/stamp_unet.py): thread 0 of the workgroup
+// running tile 0 of XCD 0 stamps s_memrealtime (100 MHz) at the points of every phase of the
+// SECOND step into the debug tail of the workspace, which nothing else reads.
+#ifndef UNET_STAMP
+#define UNET_STAMP 0
+#endif
 
 namespace ldm {
 namespace {
@@ -52,63 +65,176 @@ struct ConvPlan {
     int lds_floats;   // including 4 scratch floats at the end (stores of out-of-range slots)
 };
 
+// The device code reads a call's arguments and plan through the CONSTANT address space (the
+// kernarg segment for ldm_conv1d, the uploaded program for the loop), so every field is a
+// scalar load into SGPRs; through a generic pointer each field was a vector load with its own
+// memory wait (the loop's first version: 15.7 us per conv phase).
+#define LDM_KC __attribute__((address_space(4)))
+typedef const LDM_KC ldm_conv1d_args_t KConv;
+typedef const LDM_KC ldm_conv1d_seg_t KSeg;
+typedef const LDM_KC SegPlan KSegPlan;
+typedef const LDM_KC ConvPlan KPlan;
+
 // Staging issues every load of a segment before the first LDS store (one global round trip),
 // branch-free: out-of-range slots load a clamped in-bounds address and select 0, and store
 // to a scratch word past the operands.  The slot count NB is picked per segment from the
 // real item count (4 / 8 / 16 / 32), so a small segment does not pay a 32-slot unroll.
-template <int TP, int NB>
+// HO (hand-off): the input was written by another workgroup of the same launch (the
+// persistent loop): every load of it is an sc1 (L1-bypassing) load, loop_sync.h's rule.
+#ifndef UNET_PLAIN_LD
+#define UNET_PLAIN_LD 0       // diagnostic A/B only: plain loads for the hand-off (NOT coherent)
+#endif
+template <bool HO>
+__device__ __forceinline__ float ld_act(const float* p) {
+    if constexpr (HO && !UNET_PLAIN_LD)
+        return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<const unsigned*>(p),
+                                                           __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+
+// SiLU of a staged input: x * rcp(1 + 2^(-x log2 e)) on the transcendental unit (a few
+// instructions; the IEEE expf + division form was the dominant cost of staging, which is
+// VALU-latency-bound at one wave per SIMD).  Within 2 ulp of x / (1 + e^-x); the oracle
+// tolerances of DESIGN.md §9 hold with it.
+__device__ __forceinline__ float silu_stage(float x) {
+    return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+
+// The input window of one segment, [win][perm16(ci)] (pitch cinp + 4), flat over (ci, j)
+// with j fastest: thread tid stages items tid, tid + 256, ... with (ci, j) advanced
+// incrementally (no per-item division), every load of a pass issued before its LDS stores
+// (one global round trip per pass), branch-free (clamped address + select).  Channels
+// C..cinp-1 and positions outside [0, Lsrc) stage zeros.
+template <int NB, bool HO>
 __device__ __forceinline__ void stage_x_nb(float* __restrict__ xs, float* __restrict__ trash,
-                                           const ldm_conv1d_seg_t& s, const SegPlan& p, int b,
+                                           KSeg& s, const float* Xs, KSegPlan& p, int b,
                                            int pos0) {
-    constexpr int CW = TP <= 16 ? 32 : 64;            // window columns per pass
-    constexpr int RPP = 256 / CW;                     // channel rows per pass
     const int tid = threadIdx.x;
-    const int col = tid % CW, row = tid / CW;
     const bool up2 = s.mode == LDM_CONV_UP2;
     const int Lsrc = up2 ? 2 * s.L_in : s.L_in;
     const int pstart = pos0 * s.stride - s.pad;
-    const float* X = s.X + (int64_t)b * s.C * s.L_in;
-    const int ncolp = (p.win + CW - 1) / CW;
-    const int nitem = ncolp * ((p.cinp + RPP - 1) / RPP);
-    const int ld = p.cinp + 4;
-    for (int base = 0; base < nitem; base += NB) {
+    const float* X = Xs + (int64_t)b * s.C * s.L_in;
+    const int win = p.win, cinp = p.cinp, C = s.C, L_in = s.L_in, ld = cinp + 4;
+    const bool act = s.silu_in != 0;
+    const int dq = 256 / win, dr = 256 - dq * win;    // per-item advance of (ci, j); win < 256
+    int ci = tid / win, j = tid - ci * win;
+    const int nitem = cinp * win;
+    for (int base = 0; base < nitem; base += 256 * NB) {
         float v[NB];
         int dst[NB];
-        int rp = base / ncolp, cp = base - rp * ncolp;
+        uint64_t okm = 0;                    // item u's value is a real input (else zero)
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
-            const int ci = rp * RPP + row, j = cp * CW + col, pp = pstart + j;
-            const bool in = base + u < nitem && ci < p.cinp && j < p.win;
-            const bool ok = in && ci < s.C && pp >= 0 && pp < Lsrc;
-            const int src = ok ? ci * s.L_in + (up2 ? (pp >> 1) : pp) : 0;
-            v[u] = X[src];
-            v[u] = ok ? v[u] : 0.f;
+            const int pp = pstart + j;
+            const bool in = ci < cinp;
+            const bool ok = ci < C && pp >= 0 && pp < Lsrc;
+            const int src = ok ? ci * L_in + (up2 ? (pp >> 1) : pp) : 0;
+            v[u] = ld_act<HO>(X + src);      // consumed only in the store pass below
+            okm |= (uint64_t)ok << u;
             dst[u] = in ? j * ld + perm16(ci) : -1;
-            if (++cp == ncolp) { cp = 0; ++rp; }
+            // branch-free advance: a divergent branch here made the compiler drain every load
+            // issued so far (vmcnt(0)) at its join
+            j += dr;
+            const int wrap = j >= win ? 1 : 0;
+            j -= wrap * win;
+            ci += dq + wrap;
         }
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
             float* d = dst[u] >= 0 ? xs + dst[u] : trash;
-            *d = s.silu_in ? silu(v[u]) : v[u];
+            const float x = (okm >> u) & 1 ? v[u] : 0.f;
+            *d = act ? silu_stage(x) : x;
         }
     }
 }
 
-template <int TP>
-__device__ __forceinline__ void stage_x(float* xs, float* trash, const ldm_conv1d_seg_t& s,
-                                        const SegPlan& p, int b, int pos0) {
-    constexpr int CW = TP <= 16 ? 32 : 64;
-    const int n = ((p.win + CW - 1) / CW) * ((p.cinp + 256 / CW - 1) / (256 / CW));
-    if (n <= 4) stage_x_nb<TP, 4>(xs, trash, s, p, b, pos0);
-    else if (n <= 8) stage_x_nb<TP, 8>(xs, trash, s, p, b, pos0);
-    else if (n <= 16) stage_x_nb<TP, 16>(xs, trash, s, p, b, pos0);
-    else stage_x_nb<TP, 32>(xs, trash, s, p, b, pos0);
+// The same window from 16-byte loads (rows of L_in % 4 == 0 floats, 16-byte aligned): item =
+// (channel ci, 4-position source group g) with the groups aligned in the source row, so the
+// address and index arithmetic is paid once per 4 elements (the scalar form above was
+// VALU-bound at ~38 instructions per element, one wave per SIMD).  Raw buffer loads over the
+// shape's [C][L_in] block: channels ci >= C fall outside it and read 0; positions outside
+// [0, L_in) are masked per element.  UP2 writes every source element to its two window
+// positions.  HO: sc1 loads (cache policy 16), L1-bypassing like ld_act.
+template <int NB, bool HO>
+__device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs, float* __restrict__ trash,
+                                               KSeg& s, const float* Xs, KSegPlan& p, int b,
+                                               int pos0) {
+    const int tid = threadIdx.x;
+    const bool up2 = s.mode == LDM_CONV_UP2;
+    const int pstart = pos0 * s.stride - s.pad;               // window origin (>= -3)
+    const int win = p.win, cinp = p.cinp, L_in = s.L_in, ld = cinp + 4;
+    const bool act = s.silu_in != 0;
+    const int s0 = up2 ? (pstart >> 1) : pstart;               // floor: arithmetic shift
+    const int s1 = up2 ? ((pstart + win - 1) >> 1) : pstart + win - 1;
+    const int a0 = s0 & ~3;
+    const int ng = ((s1 - a0) >> 2) + 1;                       // <= 34 < 256
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(Xs) + (int64_t)b * s.C * L_in, (short)0, s.C * L_in * 4,
+        0x00020000);
+    const int dq = 256 / ng, dr = 256 - dq * ng;
+    int ci = tid / ng, g = tid - ci * ng;
+    const int nitem = cinp * ng;
+    for (int base = 0; base < nitem; base += 256 * NB) {
+        f32x4 v[NB];
+        int cg[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int off = ci * L_in + a0 + 4 * g;            // < 0 only for ci = 0: OOB -> 0
+            v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rs, (uint32_t)off * 4u, 0, HO ? 16 : 0));
+            cg[u] = ci < cinp ? (ci << 8) | g : -1;
+            g += dr;
+            const int wrap = g >= ng ? 1 : 0;
+            g -= wrap * ng;
+            ci += dq + wrap;
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int c = cg[u] >> 8, sp0 = a0 + 4 * (cg[u] & 0xff);
+            const int pc = perm16(c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int sp = sp0 + e;
+                const float x0 = (unsigned)sp < (unsigned)L_in ? v[u][e] : 0.f;
+                const float y = act ? silu_stage(x0) : x0;
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if (r == 1 && !up2) break;
+                    const int j = (up2 ? 2 * sp + r : sp) - pstart;
+                    const bool in = cg[u] >= 0 && (unsigned)j < (unsigned)win;
+                    float* d = in ? xs + j * ld + pc : trash;
+                    *d = y;
+                }
+            }
+        }
+    }
+}
+
+template <bool HO>
+__device__ __forceinline__ void stage_x(float* xs, float* trash, KSeg& s, const float* X,
+                                        KSegPlan& p, int b, int pos0) {
+    if ((s.L_in & 3) == 0 && ((uintptr_t)X & 15) == 0) {
+        const int ng = (p.win + 6) / 4 + 2;               // bound of the source groups per row
+        const int n = (p.cinp * ng + 255) / 256;
+        if (n <= 2) stage_x_vec_nb<2, HO>(xs, trash, s, X, p, b, pos0);
+        else if (n <= 5) stage_x_vec_nb<5, HO>(xs, trash, s, X, p, b, pos0);
+        else if (n <= 10) stage_x_vec_nb<10, HO>(xs, trash, s, X, p, b, pos0);
+        else stage_x_vec_nb<18, HO>(xs, trash, s, X, p, b, pos0);
+        return;
+    }
+    const int n = (p.cinp * p.win + 255) / 256;      // items per thread
+    if (n <= 4) stage_x_nb<4, HO>(xs, trash, s, X, p, b, pos0);
+    else if (n <= 9) stage_x_nb<9, HO>(xs, trash, s, X, p, b, pos0);
+    else if (n <= 17) stage_x_nb<17, HO>(xs, trash, s, X, p, b, pos0);
+    else stage_x_nb<34, HO>(xs, trash, s, X, p, b, pos0);
 }
 
 // Weights: 16-byte vector loads along a packed row (4 fp32 or 8 bf16 channels per load).
 template <typename TW, int NB>
-__device__ __forceinline__ void stage_w_nb(float* __restrict__ ws, const ldm_conv1d_seg_t& s,
-                                           const SegPlan& p, int co0) {
+__device__ __forceinline__ void stage_w_nb(float* __restrict__ ws, KSeg& s, KSegPlan& p,
+                                           int co0) {
     constexpr int EPV = 16 / sizeof(TW);              // elements per 16-byte vector
     const int tid = threadIdx.x;
     const int nvec = p.cinp / EPV;                    // vectors per (row, tap)
@@ -150,7 +276,7 @@ __device__ __forceinline__ void stage_w_nb(float* __restrict__ ws, const ldm_con
 }
 
 template <typename TW>
-__device__ __forceinline__ void stage_w(float* ws, const ldm_conv1d_seg_t& s, const SegPlan& p,
+__device__ __forceinline__ void stage_w(float* ws, KSeg& s, KSegPlan& p,
                                         int co0) {
     const int n = (16 * s.ksize * (p.cinp / (16 / (int)sizeof(TW))) + 255) / 256;
     if (n <= 1) stage_w_nb<TW, 1>(ws, s, p, co0);
@@ -159,20 +285,46 @@ __device__ __forceinline__ void stage_w(float* ws, const ldm_conv1d_seg_t& s, co
     else stage_w_nb<TW, 8>(ws, s, p, co0);
 }
 
-template <typename TW, int TP>
-__global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, ConvPlan pl) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
+// The operands of one conv call that the persistent loop moves with the step (the per-launch
+// kernel passes the call's own): seg[0]'s input, the per-channel bias row, and the output /
+// x_t / noise / t of the DDPM epilogue.
+struct ConvIO {
+    const float* x0;
+    const float* cbias;
+    float* Y;
+    const float* xlat;
+    const float* z;
+    int t;
+};
+
+__device__ __forceinline__ ConvIO conv_io(KConv& a) {
+    return {a.seg[0].X, a.cbias, a.Y, a.xlat, a.z, a.t};
+}
+
+// One output tile (16 channels x TP positions of shape b) of a conv call: stage every
+// segment's input window and weights in LDS (one global round trip), the MFMA contraction
+// split over the 4 waves, the partial tiles summed in wave order, the fused epilogue.
+// HO: the loop's hand-off form (sc1 loads of activations written inside the launch).
+// w_staged: the weights of this (call, co0) already sit in LDS (the loop prefetches them).
+// Ends with every LDS read done by its own wave only: a caller running another tile on the
+// same LDS first passes a workgroup barrier.
+template <typename TW, int TP, bool HO>
+__device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
+                                          const ConvIO& io, float* sm, int pos0, int co0,
+                                          int b, bool w_staged = false,
+                                          uint64_t* stp = nullptr) {
     constexpr int NT = TP / 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c16 = lane & 15;
-    const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
 
     float* trash = sm + pl.lds_floats - 4;
     for (int si = 0; si < a.n_seg; ++si) {
-        stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
-        stage_x<TP>(sm + pl.s[si].xoff, trash, a.seg[si], pl.s[si], b, pos0);
+        if (!w_staged) stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
+        stage_x<HO>(sm + pl.s[si].xoff, trash, a.seg[si], si == 0 ? io.x0 : a.seg[si].X,
+                    pl.s[si], b, pos0);
     }
     __syncthreads();
+    if (UNET_STAMP && stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
 
     f32x4 acc[NT];
 #pragma unroll
@@ -187,7 +339,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, C
     while (q >= ng) { q -= ng; ++k; }
     int cg = q;
     for (int ch = c_beg; ch < c_end; ++ch) {
-        const SegPlan& p = pl.s[si];
+        KSegPlan& p = pl.s[si];
         const int ks = a.seg[si].ksize, st = a.seg[si].stride;
         const f32x4 av = *reinterpret_cast<const f32x4*>(
             sm + p.woff + c16 * (ks * p.cinp + 4) + k * p.cinp + cg * 16 + 4 * g);
@@ -206,6 +358,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, C
         }
     }
     __syncthreads();                    // every wave is done reading the staged operands
+    if (UNET_STAMP && stp && threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
     float* red = sm;                    // [wave][t][reg][lane]
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -224,18 +377,31 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ldm_conv1d_args_t a, C
         float bb = 0.f;
         if (a.bias) bb += a.bias[co];
         if (a.bias2) bb += a.bias2[co];
-        if (a.cbias) bb += a.cbias[(int64_t)b * a.scb + co];
+        if (io.cbias) bb += io.cbias[(int64_t)b * a.scb + co];
         const int64_t idx = ((int64_t)b * a.Cout + co) * a.L_out + l;
         float pre = v + bb;
-        if (a.R) pre += a.R[idx];
+        if (a.R) pre += ld_act<HO>(a.R + idx);
+        float y = pre;
         if (a.epi == LDM_CONV_EPI_DDPM) {
-            const bool noise = a.t > 0;
-            a.Y[idx] = ddpm_update(a.xlat[idx], pre, noise ? a.z[idx] : 0.f, a.c1[a.t],
-                                   a.c2[a.t], a.sigma[a.t], noise);
-        } else {
-            a.Y[idx] = pre;
+            const bool noise = io.t > 0;
+            y = ddpm_update(ld_act<HO>(io.xlat + idx), pre, noise ? io.z[idx] : 0.f,
+                            a.c1[io.t], a.c2[io.t], a.sigma[io.t], noise);
         }
+        io.Y[idx] = y;
     }
+}
+
+struct ConvKArgs {
+    ldm_conv1d_args_t a;
+    ConvPlan pl;
+};
+
+template <typename TW, int TP>
+__global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const LDM_KC ConvKArgs* k = (const LDM_KC ConvKArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    conv_tile<TW, TP, false>(k->a, k->pl, conv_io(k->a), sm, blockIdx.x * TP, blockIdx.y * 16,
+                             blockIdx.z);
 }
 
 constexpr int kMaxLdsBytes = 160 * 1024;
@@ -278,7 +444,10 @@ int launch_tp(const ldm_conv1d_args_t& a, hipStream_t s) {
         attr_set = true;
     }
     const dim3 grid((a.L_out + TP - 1) / TP, (a.Cout + 15) / 16, a.B);
-    hipLaunchKernelGGL((conv1d_mfma_kernel<TW, TP>), grid, dim3(256), lds, s, a, pl);
+    ConvKArgs ka;
+    ka.a = a;
+    ka.pl = pl;
+    hipLaunchKernelGGL((conv1d_mfma_kernel<TW, TP>), grid, dim3(256), lds, s, ka);
     return launch_status("ldm_conv1d");
 }
 
@@ -291,11 +460,129 @@ int launch_conv(const ldm_conv1d_args_t& a, hipStream_t s) {
     return launch_tp<TW, 16>(a, s);
 }
 
-}  // namespace
-}  // namespace ldm
+// ---- C17 sampling loop: the whole reverse loop as one launch ---------------------------------
+// One replica of the step's conv program per XCD (32 workgroups, one per CU, the shapes
+// b = xcd mod 8); every conv is a phase whose 16-channel x 64-position tiles the replica's
+// workgroups deal among themselves, then an XCD-local barrier (loop_sync.h) hands the output
+// to the next phase.  At the UNet's sizes (C x L = 32768 at every level) a phase is 32 tiles
+// per shape: one tile per workgroup, so a step costs 18 barrier-separated tile rounds instead
+// of 18 dependent launches.  Activations are handed off with sc1 stores / sc1 loads; weights,
+// biases, tables and noise are never written inside the launch and use plain loads.
+constexpr int kStampPts = 6;
+static_assert(LDM_UNET_MAX_PHASES * kStampPts * 8 <= 4096, "stamps fit the debug tail");
+#ifndef UNET_LOOP_TP
+#define UNET_LOOP_TP 32
+#endif
+constexpr int kLoopTP = UNET_LOOP_TP;           // positions per tile
+constexpr int kLoopPerCU = kLoopTP == 64 ? 1 : 2;   // workgroups per CU
+constexpr int kLoopGrid = 256 * kLoopPerCU;      // 8 XCDs x 32 CUs x kLoopPerCU
+constexpr int kLoopLdsBytes = (kLoopPerCU == 1 ? 150 : 78) * 1024;   // every plan fits
+constexpr unsigned kLoopSpin = 1u << 22;
 
-extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
-    using namespace ldm;
+struct LoopPhase {
+    ldm_conv1d_args_t a;
+    ConvPlan pl;
+    int32_t patch, tiles_l, tiles_c, reserved;
+    int64_t cb_tstride;
+};
+
+struct UnetLoopArgs {
+    uint64_t ph;                 // device address of the uploaded LoopPhase table
+    int n_phase;
+    float* x2;
+    const float* noise;
+    int B, D, t_hi, steps;
+    unsigned* sync;
+    unsigned spin_limit;
+    uint64_t* stamp;             // UNET_STAMP builds: the workspace's debug tail
+};
+
+template <typename TW>
+__global__ __launch_bounds__(256) void unet_loop_kernel(UnetLoopArgs la) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    __shared__ unsigned s_xcc, s_rank;
+    __shared__ int s_ok;
+    unsigned* sync = la.sync;
+    const unsigned G = gridDim.x;
+    if (threadIdx.x == 0) {
+        unsigned xcc, rank;
+        s_ok = lsync::replica_census(sync, G, la.spin_limit, &xcc, &rank);
+        s_xcc = xcc;
+        s_rank = rank;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int xcc = (int)s_xcc, rank = (int)s_rank, nloc = (int)G / 8;
+    const int nsh = la.B > xcc ? (la.B - 1 - xcc) / 8 + 1 : 0;   // shapes of this replica
+    if (nsh == 0) return;                                           // idle replica (B < 8)
+    const int64_t xstride = (int64_t)la.B * la.D;
+    const LDM_KC LoopPhase* ph = (const LDM_KC LoopPhase*)la.ph;
+    unsigned* status = sync + 32 * lsync::R_STATUS;
+    unsigned* gen = sync + 32 * (lsync::R_GEN + xcc);
+    unsigned phase = 0;
+    bool w_next = false;             // the first tile's weights of the coming phase are in LDS
+    for (int st = 0; st < la.steps; ++st) {
+        const int t = la.t_hi - st, cur = st & 1;
+        for (int p = 0; p < la.n_phase; ++p) {
+            const LDM_KC LoopPhase& P = ph[p];
+            ConvIO io = conv_io(P.a);
+            if (P.patch & LDM_UNET_PATCH_X) io.x0 = la.x2 + cur * xstride;
+            if (P.patch & LDM_UNET_PATCH_STEP) {
+                io.Y = la.x2 + (cur ^ 1) * xstride;
+                io.xlat = la.x2 + cur * xstride;
+                io.z = la.noise + (int64_t)t * xstride;
+                io.t = t;
+            }
+            if (P.patch & LDM_UNET_PATCH_CBIAS) io.cbias = P.a.cbias + (int64_t)t * P.cb_tstride;
+            uint64_t* stp = nullptr;
+            if (UNET_STAMP && st == 1 && xcc == 0 && rank == 0)
+                stp = la.stamp + (size_t)p * kStampPts;
+            if (UNET_STAMP && stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
+            const int per = P.tiles_l * P.tiles_c, ntile = nsh * per;
+            for (int tile = rank; tile < ntile; tile += nloc) {
+                const int j = tile / per, r = tile - j * per;
+                const int ct = r / P.tiles_l, lt = r - ct * P.tiles_l;
+                if (tile != rank) __syncthreads();   // the previous tile's LDS reads are done
+                conv_tile<TW, kLoopTP, true>(P.a, P.pl, io, sm, lt * kLoopTP, ct * 16,
+                                             xcc + 8 * j, w_next && tile == rank,
+                                             tile == rank ? stp : nullptr);
+            }
+            if (UNET_STAMP && stp && threadIdx.x == 0) stp[3] = __builtin_amdgcn_s_memrealtime();
+            // XCD-local barrier (loop_sync.h replica_sync, split): drain this workgroup's
+            // output stores, arrive, and while the other workgroups finish, stage the weights of
+            // the next phase's first tile (they do not depend on this phase) into LDS.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();                         // every LDS read of this phase is done
+            if (UNET_STAMP && stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
+            ++phase;
+            bool last = false;
+            if (threadIdx.x == 0) {
+                const unsigned a = __hip_atomic_fetch_add(sync + 32 * (lsync::R_ARR + xcc), 1u,
+                                                          __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                last = a + 1 == phase * (unsigned)nloc;
+                if (last)
+                    __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const int pn = p + 1 < la.n_phase ? p + 1 : 0;
+            const LDM_KC LoopPhase& N = ph[pn];
+            w_next = (st + 1 < la.steps || pn != 0) && rank < nsh * N.tiles_l * N.tiles_c;
+            if (w_next) {
+                const int ct = (rank % (N.tiles_l * N.tiles_c)) / N.tiles_l;
+                for (int si = 0; si < N.a.n_seg; ++si)
+                    stage_w<TW>(sm + N.pl.s[si].woff, N.a.seg[si], N.pl.s[si], ct * 16);
+            }
+            if (UNET_STAMP && stp && threadIdx.x == 0) stp[5] = __builtin_amdgcn_s_memrealtime();
+            if (threadIdx.x == 0)
+                s_ok = last || lsync::spin_until(gen, phase, status, la.spin_limit);
+            __syncthreads();
+            if (!s_ok) return;
+        }
+    }
+}
+
+// The checks ldm_conv1d makes on one call (shared with the loop's program check).
+int check_conv_args(const ldm_conv1d_args_t* a) {
     LDM_REQUIRE(a && a->Y && a->B >= 1 && a->Cout >= 1 && a->L_out >= 1, LDM_EINVAL,
                 "bad conv1d args");
     LDM_REQUIRE(a->B <= 65535, LDM_EINVAL, "conv1d: B %d > 65535", a->B);
@@ -322,6 +609,131 @@ extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
                     i, g.ldw, g.kstride);
         LDM_REQUIRE(g.pad < g.ksize, LDM_EINVAL, "conv1d seg %d: pad %d >= ksize", i, g.pad);
     }
+    return 0;
+}
+
+template <typename TW>
+int launch_unet_loop(const UnetLoopArgs& la, hipStream_t s) {
+    auto* k = &unet_loop_kernel<TW>;
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static int init_err[kMaxDev];
+    int dev = 0;
+    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev, LDM_EINVAL,
+                "ldm_unet_loop: no current device");
+    std::call_once(once[dev], [&] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           kLoopLdsBytes);
+        int cus = 0, per_cu = 0;
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(k), 256, kLoopLdsBytes);
+        init_err[dev] = e != hipSuccess ? (int)e
+                        : (cus != 256 || per_cu < kLoopPerCU) ? LDM_ENOSYS : 0;
+    });
+    LDM_REQUIRE(init_err[dev] == 0, init_err[dev],
+                "ldm_unet_loop: needs 256 CUs with %d %d-byte workgroups each (MI355X): %d",
+                kLoopPerCU, kLoopLdsBytes, init_err[dev]);
+    hipError_t e = hipMemsetAsync(la.sync, 0, lsync::kSyncBytes, s);
+    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop: memset: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(k, dim3(kLoopGrid), dim3(256), kLoopLdsBytes, s, la);
+    return launch_status("ldm_unet_loop");
+}
+
+}  // namespace
+}  // namespace ldm
+
+extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
+    using namespace ldm;
+    LDM_TRY(check_conv_args(a));
     if (a->w_dtype == LDM_BF16) return launch_conv<unsigned short>(*a, (hipStream_t)s);
     return launch_conv<float>(*a, (hipStream_t)s);
+}
+
+extern "C" size_t ldm_unet_loop_ws_bytes(int n_phase) {
+    if (n_phase < 1 || n_phase > LDM_UNET_MAX_PHASES) return 0;
+    // + a 4 KiB debug tail (written only by the UNET_STAMP diagnostic build)
+    return ldm::lsync::kSyncBytes + (size_t)n_phase * sizeof(ldm::LoopPhase) + 4096;
+}
+
+extern "C" int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, void* ws,
+                                     size_t ws_bytes, ldm_stream_t s) {
+    using namespace ldm;
+    LDM_REQUIRE(ph && n_phase >= 1 && n_phase <= LDM_UNET_MAX_PHASES, LDM_EINVAL,
+                "ldm_unet_loop_prepare: n_phase %d", n_phase);
+    LDM_REQUIRE(ws && LDM_ALIGNED(ws, 256) && ws_bytes >= ldm_unet_loop_ws_bytes(n_phase),
+                LDM_EINVAL, "ldm_unet_loop_prepare: ws must be 256-B aligned, >= %zu bytes",
+                ldm_unet_loop_ws_bytes(n_phase));
+    std::vector<LoopPhase> h((size_t)n_phase);
+    for (int p = 0; p < n_phase; ++p) {
+        const ldm_unet_phase_t& q = ph[p];
+        LDM_TRY(check_conv_args(&q.conv));
+        LDM_REQUIRE(q.conv.w_dtype == ph[0].conv.w_dtype, LDM_EINVAL,
+                    "ldm_unet_loop_prepare: phase %d: w_dtype differs from phase 0", p);
+        LDM_REQUIRE((q.patch & ~(LDM_UNET_PATCH_X | LDM_UNET_PATCH_STEP |
+                                 LDM_UNET_PATCH_CBIAS)) == 0 &&
+                        (!(q.patch & LDM_UNET_PATCH_STEP) || q.conv.epi == LDM_CONV_EPI_DDPM) &&
+                        (!(q.patch & LDM_UNET_PATCH_CBIAS) ||
+                         (q.conv.cbias && q.conv.scb == 0 && q.cb_tstride >= 0)),
+                    LDM_EINVAL, "ldm_unet_loop_prepare: phase %d: patch 0x%x", p, q.patch);
+        LoopPhase& L = h[(size_t)p];
+        memset(&L, 0, sizeof(L));
+        L.a = q.conv;
+        int lds = 0;
+        LDM_REQUIRE(make_plan(q.conv, kLoopTP, &L.pl, &lds) == 0 && lds <= kLoopLdsBytes,
+                    LDM_ENOSPC, "ldm_unet_loop_prepare: phase %d needs %d B of LDS (> %d)", p,
+                    lds, kLoopLdsBytes);
+        L.patch = q.patch;
+        L.tiles_l = (q.conv.L_out + kLoopTP - 1) / kLoopTP;
+        L.tiles_c = (q.conv.Cout + 15) / 16;
+        L.cb_tstride = q.cb_tstride;
+    }
+    char* dst = reinterpret_cast<char*>(ws) + lsync::kSyncBytes;
+    hipError_t e = hipMemcpyAsync(dst, h.data(), h.size() * sizeof(LoopPhase),
+                                  hipMemcpyHostToDevice, (hipStream_t)s);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
+    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop_prepare: upload: %s",
+                hipGetErrorString(e));
+    return 0;
+}
+
+extern "C" int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* noise, int B,
+                             int D, int t_hi, int steps, void* ws, size_t ws_bytes,
+                             ldm_stream_t s) {
+    using namespace ldm;
+    LDM_REQUIRE(n_phase >= 1 && n_phase <= LDM_UNET_MAX_PHASES && x2 && noise && ws &&
+                    LDM_ALIGNED(ws, 256) && ws_bytes >= ldm_unet_loop_ws_bytes(n_phase),
+                LDM_EINVAL, "ldm_unet_loop: bad program / buffers");
+    LDM_REQUIRE(B >= 1 && B <= 16 && D >= 1 && steps >= 1 && t_hi >= steps - 1, LDM_EINVAL,
+                "ldm_unet_loop: B %d (1..16), D %d, t_hi %d, steps %d", B, D, t_hi, steps);
+    LDM_REQUIRE(w_dtype == LDM_F32 || w_dtype == LDM_BF16, LDM_EINVAL,
+                "ldm_unet_loop: w_dtype %d", w_dtype);
+    UnetLoopArgs la;
+    la.sync = reinterpret_cast<unsigned*>(ws);
+    la.ph = (uint64_t)(uintptr_t)(reinterpret_cast<char*>(ws) + lsync::kSyncBytes);
+    la.n_phase = n_phase;
+    la.x2 = x2;
+    la.noise = noise;
+    la.B = B;
+    la.D = D;
+    la.t_hi = t_hi;
+    la.steps = steps;
+    la.spin_limit = kLoopSpin;
+    la.stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + lsync::kSyncBytes +
+                                           (size_t)n_phase * sizeof(LoopPhase));
+    if (w_dtype == LDM_BF16) return launch_unet_loop<unsigned short>(la, (hipStream_t)s);
+    return launch_unet_loop<float>(la, (hipStream_t)s);
+}
+
+extern "C" int ldm_unet_loop_status(const void* ws, unsigned* status_host, ldm_stream_t s) {
+    using namespace ldm;
+    LDM_REQUIRE(ws && status_host, LDM_EINVAL, "ldm_unet_loop_status: null argument");
+    const unsigned* w = reinterpret_cast<const unsigned*>(ws) + 32 * lsync::R_STATUS;
+    hipError_t e = hipMemcpyAsync(status_host, w, sizeof(unsigned), hipMemcpyDeviceToHost,
+                                  (hipStream_t)s);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
+    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop_status: %s", hipGetErrorString(e));
+    return 0;
 }

@@ -169,8 +169,8 @@ def test_unet_forward_vs_golden(dev):
     assert e_r <= 1e-4 and e_u <= 0.1
 
 
-@pytest.mark.parametrize("use_graph", [False, True])
-def test_unet_sampling_10_vs_golden(dev, use_graph):
+@pytest.mark.parametrize("path", ["eager", "graph", "loop"])
+def test_unet_sampling_10_vs_golden(dev, path):
     import ldm_sdf
     gd = dict(np.load(os.path.join(GOLD, "unet_10.npz")))
     steps = int(gd["steps"])
@@ -179,7 +179,8 @@ def test_unet_sampling_10_vs_golden(dev, use_graph):
     noise = torch.zeros(1000, 2, 1024)
     noise[1000 - steps:] = torch.from_numpy(gd["noise_tail"])
     x = ldm_sdf.sample(m, sch, 2, steps=steps, dtype="fp32", x_T=torch.from_numpy(gd["x_T"]),
-                       noise=noise, device=dev, use_graph=use_graph).cpu().double()
+                       noise=noise, device=dev, use_graph=path == "graph",
+                       persistent=path == "loop").cpu().double()
     err = float((x - torch.from_numpy(gd["traj"][-1])).abs().max())
     assert err <= 1e-4, err
 
@@ -191,9 +192,52 @@ def test_unet_sampler_graph_equals_eager_bf16(dev):
     g = torch.Generator(device=dev).manual_seed(0)
     xT = torch.randn(4, 1024, device=dev, generator=g)
     noise = torch.randn(1000, 4, 1024, device=dev, generator=g)
-    a = ldm_sdf.Sampler(m, sch, 4, steps=25, dtype="bf16", device=dev, use_graph=False)
-    b = ldm_sdf.Sampler(m, sch, 4, steps=25, dtype="bf16", device=dev, use_graph=True)
+    a = ldm_sdf.Sampler(m, sch, 4, steps=25, dtype="bf16", device=dev, use_graph=False,
+                        persistent=False)
+    b = ldm_sdf.Sampler(m, sch, 4, steps=25, dtype="bf16", device=dev, use_graph=True,
+                        persistent=False)
     ra = a.run(xT, noise).clone()
     rb = b.run(xT, noise).clone()
     assert torch.equal(ra, rb)
     assert bool(torch.isfinite(ra).all())
+
+
+# The persistent loop (ldm_unet_loop): the same conv arithmetic per output
+# element as the per-step launches (64-position tiles instead of 16, the same contraction split
+# and wave-order sum), so the whole trajectory must be BIT-identical to the graph path --
+# including B > 8 (two shapes per XCD replica) and the full 1000 steps.
+@pytest.mark.parametrize("dtype,n,steps", [("bf16", 1, 1000), ("bf16", 3, 40), ("bf16", 9, 25),
+                                           ("bf16", 16, 12), ("fp32", 2, 30)])
+def test_unet_loop_bitwise_equals_graph(dev, dtype, n, steps):
+    import ldm_sdf
+    m = ldm_sdf.UNet1DDenoiser(seed=2468)
+    sch = ldm_sdf.DDPMSchedule()
+    g = torch.Generator(device=dev).manual_seed(n)
+    xT = torch.randn(n, 1024, device=dev, generator=g)
+    noise = torch.randn(1000, n, 1024, device=dev, generator=g)
+    lp = ldm_sdf.Sampler(m, sch, n, steps=steps, dtype=dtype, device=dev, persistent=True)
+    gr = ldm_sdf.Sampler(m, sch, n, steps=steps, dtype=dtype, device=dev, persistent=False)
+    rl = lp.run(xT, noise).clone()
+    assert lp.loop.status() == 0 and lp.loop_fallbacks == 0
+    rg = gr.run(xT, noise).clone()
+    assert bool(torch.isfinite(rl).all())
+    assert torch.equal(rl, rg), float((rl - rg).abs().max())
+    # a second run on the same workspace (sync words re-zeroed per launch) repeats it exactly
+    assert torch.equal(lp.run(xT, noise), rl)
+
+
+def test_unet_loop_rejects_bad_program(dev):
+    import ldm_sdf
+    from ldm_sdf import _capi as capi, ops
+    m = ldm_sdf.UNet1DDenoiser(seed=2468)
+    assert m.make_loop(17, "bf16", dev, ldm_sdf.DDPMSchedule().device(dev)["desc"]) is None
+    sd = ldm_sdf.DDPMSchedule().device(dev)
+    dpk = m.device_pack("bf16", dev)
+    buf = m.buffers(1, dev)
+    x = torch.zeros(2, 1, 1024, device=dev)
+    calls = m.step_args(dpk, buf, x[0], 0, out=x[1], sched=sd["desc"], z=x[0])
+    with pytest.raises(capi.LdmError, match="patch"):        # STEP patch on a non-DDPM conv
+        ops.unet_loop_prepare(calls, [capi.UNET_PATCH_STEP] + [0] * 17, [0] * 18, dev)
+    ws = ops.unet_loop_prepare(calls, [1] + [0] * 16 + [2], [0] * 18, dev)
+    with pytest.raises(capi.LdmError, match="t_hi"):
+        ops.unet_loop(ws, 18, capi.LDM_BF16, x, torch.zeros(1000, 1, 1024, device=dev), 5, 10)
