@@ -421,9 +421,10 @@ def config5(args, rank, world, dev, group, gen):
         torch.cuda.synchronize()
         return 1000 * reps / (time.perf_counter() - t0), lat, smp, status
 
-    # default Sampler path: the one-launch persistent loop when the batch has it (ldm_unet_loop)
-    sps, lat, sampler, loop_status = timed_sampler(None)
-    sps_graph, lat_graph, _, _ = timed_sampler(False)
+    # default Sampler path (the hipGraph of per-step launches for the UNet: DESIGN.md §9), and
+    # the one-launch loop (ldm_unet_loop) beside it on the same inputs
+    sps, lat, sampler, _ = timed_sampler(None)
+    sps_loop, lat_loop, _, loop_status = timed_sampler(True)
     loop_ok = all(v == 0 for v in loop_status)
     latents = ldm_sdf.dist.all_gather_rows(lat[:hi - lo].clone(), nb, group=group) \
         if world > 1 else lat[:nb].clone()
@@ -450,15 +451,15 @@ def config5(args, rank, world, dev, group, gen):
                                "unit": "TFLOP/s", "frac": ach / PEAK_TFLOPS["fp16"],
                                "flops_per_query": FLOPS_PER_QUERY_WIDEN,
                                "queries_per_launch": qpl, "avg_launch_ms": kms},
-           "unet_sample_steps_per_s": sps if loop_ok else None, "unet_batch_per_rank": nl,
-           "unet_path": ("one persistent launch for all 1000 steps (ldm_unet_loop: one replica "
-                         "of the 18-conv step per XCD, XCD-local barriers)"
+           "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
+           "unet_path": ("one persistent launch for all 1000 steps (ldm_unet_loop)"
                          if sampler.loop is not None else
                          "hipGraph of 1000 steps x 18 ldm_conv1d launches"),
-           "unet_loop_status_per_rep": loop_status,
-           "unet_graph_path": {"steps_per_s": sps_graph,
-                               "path": "hipGraph of 1000 steps x 18 ldm_conv1d launches",
-                               "bit_identical": bool(torch.equal(lat, lat_graph))},
+           "unet_loop_path": {"steps_per_s": sps_loop if loop_ok else None,
+                              "path": "ldm_unet_loop: one replica of the 18-conv step per XCD, "
+                                      "XCD-local barriers, one launch for 1000 steps",
+                              "status_per_rep": loop_status,
+                              "bit_identical": bool(torch.equal(lat, lat_loop))},
            "unet_conv_weight_bytes_per_step": wbytes}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)

@@ -106,7 +106,10 @@ class Sampler:
         make_loop = getattr(denoiser, "make_loop", None)
         self.loop = None
         self.loop_fallbacks = 0
-        if persistent is not False and make_loop is not None:
+        # a denoiser whose loop does not beat its per-step graph at this batch (prefer_loop(n)
+        # False: the 1D-UNet) runs the graph unless the loop is asked for
+        prefer = getattr(denoiser, "prefer_loop", lambda n_: True)(n)
+        if make_loop is not None and (persistent or (persistent is None and prefer)):
             self.loop = make_loop(n, dtype, self.device, self.sd["desc"])
         if persistent and self.loop is None:
             raise RuntimeError("no persistent sampling kernel for this denoiser/batch")

@@ -195,6 +195,14 @@ class UNet1DDenoiser:
             ops.conv1d_launch(a, x.device)
         return eps
 
+    def prefer_loop(self, n: int) -> bool:
+        """Whether ``Sampler`` uses the one-launch loop by default at batch n.  Measured on the
+        MI355X (profiles/r03e/unet_loop_ab*.log): the loop is 0.79x the hipGraph
+        of per-step launches at B = 1, 1.05x at B = 8 and 0.74x at B = 16 -- its 32 CUs per
+        shape are VALU/MFMA-throughput-bound where the graph spreads each conv over the chip --
+        so the graph stays the default and the loop is opt-in (``persistent=True``)."""
+        return False
+
     def make_loop(self, n: int, dtype: str, device, sched_desc):
         """Callable ``loop(x2, noise, t_hi, steps)`` running the whole reverse loop as ONE
         persistent launch (``ldm_unet_loop``: one replica of the 18-conv step per XCD, an

@@ -17,7 +17,7 @@ R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 # library for sched != 4), "q" = quarter layout, "s" = split layout, "sb" = split with its
 # in-stream barriers after the second MFMA pair (LDM_FS_BP=1, dev build)
 VARIANTS = os.environ.get("AB_VARIANTS", "s,q").split(",")
-LAYOUT = {"q": "quarter", "s": "split", "sb": "split"}
+LAYOUT = {"q": "quarter", "s": "split", "sb": "split", "s16": "split16"}
 FLOPS = 3146752
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)
