@@ -41,6 +41,12 @@ constexpr int kGWl = 512 * 4;                     // final-layer weights [w][p][
 #ifndef G_NOEPI
 #define G_NOEPI 0
 #endif
+// Diagnostic build only (-DFS16_DUMP=k, scripts/dump_split16.py; results are wrong): workgroup
+// 0 copies LDS positions 0..15 over the output after point k of its first tile (1: layer 0
+// written, 2: layer 1 part 1 done) and stops.
+#ifndef FS16_DUMP
+#define FS16_DUMP 0
+#endif
 constexpr int kGStamp = FS_STAMP ? 128 * 8 : 0;
 constexpr int kGLds = kGAct + kGRed + kGWl + kGStamp;
 static_assert(kGLds <= 160 * 1024, "LDS");
@@ -578,12 +584,31 @@ __global__ __launch_bounds__(256, 1) void dec_fs16_kernel(GArgs a) {
         run_part<T, GE_NONE, false, true>(c, accA, accB, 0, 0, false, false, none, false, 1, 0);
         acc_to_lds<T>(c, accA, nobias, 8);
         stamp(c);
+        if (FS16_DUMP == 1) {
+            fs_bar();
+            if (blockIdx.x == 0) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(smem);
+                for (int k = threadIdx.x; k < 16 * kGPos / 16; k += 256)
+                    reinterpret_cast<u32x4*>(a.out)[k] = src[k];
+            }
+            return;
+        }
 
         // ---- layers 1, 2 (and 3 when 512 wide)
         constexpr int L2P = S == 256 ? 3 : 4;
         int pi = 2;
         run_part<T, GE_FIN1, false, false>(c, accA, accB, 16, 0, true, false, none, true, pi, 0);
         run_part<T, GE_EARLY, true, false>(c, accB, accA, 16, 0, true, true, none, false, pi + 1, 0);
+
+        if (FS16_DUMP == 2) {
+            fs_bar();
+            if (blockIdx.x == 0) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(smem);
+                for (int k = threadIdx.x; k < 16 * kGPos / 16; k += 256)
+                    reinterpret_cast<u32x4*>(a.out)[k] = src[k];
+            }
+            return;
+        }
         pi += 2;
 #pragma unroll 1
         for (int l = 2; l < L2P; ++l, pi += 2) {
