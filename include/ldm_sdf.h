@@ -11,7 +11,9 @@
  *   - All buffers are caller-owned DEVICE pointers (torch tensors), contiguous, 16-byte aligned
  *     (the shim checks alignment).  The library never allocates or frees device memory.
  *   - Every launch is asynchronous on the caller's stream; no hidden synchronisation, no
- *     hipMalloc / hipMemcpy (so calls can be captured into a hipGraph).
+ *     hipMalloc / hipMemcpy (so calls can be captured into a hipGraph).  Exceptions, each
+ *     documented at its declaration: the *_status reads and ldm_unet_loop_prepare (a one-time
+ *     program upload) synchronise the stream.
  *   - Return 0 on success, a negative LDM_E* code for an argument error, or a positive
  *     hipError_t.  ldm_last_error() returns a thread-local message for the last failure.
  *   - One device per process (the current HIP device, as set by torch).

@@ -43,7 +43,7 @@ constexpr int kGWl = 512 * 4;                     // final-layer weights [w][p][
 #endif
 // Diagnostic build only (-DFS16_DUMP=k, scripts/dump_split16.py; results are wrong): workgroup
 // 0 copies LDS positions 0..15 over the output after point k of its first tile (1: layer 0
-// written, 2: layer 1 part 1 done) and stops.
+// written, 2: L1p1, 3: L2p0, 4: L2p1, 5: layer 3 written (skip 253), 6: L4p1 done) and stops.
 #ifndef FS16_DUMP
 #define FS16_DUMP 0
 #endif
@@ -407,6 +407,7 @@ __device__ __forceinline__ void fin_store(const GCtx& c, int shape, int local) {
 // [wx,wy,wz,wx,wy,wz,b_hi,b_lo] x xyz, the xyz fragments in c.b on entry) reading the first
 // position behind it -- after a barrier when `bar0` (the part follows serial LDS writes) --
 // then loads the next aux part's fragments (naux).  Without AUX the first k-step zero-inits.
+// A non-AUX part with naux (the one before layer 4) loads those fragments at its start.
 // Every part but layer 0's loads its fp32 bias (part index pi) and hands the previous one to
 // the epilogue.  EK work in window steps 0-7 (E8 false) or 8-15 (E8 true).  `mid`: the barrier
 // inside step 7; `endbar`: the one inside the last step.  np: the position the last step reads
@@ -420,6 +421,9 @@ __device__ __forceinline__ void run_part(GCtx& c, f32x4 (&acc)[4][8], const f32x
         for (int i = 0; i < 4; ++i) c.bias_y[i] = c.bias_n[i];
         load_bias(c, pi);
     }
+    // the part before layer 4's first: fetch its aux fragments now (an AUX part loads its
+    // successor's after its own aux step, below)
+    if (!AUX) load_aux(c, naux);
     if (AUX) {
         const f32x4 z = {};
         if (nk == 0 || bar0) {
@@ -614,8 +618,27 @@ __global__ __launch_bounds__(256, 1) void dec_fs16_kernel(GArgs a) {
         for (int l = 2; l < L2P; ++l, pi += 2) {
             const bool to4 = S == 512 && l == 3;      // the next part is layer 4's (aux)
             run_part<T, GE_LATE, false, false>(c, accA, accB, 16, 0, true, false, none, false, pi, 0);
+        if (FS16_DUMP == 3) {
+            fs_bar();
+            if (blockIdx.x == 0) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(smem);
+                for (int k = threadIdx.x; k < 16 * kGPos / 16; k += 256)
+                    reinterpret_cast<u32x4*>(a.out)[k] = src[k];
+            }
+            return;
+        }
             run_part<T, GE_EARLY, true, false>(c, accB, accA, 16, 0, true, true,
                                                to4 ? shp(2) : none, false, pi + 1, to4 ? 16 : 0);
+        if (FS16_DUMP == 4) {
+            fs_bar();
+            if (blockIdx.x == 0) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(smem);
+                for (int k = threadIdx.x; k < 16 * kGPos / 16; k += 256)
+                    reinterpret_cast<u32x4*>(a.out)[k] = src[k];
+            }
+            return;
+        }
+
         }
         if (S == 256) {
             // layer 3: one part of rows 64w..64w+63 -> positions 8 + 2w + q (serial, once every
@@ -624,9 +647,29 @@ __global__ __launch_bounds__(256, 1) void dec_fs16_kernel(GArgs a) {
             fs_bar();
             acc_to_lds<T>(c, accA, c.bias_n, 8);
             stamp(c);
+        if (FS16_DUMP == 5) {
+            fs_bar();
+            if (blockIdx.x == 0) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(smem);
+                for (int k = threadIdx.x; k < 16 * kGPos / 16; k += 256)
+                    reinterpret_cast<u32x4*>(a.out)[k] = src[k];
+            }
+            return;
+        }
+
             // layer 4 (K = 256, positions 8..15); part 0 -> early positions during part 1
             run_part<T, GE_NONE, false, true>(c, accA, accB, 8, 8, false, false, shp(3), true, pi + 1, 16);
             run_part<T, GE_EARLY, false, true>(c, accB, accA, 8, 8, false, true, none, false, pi + 2, 0);
+        if (FS16_DUMP == 6) {
+            fs_bar();
+            if (blockIdx.x == 0) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(smem);
+                for (int k = threadIdx.x; k < 16 * kGPos / 16; k += 256)
+                    reinterpret_cast<u32x4*>(a.out)[k] = src[k];
+            }
+            return;
+        }
+
             pi += 3;
         } else {
             run_part<T, GE_LATE, false, true>(c, accA, accB, 16, 0, true, false, shp(3), false, pi, 16);
