@@ -326,6 +326,32 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
     __syncthreads();
     if (UNET_STAMP && stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
 
+    // The epilogue's own operands (biases, residual, x_t / noise of the DDPM step) for this
+    // thread's outputs o = tid + 256 k, loaded now so their latency hides under the MFMA loop
+    // (they were a dependent round trip after it).  Out-of-tile outputs read index 0 (valid)
+    // and are not stored.
+    constexpr int NE = TP / 16;                      // 16 x TP outputs over 256 threads
+    float e_bb[NE], e_r[NE], e_x[NE], e_z[NE];
+    const bool ddpm = a.epi == LDM_CONV_EPI_DDPM;
+    const bool noise = ddpm && io.t > 0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int o = tid + 256 * k;
+        const int r = o / TP, pc = o % TP;
+        const int co = co0 + r, l = pos0 + pc;
+        const bool ok = co < a.Cout && l < a.L_out;
+        const int coc = ok ? co : 0;
+        const int64_t idx = ok ? ((int64_t)b * a.Cout + co) * a.L_out + l : 0;
+        float bb = 0.f;                              // the per-launch kernel's summation order
+        if (a.bias) bb += a.bias[coc];
+        if (a.bias2) bb += a.bias2[coc];
+        if (io.cbias) bb += io.cbias[(int64_t)b * a.scb + coc];
+        e_bb[k] = bb;
+        e_r[k] = a.R ? ld_act<HO>(a.R + idx) : 0.f;
+        e_x[k] = ddpm ? ld_act<HO>(io.xlat + idx) : 0.f;
+        e_z[k] = noise ? io.z[idx] : 0.f;
+    }
+
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -366,7 +392,9 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
         for (int i = 0; i < 4; ++i) red[((wave * NT + t) * 4 + i) * 64 + lane] = acc[t][i];
     __syncthreads();
 
-    for (int o = tid; o < 16 * TP; o += 256) {
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int o = tid + 256 * k;
         const int r = o / TP, pc = o % TP;
         const int co = co0 + r, l = pos0 + pc;
         if (co >= a.Cout || l >= a.L_out) continue;
@@ -374,19 +402,12 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) v += red[((w * NT + t) * 4 + i) * 64 + ln];
-        float bb = 0.f;
-        if (a.bias) bb += a.bias[co];
-        if (a.bias2) bb += a.bias2[co];
-        if (io.cbias) bb += io.cbias[(int64_t)b * a.scb + co];
         const int64_t idx = ((int64_t)b * a.Cout + co) * a.L_out + l;
-        float pre = v + bb;
-        if (a.R) pre += ld_act<HO>(a.R + idx);
+        float pre = v + e_bb[k];
+        if (a.R) pre += e_r[k];
         float y = pre;
-        if (a.epi == LDM_CONV_EPI_DDPM) {
-            const bool noise = io.t > 0;
-            y = ddpm_update(ld_act<HO>(io.xlat + idx), pre, noise ? io.z[idx] : 0.f,
-                            a.c1[io.t], a.c2[io.t], a.sigma[io.t], noise);
-        }
+        if (ddpm)
+            y = ddpm_update(e_x[k], pre, e_z[k], a.c1[io.t], a.c2[io.t], a.sigma[io.t], noise);
         io.Y[idx] = y;
     }
 }
