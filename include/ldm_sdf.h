@@ -506,6 +506,9 @@ int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, void* ws, siz
 int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* noise, int B, int D,
                   int t_hi, int steps, void* ws, size_t ws_bytes, ldm_stream_t s);
 int ldm_unet_loop_status(const void* ws, unsigned* status_host, ldm_stream_t s);
+/* Fault-injection control of ldm_unet_loop on the current device (tests only): polls before a
+ * barrier wait gives up (status 1); 0 restores the default. */
+int ldm_unet_loop_config(unsigned spin_limit);
 
 /* ---- C18 marching cubes on a decoded volume ---------------------------- */
 /* vol: fp32 [N][N][N] (z slowest, as decode writes it); a corner is inside when v < level.

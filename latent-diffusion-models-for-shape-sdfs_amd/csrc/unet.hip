@@ -32,6 +32,7 @@
 
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -633,6 +634,10 @@ int check_conv_args(const ldm_conv1d_args_t* a) {
     return 0;
 }
 
+// ldm_unet_loop_config (fault-injection tests only): the barrier spin limit per device
+constexpr int kLoopMaxDev = 64;
+std::atomic<unsigned> g_loop_spin[kLoopMaxDev];
+
 template <typename TW>
 int launch_unet_loop(const UnetLoopArgs& la, hipStream_t s) {
     auto* k = &unet_loop_kernel<TW>;
@@ -741,7 +746,10 @@ extern "C" int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* n
     la.D = D;
     la.t_hi = t_hi;
     la.steps = steps;
-    la.spin_limit = kLoopSpin;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLoopMaxDev) dev = 0;
+    const unsigned forced = g_loop_spin[dev].load();
+    la.spin_limit = forced ? forced : kLoopSpin;
     la.stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + lsync::kSyncBytes +
                                            (size_t)n_phase * sizeof(LoopPhase));
     if (w_dtype == LDM_BF16) return launch_unet_loop<unsigned short>(la, (hipStream_t)s);
@@ -756,5 +764,14 @@ extern "C" int ldm_unet_loop_status(const void* ws, unsigned* status_host, ldm_s
                                   (hipStream_t)s);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
     LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop_status: %s", hipGetErrorString(e));
+    return 0;
+}
+
+extern "C" int ldm_unet_loop_config(unsigned spin_limit) {
+    using namespace ldm;
+    int dev = 0;
+    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kLoopMaxDev, LDM_EINVAL,
+                "ldm_unet_loop_config: no current device");
+    g_loop_spin[dev].store(spin_limit);
     return 0;
 }

@@ -183,6 +183,7 @@ SIGNATURES = [
     ("ldm_unet_loop_prepare", _i, [C.POINTER(UnetPhase), _i, _vp, _sz, _vp]),
     ("ldm_unet_loop", _i, [_i, _i, _fp, _fp, _i, _i, _i, _i, _vp, _sz, _vp]),
     ("ldm_unet_loop_status", _i, [_vp, C.POINTER(C.c_uint), _vp]),
+    ("ldm_unet_loop_config", _i, [C.c_uint]),
     ("ldm_gemm_bf16", _i, [C.POINTER(GemmArgs), _vp]),
     ("ldm_denoiser_train_ws_bytes", _sz, [C.POINTER(Denoiser), _i]),
     ("ldm_denoiser_fwd", _i, [C.POINTER(Denoiser), _fp, _vp, _i, _fp, _vp, _vp]),

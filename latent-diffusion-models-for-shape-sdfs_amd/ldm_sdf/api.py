@@ -158,8 +158,9 @@ class Sampler:
                 return self.result
             self.loop_fallbacks += 1
             why = {1: "a grid barrier timed out",
-                   2: "replica placement mismatch (device switched to the chip-wide loop)"}
-            warnings.warn(f"ldm_sample_loop: status {st} ({why.get(st, 'unknown')}); "
+                   2: "replica placement mismatch: workgroups not 1/8 per XCD, nothing computed"}
+            warnings.warn(f"persistent sampling loop ({type(self.model).__name__}): status {st} "
+                          f"({why.get(st, 'unknown')}); "
                           "re-running this sample on the per-step path", RuntimeWarning)
             self.x[0].copy_(x_T)
             self._loop()

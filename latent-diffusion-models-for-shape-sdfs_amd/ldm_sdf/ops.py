@@ -593,6 +593,12 @@ def unet_loop(ws: torch.Tensor, n_phase: int, w_dtype: int, x2: torch.Tensor,
                "ldm_unet_loop")
 
 
+def unet_loop_config(spin_limit: int = 0) -> None:
+    """Fault-injection control of ``ldm_unet_loop`` on the current device (tests only): the
+    barrier spin limit (0: the default)."""
+    capi.check(capi.load().ldm_unet_loop_config(int(spin_limit)), "ldm_unet_loop_config")
+
+
 def unet_loop_status(ws: torch.Tensor) -> int:
     """0 when the last ``unet_loop`` on ``ws`` completed, 1 when a barrier timed out, 2 when
     its workgroups were not placed 32 per XCD (nothing computed).  Synchronises the stream."""

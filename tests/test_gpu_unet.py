@@ -241,3 +241,28 @@ def test_unet_loop_rejects_bad_program(dev):
     ws = ops.unet_loop_prepare(calls, [1] + [0] * 16 + [2], [0] * 18, dev)
     with pytest.raises(capi.LdmError, match="t_hi"):
         ops.unet_loop(ws, 18, capi.LDM_BF16, x, torch.zeros(1000, 1, 1024, device=dev), 5, 10)
+
+
+def test_unet_loop_timeout_surfaces_and_falls_back(dev):
+    """A barrier that gives up (forced with a 1-poll spin limit) must surface as status 1 and
+    make Sampler re-run the sample on the per-step path: the same numbers as the graph."""
+    import ldm_sdf
+    from ldm_sdf import ops
+    m = ldm_sdf.UNet1DDenoiser(seed=2468)
+    sch = ldm_sdf.DDPMSchedule()
+    g = torch.Generator(device=dev).manual_seed(7)
+    xT = torch.randn(2, 1024, device=dev, generator=g)
+    noise = torch.randn(1000, 2, 1024, device=dev, generator=g)
+    ref = ldm_sdf.Sampler(m, sch, 2, steps=6, dtype="bf16", device=dev,
+                          persistent=False).run(xT, noise).clone()
+    lp = ldm_sdf.Sampler(m, sch, 2, steps=6, dtype="bf16", device=dev, persistent=True)
+    ops.unet_loop_config(1)
+    try:
+        with pytest.warns(RuntimeWarning, match="status 1"):
+            got = lp.run(xT, noise).clone()
+    finally:
+        ops.unet_loop_config(0)
+    assert lp.loop_fallbacks == 1
+    assert torch.equal(got, ref)
+    assert lp.loop.status() == 1           # the status word of the abandoned launch
+    assert torch.equal(lp.run(xT, noise), ref) and lp.loop.status() == 0
