@@ -424,8 +424,10 @@ def config5(args, rank, world, dev, group, gen):
     # default Sampler path (the hipGraph of per-step launches for the UNet: DESIGN.md §9), and
     # the one-launch loop (ldm_unet_loop) beside it on the same inputs
     sps, lat, sampler, _ = timed_sampler(None)
-    sps_loop, lat_loop, _, loop_status = timed_sampler(True)
-    loop_ok = all(v == 0 for v in loop_status)
+    has_loop = 1 <= nl <= 16                     # UNet1DDenoiser.make_loop's batch range
+    if has_loop:
+        sps_loop, lat_loop, _, loop_status = timed_sampler(True)
+        loop_ok = all(v == 0 for v in loop_status)
     latents = ldm_sdf.dist.all_gather_rows(lat[:hi - lo].clone(), nb, group=group) \
         if world > 1 else lat[:nb].clone()
     dec = ldm_sdf.SDFDecoder(1024, seed=1235)            # widen-skip (L + 3 >= H)
@@ -455,11 +457,12 @@ def config5(args, rank, world, dev, group, gen):
            "unet_path": ("one persistent launch for all 1000 steps (ldm_unet_loop)"
                          if sampler.loop is not None else
                          "hipGraph of 1000 steps x 18 ldm_conv1d launches"),
-           "unet_loop_path": {"steps_per_s": sps_loop if loop_ok else None,
-                              "path": "ldm_unet_loop: one replica of the 18-conv step per XCD, "
-                                      "XCD-local barriers, one launch for 1000 steps",
-                              "status_per_rep": loop_status,
-                              "bit_identical": bool(torch.equal(lat, lat_loop))},
+           "unet_loop_path": ({"steps_per_s": sps_loop if loop_ok else None,
+                               "path": "ldm_unet_loop: one replica of the 18-conv step per XCD, "
+                                       "XCD-local barriers, one launch for 1000 steps",
+                               "status_per_rep": loop_status,
+                               "bit_identical": bool(torch.equal(lat, lat_loop))}
+                              if has_loop else None),
            "unet_conv_weight_bytes_per_step": wbytes}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)
