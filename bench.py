@@ -395,6 +395,25 @@ def handoff_latency():
     return {"one_way_ns": same[len(same) // 2], "source": os.path.relpath(files[-1], ROOT)}
 
 
+def allgather_latency():
+    """Per-layer latency of the sampler's hand-off pattern without its arithmetic: an
+    all-gather of 1024 tagged 8-byte granules among one XCD's 32 workgroups, all 8 XCDs at once
+    (scripts/microbench/allgather_latency.hip, median of its reps), from the newest
+    profiles/*/allgather_latency.json; None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "allgather_latency.json")))
+    if not files:
+        return None
+    try:
+        rows = [json.loads(l) for l in open(files[-1]) if l.strip().startswith("{")]
+        ph = sorted(r["phase_ns_median"] for r in rows if r["ok"])
+    except (OSError, ValueError, KeyError):
+        return None
+    if not ph:
+        return None
+    return {"phase_ns": ph[len(ph) // 2], "source": os.path.relpath(files[-1], ROOT)}
+
+
 def config5(args, rank, world, dev, group, gen):
     """Config 5: 1000-step DDPM sampling of ``--c5-batch`` 1024-d latents with the 1D-UNet
     (bf16 weights, hipGraph) -> fp16 MFMA decode (widen-skip decoder, L=1024) of a 512^3
@@ -669,6 +688,17 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
                         "frac = that model step time / the measured step time"}
     else:
         roof = None
+    ag = allgather_latency()
+    roof_ag = None
+    if ag is not None:
+        # each layer boundary is in fact an all-gather of the layer inside the XCD replica
+        # (32 workgroups publish 32 rows each, every one stages all 1024): 6 per step
+        model_ag = 6 * ag["phase_ns"] * 1e-9
+        roof_ag = {"bound": "xcd-allgather-latency", "achieved": sps, "peak": 1.0 / model_ag,
+                   "unit": "steps/s", "frac": sps * model_ag, "allgathers_per_step": 6,
+                   "allgather_phase_ns": ag["phase_ns"], "source": ag["source"],
+                   "note": "peak = 1 / (6 x the measured per-layer all-gather of 1024 tagged "
+                           "granules among 32 workgroups of one XCD, no arithmetic)"}
     return {"metric": "DDPM sample steps/sec", "value": sps if valid else None,
             "valid": valid, "unit": "steps/s",
             "batch": nb, "batch_per_rank": nl, "T": 1000, "shape_steps_per_s": sps * nb,
@@ -682,6 +712,7 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
                            "path": "hipGraph of 1000 fused steps (6 kernels each)",
                            "bit_identical": same},
             "roofline": roof,
+            "roofline_allgather": roof_ag,
             "roofline_hbm": {"bound": "hbm", "achieved": sps * wbytes / 1e9,
                          "peak": 8000.0, "unit": "GB/s",
                          "frac": sps * wbytes / 8e12,
