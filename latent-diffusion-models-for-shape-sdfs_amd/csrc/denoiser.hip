@@ -263,10 +263,10 @@ __global__ __launch_bounds__(64) void small_linear_v2(SmallArgs a) {
             for (int i = 0; i < half; ++i) {
                 const float send = upper ? acc[i] : acc[i + half];
                 const float keep = upper ? acc[i + half] : acc[i];
-                acc[i] = keep + __shfl_xor(send, o);
+                acc[i] = keep + xor_lane(send, o, lane);
             }
         } else {
-            acc[0] += __shfl_xor(acc[0], o);
+            acc[0] += xor_lane(acc[0], o, lane);
         }
     }
     // lane owns value index idx = (lane >> (6 - log2 V)) in natural order: idx = r*MB + b
@@ -363,10 +363,10 @@ __global__ __launch_bounds__(256) void small_linear_v3(SmallArgs a) {
             for (int i = 0; i < half; ++i) {
                 const float send = upper ? acc[i] : acc[i + half];
                 const float keep = upper ? acc[i + half] : acc[i];
-                acc[i] = keep + __shfl_xor(send, o);
+                acc[i] = keep + xor_lane(send, o, lane);
             }
         } else {
-            acc[0] += __shfl_xor(acc[0], o);
+            acc[0] += xor_lane(acc[0], o, lane);
         }
     }
     constexpr int LB = (MB >= 16) ? 4 : 3;
@@ -471,10 +471,10 @@ __global__ __launch_bounds__(256) void small_linear_v4(SmallArgs a) {
             for (int i = 0; i < half; ++i) {
                 const float send = upper ? acc[i] : acc[i + half];
                 const float keep = upper ? acc[i + half] : acc[i];
-                acc[i] = keep + __shfl_xor(send, o);
+                acc[i] = keep + xor_lane(send, o, lane);
             }
         } else {
-            acc[0] += __shfl_xor(acc[0], o);
+            acc[0] += xor_lane(acc[0], o, lane);
         }
     }
     constexpr int LB = (MB >= 16) ? 4 : 3;

@@ -163,10 +163,10 @@ __device__ __forceinline__ float row_dot(const float (&w)[NJ][8], const float* x
             for (int i = 0; i < half; ++i) {
                 const float send = upper ? acc[i] : acc[i + half];
                 const float keep = upper ? acc[i + half] : acc[i];
-                acc[i] = keep + __shfl_xor(send, o);
+                acc[i] = keep + xor_lane(send, o, lane);
             }
         } else {
-            acc[0] += __shfl_xor(acc[0], o);
+            acc[0] += xor_lane(acc[0], o, lane);
         }
     }
     return acc[0];
@@ -453,10 +453,10 @@ __device__ __forceinline__ float reduce_scatter(float (&acc)[NV], int lane) {
             for (int i = 0; i < half; ++i) {
                 const float send = upper ? acc[i] : acc[i + half];
                 const float keep = upper ? acc[i + half] : acc[i];
-                acc[i] = keep + __shfl_xor(send, o);
+                acc[i] = keep + xor_lane(send, o, lane);
             }
         } else {
-            acc[0] += __shfl_xor(acc[0], o);
+            acc[0] += xor_lane(acc[0], o, lane);
         }
     }
     return acc[0];
