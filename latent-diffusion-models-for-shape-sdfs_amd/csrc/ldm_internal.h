@@ -1,6 +1,8 @@
 // Internal helpers shared by the libldm_sdf.so translation units (not part of the ABI).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -23,6 +25,25 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
     do {                                 \
         if (int e_ = (x)) return e_;     \
     } while (0)
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, bytes) once per (kernel, device), thread-safe
+// (a function-static flag set it once per process: a second device never got it).
+template <auto Kernel>
+int set_max_lds_once(int bytes, const char* what) {
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static int err[kMaxDev];
+    int dev = 0;
+    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev, LDM_EINVAL,
+                "%s: no current device", what);
+    std::call_once(once[dev], [&] {
+        err[dev] = (int)hipFuncSetAttribute(reinterpret_cast<const void*>(Kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    });
+    LDM_REQUIRE(err[dev] == 0, err[dev], "%s: hipFuncSetAttribute: %s", what,
+                hipGetErrorString((hipError_t)err[dev]));
+    return 0;
+}
 
 #define LDM_ALIGNED(p, a) ((((uintptr_t)(p)) & ((a) - 1)) == 0)
 

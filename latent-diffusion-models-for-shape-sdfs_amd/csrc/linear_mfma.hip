@@ -348,15 +348,8 @@ template <typename TW, bool XK, bool WK, bool XV, bool WV, int KCH>
 int launch_one(const ldm_linear_args_t& a, const SplitPlan& sp, hipStream_t s) {
     auto* k = &linear_mfma_kernel<TW, XK, WK, XV, WV, KCH>;
     constexpr int kLdsBytes = Chunk<KCH>::LdsBytes;
-    static bool attr_set = false;     // one per instantiation; idempotent if raced
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 kLdsBytes);
-        LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_linear (mfma): hipFuncSetAttribute: %s",
-                    hipGetErrorString(e));
-        attr_set = true;
-    }
+    LDM_TRY((set_max_lds_once<&linear_mfma_kernel<TW, XK, WK, XV, WV, KCH>>(
+        kLdsBytes, "ldm_linear (mfma)")));
     const dim3 grid((a.M + 63) / 64, (a.Bn + 63) / 64, sp.nz);
     hipLaunchKernelGGL(k, grid, dim3(256), kLdsBytes, s, a, sp.kc_len);
     if (sp.nz > 1) {

@@ -456,15 +456,7 @@ int launch_tp(const ldm_conv1d_args_t& a, hipStream_t s) {
     LDM_REQUIRE(make_plan(a, TP, &pl, &lds) == 0, LDM_ENOSPC,
                 "conv1d: staged operands need %d B of LDS (> %d); split the channels", lds,
                 kMaxLdsBytes);
-    static bool attr_set = false;     // one per instantiation; idempotent if raced
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&conv1d_mfma_kernel<TW, TP>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
-        LDM_REQUIRE(e == hipSuccess, (int)e, "conv1d: hipFuncSetAttribute: %s",
-                    hipGetErrorString(e));
-        attr_set = true;
-    }
+    LDM_TRY((set_max_lds_once<&conv1d_mfma_kernel<TW, TP>>(kMaxLdsBytes, "conv1d")));
     const dim3 grid((a.L_out + TP - 1) / TP, (a.Cout + 15) / 16, a.B);
     ConvKArgs ka;
     ka.a = a;
