@@ -261,10 +261,11 @@ int forward(const ldm_denoiser_t* w, const TrainWs& L, const float* eps_target,
 }
 
 // Backward GEMMs from go_b / go_T (dL/d eps_hat in bf16) and the saved activations.
-// `hook` (may be null) is called at point 0 once the gradients of the in-projection,
-// out-projection and block weights are final and no later launch of this backward reads those
-// weights (after the dtemb launch, the last reader of the blocks' U_k), and at point 1 after
-// the last GEMM (the time-MLP weights), so their optimizer updates can start there.
+// `hook` (may be null) is called at point 0 once the gradients of the out-projection and block
+// weights are final and no later launch of this backward reads those weights (after the dtemb
+// launch, the last reader of the blocks' U_k), and at point 1 after the last GEMM (the time-MLP
+// and in-projection weights: dWin and dx, which reads Win^T, are in the last launch), so
+// their optimizer updates can start there.
 struct StepHook {
     int (*fn)(void* ctx, int point, hipStream_t s);
     void* ctx;
@@ -314,10 +315,9 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
         for (int k = 0; k < nb; ++k) seg(dt, L.g_b[k], H, Wt[k] + (size_t)H * H, H, H);
         dt.Cb = L.dtemb_b; dt.ldcb = H; dt.CbT = L.dtemb_T; dt.ldct = Bp;
         dt.colsum = L.p_bt2;
-        ldm_gemm_prob_t dwi = prob(H, D, H);                     // dWin = dh0^T xt
-        seg(dwi, L.dh0_T, Bp, L.xt_T, Bp, Bp);
-        dwi.C = gr->w_in; dwi.ldc = D;
-        LDM_TRY(launch({dt, dwi}, s));
+        // alone in its launch: 256 tiles, every K a multiple of 128 -> the 128-deep 2-group
+        // tile (with dWin's 64 tiles beside it the launch fell to 64 x 64 tiles: 30.8 us)
+        LDM_TRY(launch({dt}, s));
         if (hook) LDM_TRY(hook->fn(hook->ctx, 0, s));
     }
     {
@@ -334,13 +334,18 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
         ldm_gemm_prob_t dw1 = prob(H, TE, H);                    // dWt1 = gt^T e
         seg(dw1, L.gt_T, Bp, L.e_T, Bp, Bp);
         dw1.C = gr->w_t1; dw1.ldc = TE;
+        // dWin rides in the step's last launch: its 64 tiles run beside dWt1's 32 on CUs that
+        // launch leaves idle (beside dtemb it cost dtemb its 128-deep tile: 30.8 -> 22.7 us)
+        ldm_gemm_prob_t dwi = prob(H, D, H);                     // dWin = dh0^T xt
+        seg(dwi, L.dh0_T, Bp, L.xt_T, Bp, Bp);
+        dwi.C = gr->w_in; dwi.ldc = D;
         if (dx) {
             ldm_gemm_prob_t px = prob(B, D, B);                  // dx = dh0 Win
             seg(px, L.dh0_b, H, w->wt_in, H, H);
             px.C = dx; px.ldc = D;
-            LDM_TRY(launch({dw1, px}, s));
+            LDM_TRY(launch({dw1, dwi, px}, s));
         } else {
-            LDM_TRY(launch({dw1}, s));
+            LDM_TRY(launch({dw1, dwi}, s));
         }
     }
     if (hook) LDM_TRY(hook->fn(hook->ctx, 1, s));
@@ -669,8 +674,9 @@ int fork_events(hipEvent_t (&ev)[kForks + 1]) {
 }
 
 // The step's AdamW in three batches, each started as soon as its gradients are final and no
-// later launch of the step reads its weights: 0 = block, in- and out-projection weights (after
-// the dtemb launch), 1 = the time-MLP weights (after the last GEMM), 2 = the biases (after the
+// later launch of the step reads its weights: 0 = block and out-projection weights (after the
+// dtemb launch), 1 = the time-MLP and in-projection weights (after the last GEMM), 2 = the
+// biases (after the
 // bias sums).  With a side stream every batch runs there behind a fork event, on a capped grid
 // (2 workgroups per CU) so the main stream's GEMMs keep wave slots; the main stream waits for
 // the side stream at the end.
@@ -747,10 +753,11 @@ extern "C" int ldm_denoiser_train_step_adamw(
     // batch of each tensor, matched by its gradient pointer
     for (int i = 0; i < n; ++i) {
         const float* g = tensors[i].g;
-        bool b0 = g == grads->w_out || g == grads->w_in;
+        bool b0 = g == grads->w_out;
         for (int k = 0; k < w->n_blocks; ++k) b0 = b0 || g == grads->w_blk[k];
+        const bool b1 = g == grads->w_t1 || g == grads->w_t2 || g == grads->w_in;
         // without a side stream one launch after the bias sums (fewer launches, same bits)
-        const int bi = !A.side ? 2 : b0 ? 0 : (g == grads->w_t1 || g == grads->w_t2) ? 1 : 2;
+        const int bi = !A.side ? 2 : b0 ? 0 : b1 ? 1 : 2;
         A.batch[bi][A.nb[bi]++] = &tensors[i];
     }
     const TrainWs L = layout(w, B, saved);
