@@ -269,6 +269,13 @@ def bench_autodecoder(args, dev):
            "value": 1.0 / dt, "unit": "steps/s", "ms_per_step": dt * 1e3,
            "samples_per_s": S * P / dt, "flops_per_sample_fwd": fwd,
            "tflops_fwd_bwd": 3 * fwd * S * P / dt / 1e12, "dtype": "bf16",
+           "roofline": {"bound": "mfma", "achieved": 3 * fwd * S * P / dt / 1e12,
+                        "peak": PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
+                        "frac": 3 * fwd * S * P / dt / 1e12 / PEAK_TFLOPS["bf16"],
+                        "flops_per_step": 3 * fwd * S * P,
+                        "note": "3 x forward FLOPs (forward, dX and dW products) of the "
+                                "1,048,576 samples over the wall time of a step (every launch "
+                                "incl. the loss, latent gradients and Adam)"},
            "loss_first_last": [st.losses[0], st.losses[-1]]}
     if not args.no_cpu:
         from oracle import ref_cpu as R
@@ -483,9 +490,39 @@ def config5(args, rank, world, dev, group, gen):
                                "bit_identical": bool(torch.equal(lat, lat_loop))}
                               if has_loop else None),
            "unet_conv_weight_bytes_per_step": wbytes}
+    # the graph path's bound: 18 dependent launches per step, each at least one dependent graph
+    # node (the conv grids are 64-128 workgroups at B = 1: ldm_conv1d's tile rule)
+    node = graph_node_latency(128 if nl <= 2 else 512)
+    if node is not None:
+        model_step = 18 * node["node_ns"] * 1e-9
+        res["unet_roofline"] = {
+            "bound": "launch-chain", "achieved": sps, "peak": 1.0 / model_step,
+            "unit": "steps/s", "frac": sps * model_step, "launches_per_step": 18,
+            "node_ns": node["node_ns"], "node_grid": node["grid"], "source": node["source"],
+            "note": "peak = 1 / (18 x the measured latency of one dependent node of a captured "
+                    "chain of empty kernels at the convs' grid size); frac = that model step "
+                    "time / the measured step time of the default (graph) path"}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)
     return res
+
+
+def graph_node_latency(grid: int = 128):
+    """One dependent hipGraph node's latency (an empty 256-thread kernel of ``grid``
+    workgroups in a captured 18 000-launch chain) measured by
+    scripts/microbench/graph_chain_latency.hip on an MI355X, from the newest
+    profiles/*/graph_node_latency.json; None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "graph_node_latency.json")))
+    if not files:
+        return None
+    try:
+        rows = [json.loads(l) for l in open(files[-1]) if l.strip().startswith("{")]
+        row = min(rows, key=lambda r: abs(r["grid"] - grid))
+    except (OSError, ValueError, KeyError):
+        return None
+    return {"node_ns": row["node_ns_median"], "grid": row["grid"],
+            "source": os.path.relpath(files[-1], ROOT)}
 
 
 def free_port() -> int:
@@ -662,7 +699,7 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
     xg = sampler_g.run(xT, noise).clone()
     sps_graph = timed(lambda: sampler_g.run(xT, noise))
     same = bool(torch.equal(sampler.run(xT, noise), xg))
-    e2e = None
+    e2e, c3_dtype = None, None
     if not args.no_config3:      # config 3: sample(8) -> decode 128^3, end to end
         if world > 1:
             dist.barrier(group)
@@ -670,7 +707,8 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
         t2 = time.perf_counter()
         lat = ldm_sdf.sample(den, sch, nb, dtype="bf16", device=dev, group=group,
                              generator=gen)
-        ldm_sdf.decode(decoder, lat, 128, dtype=args.dtype, group=group)
+        c3_dtype = ldm_sdf.resolve_decode_dtype("auto", lat)
+        ldm_sdf.decode(decoder, lat, 128, dtype=c3_dtype, group=group)
         torch.cuda.synchronize()
         e2e = time.perf_counter() - t2
     wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nl * den.D * 4
@@ -702,9 +740,12 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
     return {"metric": "DDPM sample steps/sec", "value": sps if valid else None,
             "valid": valid, "unit": "steps/s",
             "batch": nb, "batch_per_rank": nl, "T": 1000, "shape_steps_per_s": sps * nb,
-            "path": ("one persistent launch for all 1000 steps "
-                     "(weights in registers, XCD-hierarchical grid barrier per "
-                     "layer)" if persistent
+            "path": (({"replica": "one persistent launch for all 1000 steps: one network "
+                                  "copy per XCD in registers, XCD-local tagged hand-offs "
+                                  "per layer (sample_replica_kernel)",
+                       "chipwide": "one persistent launch for all 1000 steps: weights in "
+                                   "registers, XCD-hierarchical grid barrier per layer"}
+                      .get(loop_form, f"persistent loop ({loop_form})")) if persistent
                      else "hipGraph of 1000 fused steps (6 kernels each)"),
             "loop_status": loop_status, "loop_status_per_rep": statuses,
             "loop_form": loop_form,
@@ -722,8 +763,10 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
                                  "in registers, so it is grid-barrier-latency-bound "
                                  "(DESIGN.md §5)"},
             "config3_sample_plus_decode128_s": e2e,
-            "config3": ("sample(8) (1000 bf16 steps, fresh Sampler: includes its setup) -> "
-                        "decode(128^3, bf16), wall time" if e2e is not None else None)}
+            "config3": (f"sample(8) (1000 bf16 steps, fresh Sampler: includes its setup) -> "
+                        f"decode(128^3, {c3_dtype}: dtype='auto' for these latents, "
+                        f"api.resolve_decode_dtype), wall time" if e2e is not None else None),
+            "config3_decode_dtype": c3_dtype if e2e is not None else None}
 
 
 def bench_train(args, dev, gen):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define LDM_ABI_VERSION 4
+#define LDM_ABI_VERSION 5
 
 /* dtypes */
 #define LDM_F32 0
@@ -44,8 +44,8 @@ extern "C" {
 /* workspace ops for ldm_workspace_bytes() */
 #define LDM_OP_DECODER_GRID 1
 #define LDM_OP_DECODER_POINTS 2
-/* ldm_workspace_bytes() returns the quarter layout's 64 KiB per shape, enough for every layout
-   (split: 32 KiB, pass8: 32 KiB); ldm_workspace_bytes_layout() gives the layout's own size */
+/* ldm_workspace_bytes() returns the largest per-layout need (split / split16), enough for every
+   layout; ldm_workspace_bytes_layout() gives the layout's own size */
 
 typedef void* ldm_stream_t; /* hipStream_t; NULL = the null stream */
 
@@ -61,19 +61,21 @@ typedef struct ldm_decoder {
     int32_t hidden;       /* H (512) */
     int32_t skip_width;   /* 253 or 512 */
     int32_t latent_dim;   /* L */
-    int32_t n_stages;     /* bf16/f16: number of 8 KiB weight stages per tile; f32: 0 */
-    const void* weights;  /* bf16/f16: stage blob [n_stages][8][64][8]; f32: fp32 blob */
+    int32_t n_stages;     /* bf16/f16: k-steps of one wave's weight stream (split 384 / 448,
+                             split16 192 / 224 at skip width 253 / 512); f32: 0 */
+    const void* weights;  /* bf16/f16: per-wave stream blob (ldm_sdf/pack.py pack_split /
+                             pack_split16); f32: fp32 blob */
     const float* wz;      /* fp32 [2][H][L]  latent columns of layer 0 and layer 4 */
     const float* bz;      /* fp32 [2][H]     biases of layer 0 and layer 4 */
     const float* wxyz;    /* fp32 [2][H][3]  xyz columns of layer 0 and layer 4 */
     const float* w_last;  /* fp32 [H] final 512->1 weights (bf16/f16: MFMA-row permuted) */
     float b_last;         /* final bias */
-    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_PASS8, _QUARTER, _SPLIT, _SPLIT16 */
+    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_SPLIT (default) or _SPLIT16 */
 } ldm_decoder_t;
 
 /* Stage-blob layouts of the MFMA decoder. */
-#define LDM_LAYOUT_PASS8 0   /* 8 m-chunks x 1 k-step per stage, 2 passes per layer */
-#define LDM_LAYOUT_QUARTER 1 /* 4 m-chunks x 2 k-steps per stage, 4 quarters per layer */
+#define LDM_LAYOUT_PASS8 0   /* removed in ABI 5 (superseded by SPLIT): LDM_ENOSYS */
+#define LDM_LAYOUT_QUARTER 1 /* removed in ABI 5 (superseded by SPLIT): LDM_ENOSYS */
 #define LDM_LAYOUT_SPLIT 2   /* features split over the 4 waves, per-wave weight streams */
 #define LDM_LAYOUT_SPLIT16 3 /* the split work division on 16x16x32 MFMAs, fp32 biases */
 
@@ -483,14 +485,17 @@ int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s);
  *   LDM_UNET_PATCH_STEP   Y = x2[cur ^ 1], xlat = x2[cur], z = noise[t], t  (the DDPM conv)
  *   LDM_UNET_PATCH_CBIAS  cbias = cbias + t * cb_tstride   (a [T][Cout] table's base: E_i[t])
  * ldm_unet_loop_prepare checks the program (every conv must be an ldm_conv1d-valid call with
- * batch-uniform cbias, w_dtype equal across phases, LDS plan at 64-position tiles <= 160 KiB)
- * and uploads it into ws (synchronises the stream).  ldm_unet_loop then runs `steps` reverse
- * steps from t_hi in one launch: one replica of the program per XCD (shapes b = xcd mod 8),
- * an XCD-local barrier between dependent convs; the convs' arithmetic is ldm_conv1d's, so the
- * result is bit-identical to n_phase * steps ldm_conv1d calls.  Result in x2[steps & 1].
- * LDM_ENOSYS when the device has no 8 x 32-CU replica geometry (not an MI355X) or B > 16.
+ * batch-uniform cbias, w_dtype and B equal across phases, LDS plan at 32-position tiles
+ * <= 78 KiB) and uploads it into ws with a header recording n_phase, w_dtype, B (phase 0's
+ * conv.B) and D (phase 0's seg[0].L_in) (synchronises the stream).  ldm_unet_loop then runs
+ * `steps` reverse steps from t_hi in one launch: 512 workgroups (2 per CU, 64 per XCD), one
+ * replica of the program per XCD (shapes b = xcd mod 8), an XCD-local barrier between
+ * dependent convs; the convs' arithmetic is ldm_conv1d's, so the result is bit-identical to
+ * n_phase * steps ldm_conv1d calls.  Result in x2[steps & 1].  LDM_EINVAL for B outside
+ * 1..16; LDM_ENOSYS when the device has no 8 x 32-CU replica geometry (not an MI355X).
  * ldm_unet_loop_status: 0 completed, 1 a barrier timed out (partial latents), 2 workgroups
- * were not placed 32 per XCD (nothing computed); synchronises the stream. */
+ * were not placed 64 per XCD (nothing computed), 3 the launch's n_phase / w_dtype / B / D
+ * differ from the prepared program's (nothing computed); synchronises the stream. */
 #define LDM_UNET_PATCH_X 1
 #define LDM_UNET_PATCH_STEP 2
 #define LDM_UNET_PATCH_CBIAS 4

@@ -475,12 +475,12 @@ int launch_conv(const ldm_conv1d_args_t& a, hipStream_t s) {
 }
 
 // ---- C17 sampling loop: the whole reverse loop as one launch ---------------------------------
-// One replica of the step's conv program per XCD (32 workgroups, one per CU, the shapes
-// b = xcd mod 8); every conv is a phase whose 16-channel x 64-position tiles the replica's
-// workgroups deal among themselves, then an XCD-local barrier (loop_sync.h) hands the output
-// to the next phase.  At the UNet's sizes (C x L = 32768 at every level) a phase is 32 tiles
-// per shape: one tile per workgroup, so a step costs 18 barrier-separated tile rounds instead
-// of 18 dependent launches.  Activations are handed off with sc1 stores / sc1 loads; weights,
+// One replica of the step's conv program per XCD (64 workgroups, two per CU, the shapes
+// b = xcd mod 8); every conv is a phase whose 16-channel x 32-position tiles (kLoopTP) the
+// replica's workgroups deal among themselves, then an XCD-local barrier (loop_sync.h) hands the
+// output to the next phase.  At the UNet's sizes (C x L = 32768 at every level) a phase is 64
+// tiles per shape: one tile per workgroup, so a step costs 18 barrier-separated tile rounds
+// instead of 18 dependent launches.  Activations are handed off with sc1 stores / sc1 loads; weights,
 // biases, tables and noise are never written inside the launch and use plain loads.
 constexpr int kStampPts = 6;
 static_assert(LDM_UNET_MAX_PHASES * kStampPts * 8 <= 4096, "stamps fit the debug tail");
@@ -500,6 +500,16 @@ struct LoopPhase {
     int64_t cb_tstride;
 };
 
+// Program header, written by ldm_unet_loop_prepare between the sync words and the phase table
+// (outside the region memset before each launch): the launch's arguments must match the
+// program it runs, or every workgroup returns before touching a buffer (status 3).
+struct LoopHeader {
+    int32_t magic, n_phase, w_dtype, B, D, reserved[59];
+};
+static_assert(sizeof(LoopHeader) == 256, "header keeps the phase table 256-B aligned");
+constexpr int32_t kLoopMagic = 0x554e4554;   // "UNET"
+constexpr unsigned kStatusMismatch = 3u;
+
 struct UnetLoopArgs {
     uint64_t ph;                 // device address of the uploaded LoopPhase table
     int n_phase;
@@ -518,6 +528,17 @@ __global__ __launch_bounds__(256) void unet_loop_kernel(UnetLoopArgs la) {
     __shared__ int s_ok;
     unsigned* sync = la.sync;
     const unsigned G = gridDim.x;
+    {   // the program must be the one these arguments describe (uniform: all or none return)
+        const LDM_KC LoopHeader* hd = (const LDM_KC LoopHeader*)(la.ph - sizeof(LoopHeader));
+        const int wdt = sizeof(TW) == 2 ? LDM_BF16 : LDM_F32;
+        if (hd->magic != kLoopMagic || hd->n_phase != la.n_phase || hd->w_dtype != wdt ||
+            hd->B != la.B || hd->D != la.D) {
+            if (blockIdx.x == 0 && threadIdx.x == 0)
+                __hip_atomic_store(sync + 32 * lsync::R_STATUS, kStatusMismatch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
     if (threadIdx.x == 0) {
         unsigned xcc, rank;
         s_ok = lsync::replica_census(sync, G, la.spin_limit, &xcc, &rank);
@@ -672,8 +693,10 @@ extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
 
 extern "C" size_t ldm_unet_loop_ws_bytes(int n_phase) {
     if (n_phase < 1 || n_phase > LDM_UNET_MAX_PHASES) return 0;
-    // + a 4 KiB debug tail (written only by the UNET_STAMP diagnostic build)
-    return ldm::lsync::kSyncBytes + (size_t)n_phase * sizeof(ldm::LoopPhase) + 4096;
+    // sync words | program header | phase table | a 4 KiB debug tail (written only by the
+    // UNET_STAMP diagnostic build)
+    return ldm::lsync::kSyncBytes + sizeof(ldm::LoopHeader) +
+           (size_t)n_phase * sizeof(ldm::LoopPhase) + 4096;
 }
 
 extern "C" int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, void* ws,
@@ -688,8 +711,9 @@ extern "C" int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, vo
     for (int p = 0; p < n_phase; ++p) {
         const ldm_unet_phase_t& q = ph[p];
         LDM_TRY(check_conv_args(&q.conv));
-        LDM_REQUIRE(q.conv.w_dtype == ph[0].conv.w_dtype, LDM_EINVAL,
-                    "ldm_unet_loop_prepare: phase %d: w_dtype differs from phase 0", p);
+        LDM_REQUIRE(q.conv.w_dtype == ph[0].conv.w_dtype && q.conv.B == ph[0].conv.B,
+                    LDM_EINVAL, "ldm_unet_loop_prepare: phase %d: w_dtype / B differ from phase 0",
+                    p);
         LDM_REQUIRE((q.patch & ~(LDM_UNET_PATCH_X | LDM_UNET_PATCH_STEP |
                                  LDM_UNET_PATCH_CBIAS)) == 0 &&
                         (!(q.patch & LDM_UNET_PATCH_STEP) || q.conv.epi == LDM_CONV_EPI_DDPM) &&
@@ -708,9 +732,19 @@ extern "C" int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, vo
         L.tiles_c = (q.conv.Cout + 15) / 16;
         L.cb_tstride = q.cb_tstride;
     }
+    LoopHeader hd;
+    memset(&hd, 0, sizeof(hd));
+    hd.magic = kLoopMagic;
+    hd.n_phase = n_phase;
+    hd.w_dtype = ph[0].conv.w_dtype;
+    hd.B = ph[0].conv.B;
+    hd.D = ph[0].conv.seg[0].L_in;
+    std::vector<char> blob(sizeof(LoopHeader) + h.size() * sizeof(LoopPhase));
+    memcpy(blob.data(), &hd, sizeof(hd));
+    memcpy(blob.data() + sizeof(hd), h.data(), h.size() * sizeof(LoopPhase));
     char* dst = reinterpret_cast<char*>(ws) + lsync::kSyncBytes;
-    hipError_t e = hipMemcpyAsync(dst, h.data(), h.size() * sizeof(LoopPhase),
-                                  hipMemcpyHostToDevice, (hipStream_t)s);
+    hipError_t e = hipMemcpyAsync(dst, blob.data(), blob.size(), hipMemcpyHostToDevice,
+                                  (hipStream_t)s);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
     LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop_prepare: upload: %s",
                 hipGetErrorString(e));
@@ -730,7 +764,8 @@ extern "C" int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* n
                 "ldm_unet_loop: w_dtype %d", w_dtype);
     UnetLoopArgs la;
     la.sync = reinterpret_cast<unsigned*>(ws);
-    la.ph = (uint64_t)(uintptr_t)(reinterpret_cast<char*>(ws) + lsync::kSyncBytes);
+    la.ph = (uint64_t)(uintptr_t)(reinterpret_cast<char*>(ws) + lsync::kSyncBytes +
+                                  sizeof(LoopHeader));
     la.n_phase = n_phase;
     la.x2 = x2;
     la.noise = noise;
@@ -743,6 +778,7 @@ extern "C" int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* n
     const unsigned forced = g_loop_spin[dev].load();
     la.spin_limit = forced ? forced : kLoopSpin;
     la.stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + lsync::kSyncBytes +
+                                           sizeof(LoopHeader) +
                                            (size_t)n_phase * sizeof(LoopPhase));
     if (w_dtype == LDM_BF16) return launch_unet_loop<unsigned short>(la, (hipStream_t)s);
     return launch_unet_loop<float>(la, (hipStream_t)s);

@@ -8,7 +8,8 @@ over ``torch.distributed`` (RCCL).
 from .models import DDPMSchedule, MLPDenoiser, SDFDecoder, decoder_layer_dims  # noqa: F401
 from .unet import UNet1DDenoiser  # noqa: F401
 from .mesh import marching_cubes, marching_cubes_batch, mc_table, write_ply  # noqa: F401
-from .api import Sampler, TrainState, decode, decode_points, sample, train, train_step  # noqa: F401
+from .api import (Sampler, TrainState, decode, decode_points, resolve_decode_dtype,  # noqa: F401
+                  sample, train, train_step)
 from .autodecoder import (AutoDecoderState, autodecoder_train_step,  # noqa: F401
                           train_autodecoder)
 from . import ops, dist, pack, data  # noqa: F401

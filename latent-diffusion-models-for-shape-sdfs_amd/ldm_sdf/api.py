@@ -26,13 +26,34 @@ from .models import DDPMSchedule, MLPDenoiser, SDFDecoder
 
 
 # ---------------------------------------------------------------------------------- decode
+# The bf16 decode meets SURVEY §8(c)'s 1e-2 bound (vs the fp64 decoder) only while the
+# activations stay near the scale it was calibrated at: its rounding error grows with the
+# latents' scale (He-init DeepSDF, CPU oracle at the 16-bit contract: 3.5e-3 at latent RMS
+# 0.1, 5.9e-3 at 0.2, 1.1e-2 at 0.5).  fp16 has 3 more mantissa bits (6e-4 / 1.4e-3 at RMS
+# 0.1 / 0.5, inside its 2e-3 bound) at the same MFMA rate, so dtype="auto" decodes latents
+# whose largest per-shape RMS exceeds BF16_MAX_LATENT_RMS in fp16.
+BF16_MAX_LATENT_RMS = 0.2
+
+
+def resolve_decode_dtype(dtype: str, latents: torch.Tensor) -> str:
+    """``dtype`` itself, or for "auto" bf16 when every shape's latent RMS is within the bf16
+    calibration (``BF16_MAX_LATENT_RMS``), else fp16 (one device->host read)."""
+    if dtype != "auto":
+        return dtype
+    lat = latents.float().reshape(latents.shape[0] if latents.dim() > 1 else 1, -1)
+    rms = float(lat.pow(2).mean(dim=1).sqrt().max())
+    return "bf16" if rms <= BF16_MAX_LATENT_RMS else "fp16"
+
+
 def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
-           bbox: Tuple[float, float] = (-1.0, 1.0), dtype: str = "bf16", group=None,
+           bbox: Tuple[float, float] = (-1.0, 1.0), dtype: str = "auto", group=None,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """SDF of every shape on a dense ``resolution^3`` grid over ``bbox^3``.
 
     Layout ``[B, z, y, x]`` (z slowest).  With an initialised process group the grid is
     z-slab sharded over its ranks and all-gathered (every rank returns the full volume).
+    ``dtype``: "fp32" (exact), "bf16", "fp16" or "auto" (``resolve_decode_dtype``: bf16 for
+    latents at the calibrated scale, fp16 above it, so the result stays inside §8(c)'s bound).
     """
     capi.require_device(latents)
     if latents.dim() == 1:
@@ -42,6 +63,7 @@ def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
     N = int(resolution)
     if N < 2:
         raise ValueError("resolution must be >= 2")
+    dtype = resolve_decode_dtype(dtype, latents)
     pack = decoder.device_pack(dtype, latents.device)
     desc = pack["desc"]
     beta = ops.decoder_fold(desc, latents.float().contiguous())
@@ -59,11 +81,13 @@ def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
 
 
 def decode_points(decoder: SDFDecoder, latents: torch.Tensor, xyz: torch.Tensor, *,
-                  dtype: str = "bf16") -> torch.Tensor:
-    """SDF at arbitrary points: xyz ``[B, P, 3]`` (or ``[P, 3]`` shared) -> ``[B, P]``."""
+                  dtype: str = "auto") -> torch.Tensor:
+    """SDF at arbitrary points: xyz ``[B, P, 3]`` (or ``[P, 3]`` shared) -> ``[B, P]``
+    (``dtype`` as in ``decode``)."""
     capi.require_device(latents, xyz)
     if latents.dim() == 1:
         latents = latents[None]
+    dtype = resolve_decode_dtype(dtype, latents)
     B = latents.shape[0]
     if xyz.dim() == 2:
         xyz = xyz[None].expand(B, -1, -1)
@@ -130,12 +154,15 @@ class Sampler:
 
         The persistent loop's grid barriers are bounded: if one gives up (status 1, e.g. when
         other work on the device kept part of the grid from being resident), the launch has
-        left partially updated latents; status 2 (the XCD-replica loop found its workgroups
-        placed other than 32 per XCD) left them untouched and switched the device to the
-        chip-wide loop.  With ``check`` (default) the status word is read back
-        (one stream synchronisation) and such a run is redone on the per-step path, which gives
-        the same numbers bit for bit; ``loop_fallbacks`` counts these.  ``check=False`` keeps
-        the call asynchronous: the caller then reads ``loop.status()`` itself."""
+        left partially updated latents; status 2 (an XCD-replica loop found its workgroups
+        placed other than one replica's worth per XCD) left them untouched.  After status 2
+        the MLP sampler's library has switched the device to its chip-wide loop
+        (``loop.placement_fallback``); a denoiser with no chip-wide loop (the 1D-UNet) drops
+        its loop here, so later runs stay on the per-step graph instead of retrying the
+        launch.  With ``check`` (default) the status word is read back (one stream
+        synchronisation) and such a run is redone on the per-step path, which gives the same
+        numbers bit for bit; ``loop_fallbacks`` counts these.  ``check=False`` keeps the call
+        asynchronous: the caller then reads ``loop.status()`` itself."""
         gen = getattr(self.model, "table_gen", 0)
         if gen != self._gen:
             # the denoiser was trained (or re-packed) since this sampler was built: re-pack its
@@ -158,10 +185,13 @@ class Sampler:
                 return self.result
             self.loop_fallbacks += 1
             why = {1: "a grid barrier timed out",
-                   2: "replica placement mismatch: workgroups not 1/8 per XCD, nothing computed"}
+                   2: "replica placement mismatch: workgroups not 1/8 per XCD, nothing computed",
+                   3: "launch arguments differ from the prepared program, nothing computed"}
             warnings.warn(f"persistent sampling loop ({type(self.model).__name__}): status {st} "
                           f"({why.get(st, 'unknown')}); "
                           "re-running this sample on the per-step path", RuntimeWarning)
+            if st == 2 and not getattr(self.loop, "placement_fallback", False):
+                self.loop = None          # nothing to switch to: the graph from now on
             self.x[0].copy_(x_T)
             self._loop()
             return self.result

@@ -4,8 +4,8 @@
 * Decode shards the grid by z-slab: rank r computes ``k in [r*S, min((r+1)*S, N))`` with
   ``S = ceil(N/W)`` for every shape into a local ``[B, S, N, N]`` buffer; per shape, one
   ``all_gather_into_tensor(out[b], local[b])`` writes the volume in place (z-slowest, so the
-  W slabs in rank order ARE the volume), issued asynchronously group by group so the gathers
-  overlap the next group's compute.
+  W slabs in rank order ARE the volume); a group's gathers go out as ONE coalesced collective,
+  asynchronously, so they overlap the next group's compute.
 * Sampling and training shard the batch (data parallel); training all-reduces gradients.
 
 The compute of a slab is injected (``compute_slab``) so the partition / reassembly logic is
@@ -52,8 +52,9 @@ def decode_sharded(compute_slab: Callable[..., None], B: int, N: int,
     with shapes ``[b0, b1)``.  Per shape ``b`` the volume ``out[b]`` (z slowest) is exactly the
     W slabs in rank order, so ONE ``all_gather_into_tensor(out[b], local[b])`` assembles it in
     place: no transpose and no second copy.  Shapes go in groups
-    (``shape_groups``); each group's gathers are issued asynchronously (RCCL runs them on its
-    own stream) before the next group's slabs are computed, so communication overlaps compute.
+    (``shape_groups``); each group's gathers are issued as one coalesced asynchronous
+    collective (``_gather_group``; RCCL runs it on its own stream) before the next group's
+    slabs are computed, so communication overlaps compute.
     When W does not divide N the last slab is zero-padded to S = ceil(N/W) rows and the
     gathered ``[W*S, N, N]`` is trimmed into ``out[b]``.
     """
@@ -79,18 +80,31 @@ def decode_sharded(compute_slab: Callable[..., None], B: int, N: int,
                 part = torch.empty(b1 - b0, k1 - k0, N, N, device=device, dtype=torch.float32)
                 compute_slab(k0, k1, part, b0, b1)
                 local[b0:b1, :k1 - k0].copy_(part)
+        dsts = []
         for b in range(b0, b1):
             dst = vol[b] if even else torch.empty(world * S, N, N, device=device,
                                                   dtype=torch.float32)
-            pending.append(dist.all_gather_into_tensor(dst, local[b], group=group,
-                                                       async_op=True))
+            dsts.append((b, dst))
             if not even:
                 staged.append((b, dst))
+        pending.append(_gather_group(dsts, local, group))
     for w in pending:
         w.wait()
     for b, dst in staged:
         vol[b].copy_(dst[:N])
     return vol
+
+
+def _gather_group(dsts, local: torch.Tensor, group):
+    """One coalesced collective for a group's per-shape gathers: the group's
+    ``all_gather_into_tensor(dst_b, local[b])`` calls are issued inside torch's coalescing
+    manager, which hands them to the backend as ONE grouped operation (RCCL: one
+    ``ncclGroupStart/End`` launch instead of one launch per shape), asynchronously.  Returns
+    the handle to wait on."""
+    with dist._coalescing_manager(group=group, async_ops=True) as cm:
+        for b, dst in dsts:
+            dist.all_gather_into_tensor(dst, local[b], group=group)
+    return cm
 
 
 def batch_shard(n: int, rank: int, world: int) -> Tuple[int, int]:

@@ -80,7 +80,7 @@ class SDFDecoder:
         return (self.hidden == 512 and self.n_hidden == 8 and self.skip == 4
                 and self.skip_width in (253, 512))
 
-    # the feature-split kernel (csrc/decoder_fs.hip); "quarter" / "pass8" stay selectable
+    # the feature-split kernel (csrc/decoder_fs.hip); "split16" (decoder_fs16.hip) is selectable
     DEFAULT_LAYOUT = "split"
 
     def invalidate(self) -> None:
@@ -268,11 +268,17 @@ class MLPDenoiser:
         """Call after training that kept the working copies current (the built-in AdamW
         rewrites them every step): drops only the E tables, which the next sampling pack
         rebuilds from the trained weights; the working copies (and graphs that captured their
-        addresses) stay valid."""
+        addresses) stay valid.
+
+        Retention: the tables of the PREVIOUS generation only stay allocated, so a graph
+        captured outside ``Sampler`` on them is still safe to replay once (until the next
+        ``train``).  ``Sampler`` itself re-packs and re-captures on a ``table_gen`` change
+        before its next launch, so it never needs older tables; keeping every generation
+        pinned 4 x [T, H] fp32 per ``train`` call."""
         for dev in self._dev.values():
             old = [dev.pop(f"etab{k}") for k in range(self.n_blocks) if f"etab{k}" in dev]
-            if old:             # kept alive (ALL generations): a descriptor or a graph captured
-                dev.setdefault("_stale_etab", []).append(old)   # earlier may still point there
+            if old:
+                dev["_stale_etab"] = old      # replaces (frees) the generation before it
         self.table_gen += 1
 
     def make_stepper(self, n: int, dtype: str, device, sched_desc):
@@ -300,6 +306,9 @@ class MLPDenoiser:
             return ws
         loop.status = lambda: ops.sample_loop_status(desc, ws, n)
         loop.form = ops.sample_loop_last_form     # which kernel the last launch ran
+        # status 2 (replica placement mismatch) switches this device to the chip-wide loop
+        # inside the library, so the Sampler keeps launching the loop
+        loop.placement_fallback = True
         return loop
 
     def device_pack(self, dtype: str, device, with_tables: bool = True) -> Dict[str, object]:

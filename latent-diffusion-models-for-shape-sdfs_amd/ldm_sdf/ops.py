@@ -601,7 +601,9 @@ def unet_loop_config(spin_limit: int = 0) -> None:
 
 def unet_loop_status(ws: torch.Tensor) -> int:
     """0 when the last ``unet_loop`` on ``ws`` completed, 1 when a barrier timed out, 2 when
-    its workgroups were not placed 32 per XCD (nothing computed).  Synchronises the stream."""
+    its workgroups were not placed 64 per XCD (nothing computed), 3 when the launch's n_phase /
+    w_dtype / B / D differ from the program prepared in ``ws`` (nothing computed).
+    Synchronises the stream."""
     st = C.c_uint(0)
     capi.check(capi.load().ldm_unet_loop_status(ws.data_ptr(), C.byref(st),
                                                 capi.stream_handle(ws.device)),

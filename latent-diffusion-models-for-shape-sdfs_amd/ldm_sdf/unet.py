@@ -239,6 +239,7 @@ class UNet1DDenoiser:
             return keep
         loop.status = lambda: ops.unet_loop_status(ws)
         loop.form = lambda: "unet-replica"
+        loop.placement_fallback = False          # no chip-wide UNet loop: status 2 -> graph
         loop.ws = ws                              # (diagnostics: scripts/stamp_unet.py)
         return loop
 

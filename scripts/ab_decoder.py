@@ -13,16 +13,15 @@ from ldm_sdf import ops  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-# variants: "p<sched>" = pass8 layout with LDM_DECODER_SCHED=<sched> (needs the `make DEV=1`
-# library for sched != 4), "q" = quarter layout, "s" = split layout, "sb" = split with its
-# in-stream barriers after the second MFMA pair (LDM_FS_BP=1, dev build)
-VARIANTS = os.environ.get("AB_VARIANTS", "s,q").split(",")
-LAYOUT = {"q": "quarter", "s": "split", "sb": "split", "s16": "split16"}
+# variants: "s" = split layout, "sb" = split with its in-stream barriers after the second MFMA
+# pair (LDM_FS_BP=1, dev build), "s16" = split16 layout
+VARIANTS = os.environ.get("AB_VARIANTS", "s,s16").split(",")
+LAYOUT = {"s": "split", "sb": "split", "s16": "split16"}
 FLOPS = 3146752
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)
 for dtype in os.environ.get("AB_DTYPES", "bf16").split(","):
-    pks = {v: dec.device_pack(dtype, dev, layout=LAYOUT.get(v, "pass8")) for v in VARIANTS}
+    pks = {v: dec.device_pack(dtype, dev, layout=LAYOUT[v]) for v in VARIANTS}
     z = torch.randn(B, 256, device=dev) * 0.1
     beta = ops.decoder_fold(pks[VARIANTS[0]]["desc"], z)
     out = torch.empty(B, N, N, N, device=dev)
@@ -30,8 +29,6 @@ for dtype in os.environ.get("AB_DTYPES", "bf16").split(","):
     times = {v: [] for v in VARIANTS}
     for r in range(R + 1):
         for v in VARIANTS:
-            if v.startswith("p"):
-                os.environ["LDM_DECODER_SCHED"] = v[1:]
             if v in ("s", "sb"):
                 os.environ["LDM_FS_BP"] = "1" if v == "sb" else "0"
             e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)

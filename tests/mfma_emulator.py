@@ -1,10 +1,11 @@
 """CPU emulation of the MFMA decoder kernel's data flow (TEST INFRASTRUCTURE).
 
-Follows csrc/decoder.hip literally at the fragment level -- the packed stage blob, the
-per-shape aux stages, the B fragment built from xyz, the v_mfma_f32_32x32x16 operand/result
-lane maps (cdna_hip_programming.md §3), the accumulator -> next-B-fragment conversion with
-16-bit rounding + ReLU, the pass table and the fused fp32 final layer -- so the host packer
-(ldm_sdf/pack.py) is validated against the oracle without a GPU.  Accumulation is fp64 here,
+Follows csrc/decoder_fs.hip (split layout) and csrc/decoder_fs16.hip (split16) at the
+fragment level -- the packed per-wave weight streams, the per-shape aux fragments, the B
+fragment built from xyz, the v_mfma_f32_32x32x16 / 16x16x32 operand/result lane maps
+(cdna_hip_programming.md §3), the accumulator -> next-B-fragment conversion with 16-bit
+rounding + ReLU and the fused fp32 final layer -- so the host packer (ldm_sdf/pack.py) is
+validated against the oracle without a GPU.  Accumulation is fp64 here,
 so the result differs from the device only by fp32 summation order.
 """
 from __future__ import annotations
@@ -53,178 +54,6 @@ def acc_to_Bmats(C: np.ndarray, dt: torch.dtype):
 
 def round_dt(x, dt):
     return torch.as_tensor(x, dtype=torch.float32).to(dt).to(torch.float64).numpy()
-
-
-def aux_stage(beta_l: np.ndarray, wxyz_l: np.ndarray, pass_: int, dt) -> np.ndarray:
-    """Per-shape aux stage [8, 64, 8] (csrc aux_pack_kernel)."""
-    st = np.zeros((8, 64, 8))
-    for i in range(8):
-        f = (pass_ * 8 + i) * 32 + np.arange(32)
-        hi = round_dt(beta_l[f], dt)
-        lo = round_dt(beta_l[f] - hi, dt)
-        w = wxyz_l[f]                                            # [32, 3]
-        st[i, :32, 0:3] = round_dt(w, dt)
-        st[i, :32, 3:6] = round_dt(w, dt)
-        st[i, :32, 6] = hi
-        st[i, :32, 7] = lo
-    return st
-
-
-def emulate(packed: dict, beta: np.ndarray, xyz: np.ndarray, dtype: str) -> np.ndarray:
-    """beta [B,2,512], xyz [B,P,3] (P multiple of 32) -> sdf [B,P] (float64)."""
-    dt = torch.bfloat16 if dtype == "bf16" else torch.float16
-    blob = packed["weights"].to(torch.float64).numpy()            # [nst, 8, 64, 8]
-    wl = packed["w_last"].numpy().astype(np.float64)              # permuted [16][2][16]
-    wxyz = packed["wxyz"].numpy().astype(np.float64)
-    sw = packed["skip_width"]
-    plan = pack.stage_plan(sw)
-    S = pack.skip_pad(sw)
-    B, P, _ = xyz.shape
-    out = np.zeros((B, P))
-    # pass table (csrc Passes<S>): list of (k-steps, mode)
-    if S == 256:
-        modes = ["LO", "HI", "TMP", "MERGE", "TMP", "MERGE", "LO", "TMP", "MERGE", "TMP",
-                 "MERGE", "TMP", "MERGE", "FIN0", "FIN1"]
-    else:
-        modes = ["LO", "HI"] + ["TMP", "MERGE"] * 6 + ["FIN0", "FIN1"]
-    for b in range(B):
-        auxs = [aux_stage(beta[b, 0], wxyz[0], 0, dt), aux_stage(beta[b, 0], wxyz[0], 1, dt),
-                aux_stage(beta[b, 1], wxyz[1], 0, dt), aux_stage(beta[b, 1], wxyz[1], 1, dt)]
-        for g0 in range(0, P, 32):
-            x = xyz[b, g0:g0 + 32].astype(np.float32)
-            hi = round_dt(x, dt)
-            lo = round_dt(x.astype(np.float64) - hi, dt)
-            Baux = np.zeros((16, 32))
-            Baux[0:3] = hi.T
-            Baux[3:6] = lo.T
-            Baux[6:8] = 1.0
-            hb = [np.zeros((16, 32)) for _ in range(32)]
-            tmp = None
-            part = np.zeros(32 * 2)          # per lane (h, col)
-            si = 0
-            aux_seen = 0
-            for mode in modes:
-                C = [np.zeros((32, 32)) for _ in range(8)]
-                while True:
-                    st = plan[si]
-                    if st.per_shape:
-                        data = auxs[aux_seen]
-                        aux_seen += 1
-                    else:
-                        data = blob[si]
-                    Bm = Baux if st.ks < 0 else hb[st.ks]
-                    for i in range(8):
-                        C[i] += frag_to_A(data[i]) @ Bm
-                    si += 1
-                    if st.ks < 0:
-                        break
-                new = []
-                for i in range(8):
-                    new.extend(acc_to_Bmats(C[i], dt))
-                if mode == "LO":
-                    hb[0:16] = new
-                elif mode == "HI":
-                    hb[16:32] = new
-                elif mode == "TMP":
-                    tmp = new
-                elif mode == "MERGE":
-                    hb[16:32] = new
-                    hb[0:16] = tmp
-                else:
-                    pi = 0 if mode == "FIN0" else 1
-                    for i in range(8):
-                        mc = pi * 8 + i
-                        for h in range(2):
-                            rows = acc_rows(h)
-                            w = wl[(mc * 2 + h) * 16:(mc * 2 + h) * 16 + 16]
-                            part[h * 32:(h + 1) * 32] += (np.maximum(C[i][rows, :], 0) *
-                                                          w[:, None]).sum(0)
-            tot = part[:32] + part[32:]
-            out[b, g0:g0 + 32] = np.tanh(tot + packed["b_last"])
-    return out
-
-
-def aux_stage_quarter(beta_l: np.ndarray, wxyz_l: np.ndarray, q: int, dt) -> np.ndarray:
-    """Per-shape aux stage of the quarter layout (csrc/decoder_q.hip qaux_pack_kernel)."""
-    st = np.zeros((8, 64, 8))
-    for c in range(4):
-        f = (4 * q + c) * 32 + np.arange(32)
-        hi = round_dt(beta_l[f], dt)
-        lo = round_dt(beta_l[f] - hi, dt)
-        w = wxyz_l[f]
-        st[c, :32, 0:3] = round_dt(w, dt)
-        st[c, :32, 3:6] = round_dt(w, dt)
-        st[c, :32, 6] = hi
-        st[c, :32, 7] = lo
-    return st
-
-
-def emulate_quarter(packed: dict, beta: np.ndarray, xyz: np.ndarray, dtype: str) -> np.ndarray:
-    """Fragment-level replay of the quarter layout: per quarter, acc[c] += A(frag e*4+c) @
-    B(hb[2j+e]) over its pair-stages plus the aux stage (frags 0..3 x the xyz/one fragment);
-    the layer's new k-step 8q+2c+s is chunk c of quarter q converted (16-bit, ReLU)."""
-    dt = torch.bfloat16 if dtype == "bf16" else torch.float16
-    blob = packed["weights"].to(torch.float64).numpy()
-    wl = packed["w_last"].numpy().astype(np.float64)
-    wxyz = packed["wxyz"].numpy().astype(np.float64)
-    plan = pack.stage_plan_quarter(packed["skip_width"])
-    B, P, _ = xyz.shape
-    out = np.zeros((B, P))
-    for b in range(B):
-        auxs = [aux_stage_quarter(beta[b, 0], wxyz[0], q, dt) for q in range(4)] + \
-               [aux_stage_quarter(beta[b, 1], wxyz[1], q, dt) for q in range(4)]
-        for g0 in range(0, P, 32):
-            x = xyz[b, g0:g0 + 32].astype(np.float32)
-            hi = round_dt(x, dt)
-            lo = round_dt(x.astype(np.float64) - hi, dt)
-            Baux = np.zeros((16, 32))
-            Baux[0:3] = hi.T
-            Baux[3:6] = lo.T
-            Baux[6:8] = 1.0
-            hb = [np.zeros((16, 32)) for _ in range(32)]
-            new = {}
-            part = np.zeros(64)
-            si, aux_seen = 0, 0
-            while si < len(plan):
-                st0 = plan[si]
-                layer, q = st0.layer, st0.pass_
-                C = [np.zeros((32, 32)) for _ in range(4)]
-                while True:
-                    st = plan[si]
-                    data = auxs[aux_seen] if st.per_shape else blob[si]
-                    if st.per_shape:
-                        aux_seen += 1
-                    if st.ks < 0:
-                        for c in range(4):
-                            C[c] += frag_to_A(data[c]) @ Baux
-                    else:
-                        for e in range(2):
-                            for c in range(4):
-                                C[c] += frag_to_A(data[e * 4 + c]) @ hb[2 * st.ks + e]
-                    si += 1
-                    if st.ks < 0:
-                        break
-                if layer == 7:
-                    for c in range(4):
-                        mc = 4 * q + c
-                        for h in range(2):
-                            rows = acc_rows(h)
-                            w = wl[(mc * 2 + h) * 16:(mc * 2 + h) * 16 + 16]
-                            part[h * 32:(h + 1) * 32] += (np.maximum(C[c][rows, :], 0) *
-                                                          w[:, None]).sum(0)
-                else:
-                    for c in range(4):
-                        f0, f1 = acc_to_Bmats(C[c], dt)
-                        new[8 * q + 2 * c] = f0
-                        new[8 * q + 2 * c + 1] = f1
-                    last_q = (si >= len(plan)) or plan[si].layer != layer
-                    if last_q:
-                        for k, v in new.items():
-                            hb[k] = v
-                        new = {}
-            tot = part[:32] + part[32:]
-            out[b, g0:g0 + 32] = np.tanh(tot + packed["b_last"])
-    return out
 
 
 def split_aux_shape(beta_b: np.ndarray, wxyz: np.ndarray, skip_width: int, dt) -> np.ndarray:

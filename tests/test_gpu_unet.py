@@ -203,7 +203,7 @@ def test_unet_sampler_graph_equals_eager_bf16(dev):
 
 
 # The persistent loop (ldm_unet_loop): the same conv arithmetic per output
-# element as the per-step launches (64-position tiles instead of 16, the same contraction split
+# element as the per-step launches (32-position tiles instead of 16, the same contraction split
 # and wave-order sum), so the whole trajectory must be BIT-identical to the graph path --
 # including B > 8 (two shapes per XCD replica) and the full 1000 steps.
 @pytest.mark.parametrize("dtype,n,steps", [("bf16", 1, 1000), ("bf16", 3, 40), ("bf16", 9, 25),
@@ -241,6 +241,34 @@ def test_unet_loop_rejects_bad_program(dev):
     ws = ops.unet_loop_prepare(calls, [1] + [0] * 16 + [2], [0] * 18, dev)
     with pytest.raises(capi.LdmError, match="t_hi"):
         ops.unet_loop(ws, 18, capi.LDM_BF16, x, torch.zeros(1000, 1, 1024, device=dev), 5, 10)
+
+
+def test_unet_loop_rejects_launch_that_differs_from_program(dev):
+    """a launch whose B, n_phase or w_dtype differ from the program prepared in the
+    workspace (here at B = 1) must compute nothing and report status 3 -- before, a larger B
+    read and wrote past the program's intermediate buffers."""
+    import ldm_sdf
+    from ldm_sdf import _capi as capi, ops
+    m = ldm_sdf.UNet1DDenoiser(seed=2468)
+    sd = ldm_sdf.DDPMSchedule().device(dev)
+    dpk = m.device_pack("bf16", dev)
+    buf = m.buffers(1, dev)
+    x = torch.zeros(2, 1, 1024, device=dev)
+    calls = m.step_args(dpk, buf, x[0], 0, out=x[1], sched=sd["desc"], z=x[0])
+    ws = ops.unet_loop_prepare(calls, [1] + [0] * 16 + [2], [0] * 18, dev)
+    x4 = torch.full((2, 4, 1024), 7.0, device=dev)
+    noise4 = torch.zeros(1000, 4, 1024, device=dev)
+    for args in ((18, capi.LDM_BF16, x4, noise4),               # B 4 vs the program's 1
+                 (17, capi.LDM_BF16, x, noise4[:, :1]),         # n_phase
+                 (18, capi.LDM_F32, x, noise4[:, :1])):         # weight dtype
+        xin = args[2]
+        before = xin.clone()
+        ops.unet_loop(ws, args[0], args[1], xin, args[3].contiguous(), 999, 3)
+        assert ops.unet_loop_status(ws) == 3, args[:2]
+        assert torch.equal(xin, before)
+    # the matching launch runs
+    ops.unet_loop(ws, 18, capi.LDM_BF16, x, noise4[:, :1].contiguous(), 999, 3)
+    assert ops.unet_loop_status(ws) == 0
 
 
 def test_unet_loop_timeout_surfaces_and_falls_back(dev):
