@@ -1,4 +1,4 @@
-// Device helpers shared by the decoder kernels (decoder.hip, decoder_q.hip).  Internal.
+// Device helpers shared by the decoder kernels (decoder.hip, decoder_fs.hip, decoder_fs16.hip).
 #pragma once
 #include "ldm_internal.h"
 
@@ -93,39 +93,6 @@ __device__ __forceinline__ void acc_to_frags(const f32x16& a, u32x4& f0, u32x4& 
         f0[q] = relu2(Elem<T>::pack(a[2 * q], a[2 * q + 1]));
         f1[q] = relu2(Elem<T>::pack(a[8 + 2 * q], a[8 + 2 * q + 1]));
     }
-}
-
-// Two consecutive 1 KiB LDS-DMA pieces with one M0 save/restore.  The second piece gets its
-// own address register (an instruction offset would also move the LDS destination).
-// Two 1 KiB LDS-DMA pieces in the saddr form: global = sbase + voff (+1024), LDS = M0 (+1024)
-// + lane*16 (the instruction offset moves both sides).  One M0 write serves both pieces.  M0 is
-// not restored: the decoder kernels use M0 nowhere else (check: `make asm`, grep m0).
-__device__ __forceinline__ void glds2_saddr(const uint8_t* sbase, uint32_t voff, uint32_t lds_dst) {
-    asm volatile(
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, %1\n\t"
-        "global_load_lds_dwordx4 %0, %1 offset:1024"
-        :
-        : "v"(voff), "s"(sbase), "s"(lds_dst)
-        : "memory");
-}
-
-__device__ __forceinline__ void glds16x2(const uint8_t* gsrc, uint32_t lds_dst) {
-    unsigned keep;
-    const uint8_t* g2 = gsrc + 1024;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_add_u32 m0, %3, 0x400\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "v"(g2), "s"(lds_dst)
-        : "memory");
 }
 
 }  // namespace dec

@@ -1,7 +1,8 @@
 // Feature-split MFMA decoder (weight layout LDM_LAYOUT_SPLIT): SURVEY.md §8(a) A1+A3.
 //
-// Same math and operand maps as the quarter kernel (decoder_q.hip), a
-// different split of the work inside a workgroup (DESIGN.md §4 "split kernel"):
+// The operand maps of DESIGN.md §3 (v_mfma_f32_32x32x16, accumulator rows as the next layer's B
+// fragment) with the work inside a workgroup split by output feature (DESIGN.md §4 "split
+// kernel"; it superseded the round-1/2 pass8 and quarter kernels, removed in ABI 5):
 //   * a tile is 128 points = 4 point chunks (n) of 32, shared by the workgroup's 4 waves;
 //   * wave w owns the OUTPUT FEATURES [128w, 128w+128) of every 512-wide layer as two parts of
 //     64 rows (2 m-chunks of 32); the one-part layer 3 of DeepSDF (253 -> 256) gives each wave
@@ -12,8 +13,8 @@
 //   * each wave streams ITS OWN weight fragments (2 per k-step, 2 KiB) from L2 straight into a
 //     register ring (raw buffer loads, kFsD k-steps ahead): no LDS ring, no DMA barrier.
 //     Per k-step a wave reads 2 A fragments (L2) + 4 B fragments (LDS) for 8 MFMAs: each
-//     fragment feeds 4 (A) or 2 (B) MFMAs, where the quarter kernel read one LDS fragment per
-//     MFMA; the weight bytes per point are unchanged (each feeds the tile's 128 points).
+//     fragment feeds 4 (A) or 2 (B) MFMAs (the removed quarter kernel read one LDS fragment
+//     per MFMA); each weight byte feeds the tile's 128 points.
 //   * a part's accumulators (2 m x 4 n tiles = 128 fp32) alternate between two sets A and B,
 //     and a finished set is converted (16-bit + ReLU) straight into LDS inside a 16-step
 //     window of a LATER part, half a tile per step, between its MFMAs:
@@ -32,7 +33,7 @@
 //   * the bias (and, for layers 0 and 4, xyz + the folded latent) enters as one aux MFMA step
 //     at the START of each part (A = [wx,wy,wz,wx,wy,wz,b_hi,b_lo], B = [x_hi,y_hi,z_hi,x_lo,
 //     y_lo,z_lo,1,1]), which also zero-initialises the accumulators.
-// Barriers per tile: 3 per layer (the quarter kernel: one per 2 k-steps, ~207).
+// Barriers per tile: 3 per layer.
 #include "decoder_common.h"
 
 namespace ldm {
@@ -42,7 +43,8 @@ using namespace dec;
 // k-steps of A fragments in flight per wave (register ring depth = one 4-step stream group)
 constexpr int kFsD = 4;
 // FV (kernel variant, template): bit 0 = an in-stream barrier sits after the step's SECOND
-// MFMA pair instead of its first (dev-build A/B: LDM_FS_BP=1)
+// MFMA pair instead of its first; bit 1 = one LDS base per 4-step group (dev-build A/B:
+// LDM_FS_V=<FV>)
 constexpr int kFsDefaultV = 0;
 
 constexpr int kFsStep = 2048;                       // one wave's A fragments of one k-step
@@ -344,9 +346,13 @@ template <typename T, int EK, int K0, int BAR, int FV>
 __device__ __forceinline__ void group4(FCtx<FV>& c, f32x16 (&acc)[2][4], const f32x16 (&accY)[2][4],
                                        int p0) {
     constexpr int BP = (FV & 1) ? 2 : 1;     // MFMA pairs before the in-stream barrier
+    // FV bit 1: ONE LDS base for the group's four next positions (r * 4 KiB + n * 1 KiB fold
+    // into the ds_read immediates) instead of an address formed per step
+    const char* gbase = (FV & 2) ? lds_at(c, (p0 + 1) * 4096) : nullptr;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const u32x4* nb = reinterpret_cast<const u32x4*>(lds_at(c, (p0 + r + 1) * 4096));
+        const u32x4* nb = reinterpret_cast<const u32x4*>(
+            (FV & 2) ? gbase + r * 4096 : lds_at(c, (p0 + r + 1) * 4096));
         const u32x4 a0 = c.ring[r][0], a1 = c.ring[r][1];
         const int k = K0 + r;
         // the step's VALU (epilogue: AGPR reads, cvt, ReLU, LDS address) 2 per MFMA gap, 4 in
@@ -702,7 +708,12 @@ void launch_fs_d(const FArgs& a, bool points, hipStream_t s, int grid) {
 template <typename T, int S>
 void launch_fs(const FArgs& a, bool points, hipStream_t s, int grid) {
 #ifdef LDM_DEV_KNOBS
-    if (dev_knob("LDM_FS_BP", 0) == 1) return launch_fs_d<T, S, 1>(a, points, s, grid);
+    switch (dev_knob("LDM_FS_V", kFsDefaultV)) {
+        case 1: return launch_fs_d<T, S, 1>(a, points, s, grid);
+        case 2: return launch_fs_d<T, S, 2>(a, points, s, grid);
+        case 3: return launch_fs_d<T, S, 3>(a, points, s, grid);
+        default: break;
+    }
 #endif
     launch_fs_d<T, S, kFsDefaultV>(a, points, s, grid);
 }

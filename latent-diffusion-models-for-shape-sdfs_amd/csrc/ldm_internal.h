@@ -77,25 +77,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-// Decoder kernel geometry.  One 8 KiB "stage" = 8 MFMA A-fragments
-// (8 output m-chunks of 32 rows x one 16-wide k-step), 1 KiB each: [chunk][lane][8 elem].
+// Decoder kernel geometry.
 constexpr int kHidden = 512;
-constexpr int kStageBytes = 8192;
-constexpr int kTilePoints = 128;   // points per workgroup tile (4 waves x 32)
-
-// Number of 8 KiB stages per tile for skip width S (256 padded from 253, or 512).
-__host__ __device__ constexpr int dec_n_stages(int S) {
-    return 2 /*L0*/ + 66 /*L1*/ + 66 /*L2*/ + (S / 256) * 33 /*L3*/ + 2 * (S / 16 + 1) /*L4*/ +
-           3 * 66 /*L5-7*/;
-}
-__host__ __device__ constexpr int dec_base4(int S) { return 2 + 66 + 66 + (S / 256) * 33; }
-
-// quarter-pipelined decoder (decoder_q.hip)
-size_t decoder_q_aux_bytes(int B);
-int decoder_q_n_stages(int skip_width);
-int decoder_q_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int B, int npts,
-                  int N, int k0, float vs, float origin, float* out, void* ws, size_t ws_bytes,
-                  hipStream_t s, int num_cus);
+constexpr int kTilePoints = 128;   // points per workgroup tile (4 point chunks of 32)
 
 // feature-split decoder (decoder_fs.hip)
 size_t decoder_fs_aux_bytes(int B);

@@ -153,29 +153,86 @@ __device__ __forceinline__ float grid_c(int i, float vs, float origin) {
     return i * vs + origin;             // A1: two roundings
 }
 
-// 1. classify: block (64, 4), grid (ceil(N/64), ceil(N/4), N)
+// Every volume load below is UNCONDITIONAL, at a clamped (in-bounds) index, with the value
+// selected after: a load under a divergent branch makes the compiler wait for it before the
+// branch rejoins (one memory round trip per load), which is what the first
+// kernels of this file paid.
+
+// table of triangle counts, staged per workgroup into LDS (a divergent __constant__ lookup is a
+// vector memory round trip)
+__device__ __forceinline__ void stage_ntri(unsigned char* s_ntri) {
+    if (threadIdx.x < 64)
+        reinterpret_cast<unsigned*>(s_ntri)[threadIdx.x] =
+            reinterpret_cast<const unsigned*>(kMc.ntri)[threadIdx.x];
+}
+
+// 1. classify: one thread per "quad" = 4 consecutive points of a row (Q = ceil(N/4) quads per
+// row, rows in (k, j) order), flat over the Q * N * N quads.  Per quad it loads the 5 values
+// i0 .. i0+4 of the rows (j, k), (j+1, k), (j, k+1), (j+1, k+1) (clamped to the volume), as
+// 16-byte vectors when rows are 16-byte aligned (N % 4 == 0), and writes 4 codes.
+template <bool VEC>
 __global__ __launch_bounds__(256) void mc_classify_kernel(const float* __restrict__ vol, int N,
                                                           float iso,
                                                           unsigned short* __restrict__ code) {
-    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y, k = blockIdx.z;
-    if (i >= N || j >= N) return;
+    __shared__ unsigned char s_ntri[256];
+    stage_ntri(s_ntri);
+    const int Q = (N + 3) >> 2;
     const int64_t NN = (int64_t)N * N;
-    const int64_t p = k * NN + (int64_t)j * N + i;
-    const bool in0 = vol[p] < iso;
-    unsigned m = 0;
-    if (i + 1 < N && ((vol[p + 1] < iso) != in0)) m |= 1;
-    if (j + 1 < N && ((vol[p + N] < iso) != in0)) m |= 2;
-    if (k + 1 < N && ((vol[p + NN] < iso) != in0)) m |= 4;
-    unsigned cfg = 0, nt = 0;
-    if (i + 1 < N && j + 1 < N && k + 1 < N) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t gc = min(g, (int64_t)Q * NN - 1);      // past the end: a clamped quad
+    const int64_t row = gc / Q;
+    const int i0 = (int)(gc - row * Q) * 4, j = (int)(row % N), k = (int)(row / N);
+    const int j1 = min(j + 1, N - 1), k1 = min(k + 1, N - 1);
+    const int64_t r[4] = {k * NN + (int64_t)j * N, k * NN + (int64_t)j1 * N,
+                          k1 * NN + (int64_t)j * N, k1 * NN + (int64_t)j1 * N};
+    float v[4][5];
+    const int ic = min(i0, N - 1);
+    if (VEC && i0 + 4 <= N) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int64_t q = p + (c & 1) + ((c >> 1) & 1) * (int64_t)N + ((c >> 2) & 1) * NN;
-            cfg |= (unsigned)(vol[q] < iso) << c;
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(vol + r[q] + i0);
+            v[q][0] = a[0]; v[q][1] = a[1]; v[q][2] = a[2]; v[q][3] = a[3];
+            v[q][4] = vol[r[q] + min(i0 + 4, N - 1)];
         }
-        nt = kMc.ntri[cfg];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 5; ++u) v[q][u] = vol[r[q] + min(ic + u, N - 1)];
     }
-    code[p] = (unsigned short)(m | (nt << 3) | (cfg << 8));
+    __syncthreads();                                   // s_ntri
+    if (g != gc) return;
+    const bool jy = j + 1 < N, kz = k + 1 < N;
+    unsigned short cd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const bool ix = i0 + u + 1 < N;
+        const bool in0 = v[0][u] < iso;
+        unsigned m = 0;
+        if (ix && ((v[0][u + 1] < iso) != in0)) m |= 1;
+        if (jy && ((v[1][u] < iso) != in0)) m |= 2;
+        if (kz && ((v[2][u] < iso) != in0)) m |= 4;
+        // corner c = (c & 1, c >> 1 & 1, c >> 2 & 1): rows 0..3 = (dy, dz) = 00, 10, 01, 11
+        unsigned cfg = (unsigned)in0 | (unsigned)(v[0][u + 1] < iso) << 1 |
+                       (unsigned)(v[1][u] < iso) << 2 | (unsigned)(v[1][u + 1] < iso) << 3 |
+                       (unsigned)(v[2][u] < iso) << 4 | (unsigned)(v[2][u + 1] < iso) << 5 |
+                       (unsigned)(v[3][u] < iso) << 6 | (unsigned)(v[3][u + 1] < iso) << 7;
+        const bool cube = ix && jy && kz;
+        cfg = cube ? cfg : 0u;
+        const unsigned nt = cube ? s_ntri[cfg] : 0u;
+        cd[u] = (unsigned short)(m | (nt << 3) | (cfg << 8));
+    }
+    unsigned short* dst = code + r[0] + i0;
+    if (VEC && i0 + 4 <= N) {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 w = {(unsigned)cd[0] | (unsigned)cd[1] << 16,
+                         (unsigned)cd[2] | (unsigned)cd[3] << 16};
+        *reinterpret_cast<u32x2*>(dst) = w;
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + u < N) dst[u] = cd[u];
+    }
 }
 
 __device__ __forceinline__ int nvert_of(unsigned c) { return __popc(c & 7u); }
@@ -241,29 +298,58 @@ __global__ __launch_bounds__(256) void mc_block_sums_kernel(const unsigned short
     if (threadIdx.x == 0) bsum[blockIdx.x] = make_int2(tv, tt);
 }
 
-// 3. exclusive scan of the chunk sums (one workgroup) + totals
+// 3. exclusive scan of the chunk sums (one workgroup) + totals: thread t owns the chunks
+// [t * per, (t + 1) * per), summed serially, then ONE block scan of the 256 thread sums and a
+// second serial pass writes the offsets (the previous form ran nb / 256 block scans, each with
+// its barriers: 16 us at 256^3)
 __global__ __launch_bounds__(256) void mc_chunk_scan_kernel(const int2* __restrict__ bsum, int nb,
                                                             int2* __restrict__ boff,
                                                             int32_t* __restrict__ totals) {
     __shared__ int lds[8];
-    int cv = 0, ct = 0;
-    for (int b0 = 0; b0 < nb; b0 += 256) {
-        const int b = b0 + threadIdx.x;
-        const int2 s = b < nb ? bsum[b] : make_int2(0, 0);
-        int tv, tt;
-        const int ev = block_excl_scan(s.x, lds, &tv);
-        const int et = block_excl_scan(s.y, lds + 4, &tt);
-        if (b < nb) boff[b] = make_int2(cv + ev, ct + et);
-        cv += tv;
-        ct += tt;
+    const int per = (nb + 255) / 256;
+    const int b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
+    int sv = 0, st = 0;
+    for (int b = b0; b < b1; ++b) {
+        const int2 x = bsum[b];
+        sv += x.x;
+        st += x.y;
+    }
+    int tv, tt;
+    int cv = block_excl_scan(sv, lds, &tv);
+    int ct = block_excl_scan(st, lds + 4, &tt);
+    for (int b = b0; b < b1; ++b) {
+        const int2 x = bsum[b];
+        boff[b] = make_int2(cv, ct);
+        cv += x.x;
+        ct += x.y;
     }
     if (threadIdx.x == 0) {
-        totals[0] = cv;
-        totals[1] = ct;
+        totals[0] = tv;
+        totals[1] = tt;
     }
 }
 
-// 4. vertices + per-point first vertex index
+// The 16 volume values v[q] = vol[p0 + q + st] of this thread's points, shifted by `st`
+// (0, 1, N or N*N), clamped to the volume: four 16-byte loads when the run is aligned and
+// in bounds, else 16 scalar loads (all issued before any use).
+__device__ __forceinline__ void load_run(const float* __restrict__ vol, int64_t n, int64_t p0,
+                                         int64_t st, bool vec, float (&v)[kPer]) {
+    const int64_t b = p0 + st;
+    if (vec && b + kPer <= n) {
+#pragma unroll
+        for (int q = 0; q < kPer / 4; ++q) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(vol + b + 4 * q);
+            v[4 * q] = a[0]; v[4 * q + 1] = a[1]; v[4 * q + 2] = a[2]; v[4 * q + 3] = a[3];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) v[q] = vol[min(b + q, n - 1)];
+    }
+}
+
+// 4. vertices + per-point first vertex index.  A thread that owns vertices loads its 16
+// points' values and their +x, +y, +z neighbours up front (clamped, unconditional), then emits
+// the vertices from registers.
 __global__ __launch_bounds__(256) void mc_vertices_kernel(const float* __restrict__ vol, int N,
                                                           float iso, float vs, float origin,
                                                           const unsigned short* __restrict__ code,
@@ -282,41 +368,62 @@ __global__ __launch_bounds__(256) void mc_vertices_kernel(const float* __restric
     int off = boff[blockIdx.x].x + block_excl_scan(nv, lds, &tot);
     if (nv == 0) return;
     const int64_t p0 = (int64_t)blockIdx.x * kChunk + threadIdx.x * kPer;
+    const bool vec = (N & 3) == 0;
+    float v0[kPer], vy[kPer], vz[kPer];
+    load_run(vol, n, p0, 0, vec, v0);
+    load_run(vol, n, p0, N, vec, vy);
+    load_run(vol, n, p0, NN, vec, vz);
+    const float v16 = vol[min(p0 + kPer, n - 1)];
+    // (i, j, k) of p0, then stepped point by point
+    int i = (int)(p0 % N), j = (int)((p0 / N) % N), k = (int)(p0 / NN);
+#pragma unroll
     for (int q = 0; q < kPer; ++q) {
         const unsigned m = c[q] & 7u;
-        if (!m) continue;
-        const int64_t p = p0 + q;
-        vofs[p] = off;
-        const int i = (int)(p % N), j = (int)((p / N) % N), k = (int)(p / NN);
-        const float v0 = vol[p];
-        const float x = grid_c(i, vs, origin), y = grid_c(j, vs, origin), z = grid_c(k, vs, origin);
+        if (m) {
+            const int64_t p = p0 + q;
+            vofs[p] = off;
+            const float x = grid_c(i, vs, origin), y = grid_c(j, vs, origin);
+            const float z = grid_c(k, vs, origin);
+            const float v1s[3] = {q + 1 < kPer ? v0[q + 1] : v16, vy[q], vz[q]};
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            if (!(m & (1u << a))) continue;
-            const int64_t st = a == 0 ? 1 : (a == 1 ? (int64_t)N : NN);
-            const float v1 = vol[p + st];
-            const float t = (iso - v0) / (v1 - v0);
-            float o[3] = {x, y, z};
-            const int ia = a == 0 ? i : (a == 1 ? j : k);
-            const float c0 = o[a], c1 = grid_c(ia + 1, vs, origin);
-            const float d = c1 - c0;
-            const float td = t * d;
-            o[a] = c0 + td;
-            float* dst = verts + (int64_t)off * 3;
-            dst[0] = o[0];
-            dst[1] = o[1];
-            dst[2] = o[2];
-            ++off;
+            for (int a = 0; a < 3; ++a) {
+                if (!(m & (1u << a))) continue;
+                const float t = (iso - v0[q]) / (v1s[a] - v0[q]);
+                float o[3] = {x, y, z};
+                const int ia = a == 0 ? i : (a == 1 ? j : k);
+                const float c0 = o[a], c1 = grid_c(ia + 1, vs, origin);
+                const float d = c1 - c0;
+                const float td = t * d;
+                o[a] = c0 + td;
+                float* dst = verts + (int64_t)off * 3;
+                dst[0] = o[0];
+                dst[1] = o[1];
+                dst[2] = o[2];
+                ++off;
+            }
+        }
+        if (++i == N) {
+            i = 0;
+            if (++j == N) {
+                j = 0;
+                ++k;
+            }
         }
     }
 }
 
-// 5. triangles
+// 5. triangles.  The case table is staged into LDS; per cube with triangles every vertex id it
+// can reference (its 12 edges, owned by corners 0..6) is formed from ONE round of 14
+// independent gathers (code and vofs of the 7 owner corners), kept in LDS per thread, and the
+// triangles are read off the table.
 __global__ __launch_bounds__(256) void mc_faces_kernel(int N, const unsigned short* __restrict__ code,
                                                        const int2* __restrict__ boff,
                                                        const int32_t* __restrict__ vofs,
                                                        int32_t* __restrict__ faces) {
     __shared__ int lds[4];
+    __shared__ __attribute__((aligned(16))) signed char s_tri[256 * 16];
+    __shared__ int s_ev[12][256];
+    reinterpret_cast<u32x4*>(s_tri)[threadIdx.x] = reinterpret_cast<const u32x4*>(kMc.tri)[threadIdx.x];
     const int64_t NN = (int64_t)N * N, n = NN * N;
     unsigned c[kPer];
     load_codes(code, n, blockIdx.x, c);
@@ -324,24 +431,32 @@ __global__ __launch_bounds__(256) void mc_faces_kernel(int N, const unsigned sho
 #pragma unroll
     for (int q = 0; q < kPer; ++q) nt += ntri_of(c[q]);
     int tot;
-    int off = boff[blockIdx.x].y + block_excl_scan(nt, lds, &tot);
+    int off = boff[blockIdx.x].y + block_excl_scan(nt, lds, &tot);   // (its barriers: s_tri)
     if (nt == 0) return;
     const int64_t p0 = (int64_t)blockIdx.x * kChunk + threadIdx.x * kPer;
+    int* ev = &s_ev[0][threadIdx.x];
     for (int q = 0; q < kPer; ++q) {
         const int ntq = ntri_of(c[q]);
         if (!ntq) continue;
-        const int64_t p = p0 + q;
-        const unsigned cfg = c[q] >> 8;
+        const int64_t p = p0 + q;            // a cube with triangles: every owner is in bounds
+        unsigned oc[7];
+        int ov[7];
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+            const int64_t o = p + (s & 1) + ((s >> 1) & 1) * (int64_t)N + ((s >> 2) & 1) * NN;
+            oc[s] = code[o];
+            ov[s] = vofs[o];
+        }
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+            const int s = mc_edge_start(e), a = e >> 2;
+            ev[e * 256] = ov[s] + __popc(oc[s] & 7u & ((1u << a) - 1u));
+        }
+        const signed char* tr = s_tri + (c[q] >> 8) * 16;
         for (int t = 0; t < ntq; ++t) {
             int32_t* dst = faces + (int64_t)off * 3;
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const int e = kMc.tri[cfg][3 * t + r];
-                const int a = e >> 2, s = mc_edge_start(e);
-                const int64_t owner = p + (s & 1) + ((s >> 1) & 1) * (int64_t)N + ((s >> 2) & 1) * NN;
-                const unsigned om = code[owner] & 7u;
-                dst[r] = vofs[owner] + __popc(om & ((1u << a) - 1u));
-            }
+            for (int r = 0; r < 3; ++r) dst[r] = ev[tr[3 * t + r] * 256];
             ++off;
         }
     }
@@ -414,8 +529,14 @@ extern "C" int ldm_mc_count(const float* vol, int N, float level, void* ws, size
         const hipError_t e = hipMemsetAsync(w.code + n, 0, ((int64_t)nb * kChunk - n) * 2, st);
         LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_mc_count: memset: %s", hipGetErrorString(e));
     }
-    hipLaunchKernelGGL(mc_classify_kernel, dim3((N + 63) / 64, (N + 3) / 4, N), dim3(64, 4), 0,
-                       st, vol, N, level, w.code);
+    const int64_t quads = (int64_t)((N + 3) / 4) * N * N;
+    const dim3 cgrid((unsigned)((quads + 255) / 256));
+    if ((N & 3) == 0)
+        hipLaunchKernelGGL(mc_classify_kernel<true>, cgrid, dim3(256), 0, st, vol, N, level,
+                           w.code);
+    else
+        hipLaunchKernelGGL(mc_classify_kernel<false>, cgrid, dim3(256), 0, st, vol, N, level,
+                           w.code);
     hipLaunchKernelGGL(mc_block_sums_kernel, dim3(nb), dim3(256), 0, st, w.code, n, w.bsum);
     hipLaunchKernelGGL(mc_chunk_scan_kernel, dim3(1), dim3(256), 0, st, w.bsum, nb, w.boff,
                        counts_out);

@@ -13,10 +13,10 @@ from ldm_sdf import ops  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-# variants: "s" = split layout, "sb" = split with its in-stream barriers after the second MFMA
-# pair (LDM_FS_BP=1, dev build), "s16" = split16 layout
+# variants: "s" = split layout (default kernel), "s<V>" (V = 1..3) = split with kernel variant
+# FV = V (LDM_FS_V, needs the `make DEV=1` library: csrc/decoder_fs.hip), "s16" = split16
 VARIANTS = os.environ.get("AB_VARIANTS", "s,s16").split(",")
-LAYOUT = {"s": "split", "sb": "split", "s16": "split16"}
+LAYOUT = {"s": "split", "s1": "split", "s2": "split", "s3": "split", "s16": "split16"}
 FLOPS = 3146752
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)
@@ -29,8 +29,8 @@ for dtype in os.environ.get("AB_DTYPES", "bf16").split(","):
     times = {v: [] for v in VARIANTS}
     for r in range(R + 1):
         for v in VARIANTS:
-            if v in ("s", "sb"):
-                os.environ["LDM_FS_BP"] = "1" if v == "sb" else "0"
+            if v.startswith("s") and v != "s16":
+                os.environ["LDM_FS_V"] = v[1:] or "0"
             e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
             e0.record()
             ops.decoder_grid_fwd(pks[v]["desc"], beta, N, 0, N, out=out)
