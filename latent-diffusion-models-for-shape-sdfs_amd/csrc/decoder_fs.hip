@@ -44,8 +44,9 @@ using namespace dec;
 constexpr int kFsD = 4;
 // FV (kernel variant, template): bit 0 = an in-stream barrier sits after the step's SECOND
 // MFMA pair instead of its first; bit 1 = one LDS base per 4-step group (dev-build A/B:
-// LDM_FS_V=<FV>)
-constexpr int kFsDefaultV = 0;
+// LDM_FS_V=<FV>).  Measured and dropped: layers 2..7 as one runtime loop with every part kind
+// inlined once (74 -> 50 KB of code, 1.2 % slower: profiles/r04b/ab_decoder_v.log).
+constexpr int kFsDefaultV = 2;   // group base: +0.5 % (profiles/r04b/ab_decoder_v.log)
 
 constexpr int kFsStep = 2048;                       // one wave's A fragments of one k-step
 // activation buffer: 32 positions of 4 KiB + position 32 = the tile's aux B fragments
@@ -632,11 +633,11 @@ __global__ __launch_bounds__(256, 1) void dec_fs_kernel(FArgs a) {
 
         // ---- two-part layers 1, 2 (and 3 when 512 wide).  L1p0 folds the previous tile's
         // layer 7 part 1 into its outputs (FE_FIN1); p1 of layer l publishes with its end barrier
-        constexpr int L2P = S == 256 ? 3 : 4;
         int pi = 2;
         run_part<T, FE_FIN1, false, FV>(c, accA, accB, 32, true, false, bias(pi + 1), 0, true);
         run_part<T, FE_EARLY, true, FV>(c, accB, accA, 32, true, true, bias(pi + 2), 0, false);
         pi += 2;
+        constexpr int L2P = S == 256 ? 3 : 4;
 #pragma unroll 1
         for (int l = 2; l < L2P; ++l, pi += 2) {
             // the part after layer 3 (512 wide) is layer 4's: per-shape aux
@@ -709,8 +710,8 @@ template <typename T, int S>
 void launch_fs(const FArgs& a, bool points, hipStream_t s, int grid) {
 #ifdef LDM_DEV_KNOBS
     switch (dev_knob("LDM_FS_V", kFsDefaultV)) {
+        case 0: return launch_fs_d<T, S, 0>(a, points, s, grid);
         case 1: return launch_fs_d<T, S, 1>(a, points, s, grid);
-        case 2: return launch_fs_d<T, S, 2>(a, points, s, grid);
         case 3: return launch_fs_d<T, S, 3>(a, points, s, grid);
         default: break;
     }
