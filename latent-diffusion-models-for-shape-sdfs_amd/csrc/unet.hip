@@ -233,46 +233,66 @@ __device__ __forceinline__ void stage_x(float* xs, float* trash, KSeg& s, const 
 }
 
 // Weights: 16-byte vector loads along a packed row (4 fp32 or 8 bf16 channels per load).
+// Item it (< nitem = 16 rows x taps x cinp / EPV) -> (co, tap k, element e) of the LDS row.
+template <typename TW>
+__device__ __forceinline__ void w_item(int it, int per_row, int nvec, int& co, int& k, int& e) {
+    constexpr int EPV = 16 / sizeof(TW);
+    co = it / per_row;
+    const int r = it - co * per_row;
+    k = r / nvec;
+    e = (r - k * nvec) * EPV;
+}
+
+template <typename TW, int NB>
+__device__ __forceinline__ void w_load(u32x4 (&v)[NB], KSeg& s, KSegPlan& p, int co0, int base) {
+    constexpr int EPV = 16 / sizeof(TW);
+    const int nvec = p.cinp / EPV, per_row = s.ksize * nvec, nitem = 16 * per_row;
+    const char* W = reinterpret_cast<const char*>(s.W);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int it = base + u * 256 + (int)threadIdx.x;
+        int co, k, e;
+        w_item<TW>(it < nitem ? it : 0, per_row, nvec, co, k, e);
+        const int64_t gi = (int64_t)(co0 + co) * s.ldw + (int64_t)k * s.kstride + e;
+        v[u] = *reinterpret_cast<const u32x4*>(W + gi * (int64_t)sizeof(TW));
+    }
+}
+
+template <typename TW, int NB>
+__device__ __forceinline__ void w_store(const u32x4 (&v)[NB], float* __restrict__ ws, KSeg& s,
+                                        KSegPlan& p, int base) {
+    constexpr int EPV = 16 / sizeof(TW);
+    const int nvec = p.cinp / EPV, per_row = s.ksize * nvec, nitem = 16 * per_row;
+    const int ld = s.ksize * p.cinp + 4;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int it = base + u * 256 + (int)threadIdx.x;
+        if (it >= nitem) continue;
+        int co, k, e;
+        w_item<TW>(it, per_row, nvec, co, k, e);
+        float* d = ws + co * ld + k * p.cinp + e;
+        if constexpr (sizeof(TW) == 2) {
+            const u32x4 w = v[u];
+            *reinterpret_cast<f32x4*>(d) = f32x4{
+                __builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
+                __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
+            *reinterpret_cast<f32x4*>(d + 4) = f32x4{
+                __builtin_bit_cast(float, w[2] << 16), __builtin_bit_cast(float, w[2] & 0xffff0000u),
+                __builtin_bit_cast(float, w[3] << 16), __builtin_bit_cast(float, w[3] & 0xffff0000u)};
+        } else {
+            *reinterpret_cast<u32x4*>(d) = v[u];
+        }
+    }
+}
+
 template <typename TW, int NB>
 __device__ __forceinline__ void stage_w_nb(float* __restrict__ ws, KSeg& s, KSegPlan& p,
                                            int co0) {
-    constexpr int EPV = 16 / sizeof(TW);              // elements per 16-byte vector
-    const int tid = threadIdx.x;
-    const int nvec = p.cinp / EPV;                    // vectors per (row, tap)
-    const int per_row = s.ksize * nvec;
-    const int nitem = 16 * per_row;
-    const int ld = s.ksize * p.cinp + 4;
-    const char* W = reinterpret_cast<const char*>(s.W);
+    const int nitem = 16 * s.ksize * (p.cinp / (16 / (int)sizeof(TW)));
     for (int base = 0; base < nitem; base += 256 * NB) {
         u32x4 v[NB];
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int it = base + u * 256 + tid;
-            const int itc = it < nitem ? it : 0;
-            const int co = itc / per_row, r = itc - co * per_row;
-            const int k = r / nvec, e = (r - k * nvec) * EPV;
-            const int64_t gi = (int64_t)(co0 + co) * s.ldw + (int64_t)k * s.kstride + e;
-            v[u] = *reinterpret_cast<const u32x4*>(W + gi * (int64_t)sizeof(TW));
-        }
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int it = base + u * 256 + tid;
-            if (it >= nitem) continue;
-            const int co = it / per_row, r = it - co * per_row;
-            const int k = r / nvec, e = (r - k * nvec) * EPV;
-            float* d = ws + co * ld + k * p.cinp + e;
-            if constexpr (sizeof(TW) == 2) {
-                const u32x4 w = v[u];
-                *reinterpret_cast<f32x4*>(d) = f32x4{
-                    __builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
-                    __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
-                *reinterpret_cast<f32x4*>(d + 4) = f32x4{
-                    __builtin_bit_cast(float, w[2] << 16), __builtin_bit_cast(float, w[2] & 0xffff0000u),
-                    __builtin_bit_cast(float, w[3] << 16), __builtin_bit_cast(float, w[3] & 0xffff0000u)};
-            } else {
-                *reinterpret_cast<u32x4*>(d) = v[u];
-            }
-        }
+        w_load<TW, NB>(v, s, p, co0, base);
+        w_store<TW, NB>(v, ws, s, p, base);
     }
 }
 
@@ -313,7 +333,7 @@ template <typename TW, int TP, bool HO>
 __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
                                           const ConvIO& io, float* sm, int pos0, int co0,
                                           int b, bool w_staged = false,
-                                          uint64_t* stp = nullptr) {
+                                          uint64_t* stp = nullptr, bool stp_ext = false) {
     constexpr int NT = TP / 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c16 = lane & 15;
@@ -330,7 +350,8 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
     // The epilogue's own operands (biases, residual, x_t / noise of the DDPM step) for this
     // thread's outputs o = tid + 256 k, loaded now so their latency hides under the MFMA loop
     // (they were a dependent round trip after it).  Out-of-tile outputs read index 0 (valid)
-    // and are not stored.
+    // and are not stored.  (Issuing them before the staging instead, with each segment's
+    // weights and window in one round trip, measured 4 us per step SLOWER: DESIGN.md §9.)
     constexpr int NE = TP / 16;                      // 16 x TP outputs over 256 threads
     float e_bb[NE], e_r[NE], e_x[NE], e_z[NE];
     const bool ddpm = a.epi == LDM_CONV_EPI_DDPM;
@@ -353,37 +374,88 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
         e_z[k] = noise ? io.z[idx] : 0.f;
     }
 
-    f32x4 acc[NT];
+    // The contraction: this wave's chunks (16 channels x one tap) [c_beg, c_end), TWO at a time
+    // on two accumulator sets (chunk pairs alternate, so the MFMA chains interleave instead of
+    // each MFMA waiting out its predecessor's 40-cycle latency), the next pair's operands read
+    // from LDS before this pair's MFMAs, and the segment geometry (plan fields: scalar loads)
+    // re-read only when a segment changes -- the loop read them per chunk and waited on every
+    // LDS read (the MFMA phase was ~25 % of the step).  The two sets are
+    // added at the end, so per output the sum order is fixed (graph == loop, bit for bit).
+    f32x4 acc0[NT], acc1[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NT; ++t) {
+        acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     const int c_beg = pl.nchunks * wave / 4, c_end = pl.nchunks * (wave + 1) / 4;
-    // walk this wave's chunks with carried (segment, tap, channel group) counters
+    // chunk iterator: (segment, tap, channel group) with the lane's operand offsets (floats)
     int si = 0;
     while (si + 1 < a.n_seg && c_beg >= pl.s[si + 1].ch0) ++si;
-    int ng = pl.s[si].cinp >> 4;
-    int q = c_beg - pl.s[si].ch0;
-    int k = 0;
-    while (q >= ng) { q -= ng; ++k; }
-    int cg = q;
-    for (int ch = c_beg; ch < c_end; ++ch) {
-        KSegPlan& p = pl.s[si];
-        const int ks = a.seg[si].ksize, st = a.seg[si].stride;
-        const f32x4 av = *reinterpret_cast<const f32x4*>(
-            sm + p.woff + c16 * (ks * p.cinp + 4) + k * p.cinp + cg * 16 + 4 * g);
+    int ng = 0, ks = 0, st = 0, cinp = 0, wrow = 0, xbase = 0, k = 0, cg = 0;
+    auto set_seg = [&](int s_) {
+        KSegPlan& p = pl.s[s_];
+        cinp = p.cinp;
+        ng = cinp >> 4;
+        ks = a.seg[s_].ksize;
+        st = a.seg[s_].stride;
+        wrow = p.woff + c16 * (ks * cinp + 4) + 4 * g;
+        xbase = p.xoff + 4 * g;
+    };
+    set_seg(si);
+    {
+        int q = c_beg - pl.s[si].ch0;
+        while (q >= ng) { q -= ng; ++k; }
+        cg = q;
+    }
+    auto load_chunk = [&](f32x4& av, f32x4 (&bv)[NT]) {
+        av = *reinterpret_cast<const f32x4*>(sm + wrow + k * cinp + cg * 16);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int j = (t * 16 + c16) * st + k;
-            const f32x4 bv = *reinterpret_cast<const f32x4*>(
-                sm + p.xoff + j * (p.cinp + 4) + cg * 16 + 4 * g);
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc[t], 0, 0, 0);
-        }
+        for (int t = 0; t < NT; ++t)
+            bv[t] = *reinterpret_cast<const f32x4*>(
+                sm + xbase + ((t * 16 + c16) * st + k) * (cinp + 4) + cg * 16);
         if (++cg == ng) {
             cg = 0;
-            if (++k == ks && si + 1 < a.n_seg) { k = 0; ++si; ng = pl.s[si].cinp >> 4; }
+            if (++k == ks && si + 1 < a.n_seg) {
+                k = 0;
+                set_seg(++si);
+            }
         }
+    };
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 a0 = z4, a1 = z4, b0[NT], b1[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b0[t] = b1[t] = z4;
+    bool h0 = c_beg < c_end, h1 = c_beg + 1 < c_end;
+    if (h0) load_chunk(a0, b0);
+    if (h1) load_chunk(a1, b1);
+    for (int ch = c_beg; h0; ch += 2) {
+        // the next pair first (its LDS latency hides under this pair's MFMAs); a missing
+        // second chunk is all zeros: its MFMAs add exact zeros
+        f32x4 n0 = z4, n1 = z4, m0[NT], m1[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) m0[t] = m1[t] = z4;
+        const bool g0 = ch + 2 < c_end, g1 = ch + 3 < c_end;
+        if (g0) load_chunk(n0, m0);
+        if (g1) load_chunk(n1, m1);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                acc0[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[m], b0[t][m], acc0[t], 0, 0, 0);
+                acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[m], b1[t][m], acc1[t], 0, 0, 0);
+            }
+        a0 = n0;
+        a1 = n1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            b0[t] = m0[t];
+            b1[t] = m1[t];
+        }
+        h0 = g0;
     }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = acc0[t] + acc1[t];
     __syncthreads();                    // every wave is done reading the staged operands
     if (UNET_STAMP && stp && threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
     float* red = sm;                    // [wave][t][reg][lane]
@@ -392,6 +464,7 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
 #pragma unroll
         for (int i = 0; i < 4; ++i) red[((wave * NT + t) * 4 + i) * 64 + lane] = acc[t][i];
     __syncthreads();
+    if (UNET_STAMP && stp && stp_ext && threadIdx.x == 0) stp[6] = __builtin_amdgcn_s_memrealtime();
 
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
@@ -411,6 +484,10 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
             y = ddpm_update(e_x[k], pre, e_z[k], a.c1[io.t], a.c2[io.t], a.sigma[io.t], noise);
         io.Y[idx] = y;
     }
+    if (UNET_STAMP && stp && stp_ext && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stp[7] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 struct ConvKArgs {
@@ -418,12 +495,29 @@ struct ConvKArgs {
     ConvPlan pl;
 };
 
+#if UNET_STAMP
+// diagnostic build: workgroup (0, 0, 0) of every ldm_conv1d launch stamps entry, staging done,
+// MFMA done, reduction done and stores drained into a ring of 256 launches (ldm_dev_conv_stamps)
+__device__ uint64_t g_conv_stamp[256][8];
+__device__ unsigned g_conv_stamp_n;
+#endif
+
 template <typename TW, int TP>
 __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const LDM_KC ConvKArgs* k = (const LDM_KC ConvKArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    uint64_t* stp = nullptr;
+#if UNET_STAMP
+    // thread 0 alone writes stamps (conv_tile checks), so only it needs the slot; no static LDS
+    // (the dynamic allocation is the whole 160 KiB)
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        stp = g_conv_stamp[atomicAdd(&g_conv_stamp_n, 1u) & 255u];
+        stp[0] = t0;
+    }
+#endif
     conv_tile<TW, TP, false>(k->a, k->pl, conv_io(k->a), sm, blockIdx.x * TP, blockIdx.y * 16,
-                             blockIdx.z);
+                             blockIdx.z, false, stp, true);
 }
 
 constexpr int kMaxLdsBytes = 160 * 1024;
@@ -690,6 +784,17 @@ extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
     if (a->w_dtype == LDM_BF16) return launch_conv<unsigned short>(*a, (hipStream_t)s);
     return launch_conv<float>(*a, (hipStream_t)s);
 }
+
+#if UNET_STAMP
+// diagnostic build only: the conv stamp ring (256 x 8 s_memrealtime values) and its counter
+extern "C" int ldm_dev_conv_stamps(uint64_t* host, unsigned* n) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ldm::g_conv_stamp), sizeof(ldm::g_conv_stamp)) !=
+            hipSuccess ||
+        hipMemcpyFromSymbol(n, HIP_SYMBOL(ldm::g_conv_stamp_n), sizeof(unsigned)) != hipSuccess)
+        return -1;
+    return 0;
+}
+#endif
 
 extern "C" size_t ldm_unet_loop_ws_bytes(int n_phase) {
     if (n_phase < 1 || n_phase > LDM_UNET_MAX_PHASES) return 0;

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-4 GPU batch 3: per-phase stamps of the UNet step's 18 ldm_conv1d launches (graph path).
+set -e
+O=$GRAFT_REPO_ROOT/gpurun_out/r04c
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+LIB=$GRAFT_REPO_ROOT/latent-diffusion-models-for-shape-sdfs_amd/ldm_sdf/libldm_stamp.so
+LDM_SDF_LIB=$LIB timeout -k 10 120 python -u scripts/stamp_conv.py 1 > $O/stamp_conv_b1.log 2>&1
+LDM_SDF_LIB=$LIB timeout -k 10 120 python -u scripts/stamp_conv.py 8 > $O/stamp_conv_b8.log 2>&1
+echo batch3 done
