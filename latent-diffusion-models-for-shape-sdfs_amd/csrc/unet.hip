@@ -59,11 +59,17 @@ struct SegPlan {
     int xoff;   // LDS float offset of the window  [win][cinp + 4]
     int woff;   // LDS float offset of the weights [16][ksize * cinp + 4]
     int ch0;    // first contraction chunk (16 channels x one tap) of this segment
+    // the launch kernel's direct staging (fast_* below; make_plan): every index a shift or mask
+    int lgv;    // log2 of the 16-byte weight vectors per (row, tap): cinp / (16 / sizeof(TW))
+    int nw;     // weight vectors of the tile: 16 rows x ksize taps x (1 << lgv)
+    int lgng;   // log2 of the 4-position source groups staged per channel (>= the window's)
+    int nx;     // window items (4 channels x 4 positions each): cinp / 4 << lgng
 };
 struct ConvPlan {
     SegPlan s[LDM_CONV_MAX_SEGS];
     int nchunks;
-    int lds_floats;   // including 4 scratch floats at the end (stores of out-of-range slots)
+    int lds_floats;
+    int fast;         // every segment fits the direct staging (make_plan)
 };
 
 // The device code reads a call's arguments and plan through the CONSTANT address space (the
@@ -77,8 +83,9 @@ typedef const LDM_KC SegPlan KSegPlan;
 typedef const LDM_KC ConvPlan KPlan;
 
 // Staging issues every load of a segment before the first LDS store (one global round trip),
-// branch-free: out-of-range slots load a clamped in-bounds address and select 0, and store
-// to a scratch word past the operands.  The slot count NB is picked per segment from the
+// branch-free: out-of-range slots load a clamped in-bounds address and select 0; their stores
+// are skipped (exec-masked: a store needs no wait where the branch rejoins, and a common scratch
+// address made the idle lanes' stores one LDS bank-conflict chain).  The slot count NB is picked per segment from the
 // real item count (4 / 8 / 16 / 32), so a small segment does not pay a 32-slot unroll.
 // HO (hand-off): the input was written by another workgroup of the same launch (the
 // persistent loop): every load of it is an sc1 (L1-bypassing) load, loop_sync.h's rule.
@@ -109,7 +116,7 @@ __device__ __forceinline__ float silu_stage(float x) {
 // (one global round trip per pass), branch-free (clamped address + select).  Channels
 // C..cinp-1 and positions outside [0, Lsrc) stage zeros.
 template <int NB, bool HO>
-__device__ __forceinline__ void stage_x_nb(float* __restrict__ xs, float* __restrict__ trash,
+__device__ __forceinline__ void stage_x_nb(float* __restrict__ xs,
                                            KSeg& s, const float* Xs, KSegPlan& p, int b,
                                            int pos0) {
     const int tid = threadIdx.x;
@@ -144,9 +151,9 @@ __device__ __forceinline__ void stage_x_nb(float* __restrict__ xs, float* __rest
         }
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
-            float* d = dst[u] >= 0 ? xs + dst[u] : trash;
+            if (dst[u] < 0) continue;        // exec-masked store (see fast_w_store)
             const float x = (okm >> u) & 1 ? v[u] : 0.f;
-            *d = act ? silu_stage(x) : x;
+            xs[dst[u]] = act ? silu_stage(x) : x;
         }
     }
 }
@@ -159,7 +166,7 @@ __device__ __forceinline__ void stage_x_nb(float* __restrict__ xs, float* __rest
 // [0, L_in) are masked per element.  UP2 writes every source element to its two window
 // positions.  HO: sc1 loads (cache policy 16), L1-bypassing like ld_act.
 template <int NB, bool HO>
-__device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs, float* __restrict__ trash,
+__device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs,
                                                KSeg& s, const float* Xs, KSegPlan& p, int b,
                                                int pos0) {
     const int tid = threadIdx.x;
@@ -205,8 +212,7 @@ __device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs, float* __
                     if (r == 1 && !up2) break;
                     const int j = (up2 ? 2 * sp + r : sp) - pstart;
                     const bool in = cg[u] >= 0 && (unsigned)j < (unsigned)win;
-                    float* d = in ? xs + j * ld + pc : trash;
-                    *d = y;
+                    if (in) xs[j * ld + pc] = y;   // exec-masked store (see fast_w_store)
                 }
             }
         }
@@ -214,22 +220,22 @@ __device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs, float* __
 }
 
 template <bool HO>
-__device__ __forceinline__ void stage_x(float* xs, float* trash, KSeg& s, const float* X,
+__device__ __forceinline__ void stage_x(float* xs, KSeg& s, const float* X,
                                         KSegPlan& p, int b, int pos0) {
     if ((s.L_in & 3) == 0 && ((uintptr_t)X & 15) == 0) {
         const int ng = (p.win + 6) / 4 + 2;               // bound of the source groups per row
         const int n = (p.cinp * ng + 255) / 256;
-        if (n <= 2) stage_x_vec_nb<2, HO>(xs, trash, s, X, p, b, pos0);
-        else if (n <= 5) stage_x_vec_nb<5, HO>(xs, trash, s, X, p, b, pos0);
-        else if (n <= 10) stage_x_vec_nb<10, HO>(xs, trash, s, X, p, b, pos0);
-        else stage_x_vec_nb<18, HO>(xs, trash, s, X, p, b, pos0);
+        if (n <= 2) stage_x_vec_nb<2, HO>(xs, s, X, p, b, pos0);
+        else if (n <= 5) stage_x_vec_nb<5, HO>(xs, s, X, p, b, pos0);
+        else if (n <= 10) stage_x_vec_nb<10, HO>(xs, s, X, p, b, pos0);
+        else stage_x_vec_nb<18, HO>(xs, s, X, p, b, pos0);
         return;
     }
     const int n = (p.cinp * p.win + 255) / 256;      // items per thread
-    if (n <= 4) stage_x_nb<4, HO>(xs, trash, s, X, p, b, pos0);
-    else if (n <= 9) stage_x_nb<9, HO>(xs, trash, s, X, p, b, pos0);
-    else if (n <= 17) stage_x_nb<17, HO>(xs, trash, s, X, p, b, pos0);
-    else stage_x_nb<34, HO>(xs, trash, s, X, p, b, pos0);
+    if (n <= 4) stage_x_nb<4, HO>(xs, s, X, p, b, pos0);
+    else if (n <= 9) stage_x_nb<9, HO>(xs, s, X, p, b, pos0);
+    else if (n <= 17) stage_x_nb<17, HO>(xs, s, X, p, b, pos0);
+    else stage_x_nb<34, HO>(xs, s, X, p, b, pos0);
 }
 
 // Weights: 16-byte vector loads along a packed row (4 fp32 or 8 bf16 channels per load).
@@ -322,57 +328,80 @@ __device__ __forceinline__ ConvIO conv_io(KConv& a) {
     return {a.seg[0].X, a.cbias, a.Y, a.xlat, a.z, a.t};
 }
 
-// One output tile (16 channels x TP positions of shape b) of a conv call: stage every
-// segment's input window and weights in LDS (one global round trip), the MFMA contraction
-// split over the 4 waves, the partial tiles summed in wave order, the fused epilogue.
-// HO: the loop's hand-off form (sc1 loads of activations written inside the launch).
-// w_staged: the weights of this (call, co0) already sit in LDS (the loop prefetches them).
-// Ends with every LDS read done by its own wave only: a caller running another tile on the
-// same LDS first passes a workgroup barrier.
-template <typename TW, int TP, bool HO>
-__device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
-                                          const ConvIO& io, float* sm, int pos0, int co0,
-                                          int b, bool w_staged = false,
-                                          uint64_t* stp = nullptr, bool stp_ext = false) {
-    constexpr int NT = TP / 16;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int g = lane >> 4, c16 = lane & 15;
-
-    float* trash = sm + pl.lds_floats - 4;
-    for (int si = 0; si < a.n_seg; ++si) {
-        if (!w_staged) stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
-        stage_x<HO>(sm + pl.s[si].xoff, trash, a.seg[si], si == 0 ? io.x0 : a.seg[si].X,
-                    pl.s[si], b, pos0);
+// Diagnostic stamps (UNET_STAMP builds only; every mark compiles away otherwise).  StampPtr
+// writes s_memrealtime into the loop's debug tail as it goes (marks 1 and 2; 6 and 7 with ext);
+// StampRegs keeps the launch kernel's marks in registers and writes them at the kernel's end,
+// so the slot's atomic and the stores stay out of the timed path.
+struct StampPtr {
+    uint64_t* p;
+    bool ext;
+    __device__ __forceinline__ void mark(int k) {
+        if (UNET_STAMP && p && threadIdx.x == 0 && (ext || k <= 2))
+            p[k] = __builtin_amdgcn_s_memrealtime();
     }
-    __syncthreads();
-    if (UNET_STAMP && stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
+};
+struct StampRegs {
+    bool on;
+    uint64_t t[8];
+    __device__ __forceinline__ void mark(int k) {
+        if (UNET_STAMP && on) t[k] = __builtin_amdgcn_s_memrealtime();
+    }
+};
 
-    // The epilogue's own operands (biases, residual, x_t / noise of the DDPM step) for this
-    // thread's outputs o = tid + 256 k, loaded now so their latency hides under the MFMA loop
-    // (they were a dependent round trip after it).  Out-of-tile outputs read index 0 (valid)
-    // and are not stored.  (Issuing them before the staging instead, with each segment's
-    // weights and window in one round trip, measured 4 us per step SLOWER: DESIGN.md §9.)
-    constexpr int NE = TP / 16;                      // 16 x TP outputs over 256 threads
-    float e_bb[NE], e_r[NE], e_x[NE], e_z[NE];
+// The epilogue's own operands (biases, residual, x_t / noise of the DDPM step, the step's
+// schedule coefficients) for thread tid's outputs o = tid + 256 k of the tile, ISSUED early so
+// their latency hides under other work and consumed only in conv_finish: every load is
+// unconditional (an absent operand reads a valid dummy address and is zeroed there), because a
+// load under a branch, or a sum right after the loads, made the compiler wait for every load in
+// flight (vmcnt(0)) -- three serial round trips in the launch kernel's staging.
+// Out-of-tile outputs read index 0 (valid) and are not stored.
+template <int TP>
+struct EpiOps {
+    static constexpr int NE = TP / 16;           // 16 x TP outputs over 256 threads
+    float b1[NE], b2[NE], b3[NE], r[NE], x[NE], z[NE];
+    float c1, c2, sg;
+};
+
+template <int TP, bool HO>
+__device__ __forceinline__ void epi_load(EpiOps<TP>& e, KConv& a, const ConvIO& io, int pos0,
+                                         int co0, int b) {
+    const int tid = threadIdx.x;
     const bool ddpm = a.epi == LDM_CONV_EPI_DDPM;
     const bool noise = ddpm && io.t > 0;
+    const float* dummy = a.seg[0].X;             // any valid address
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {
+    for (int k = 0; k < EpiOps<TP>::NE; ++k) {
         const int o = tid + 256 * k;
         const int r = o / TP, pc = o % TP;
         const int co = co0 + r, l = pos0 + pc;
         const bool ok = co < a.Cout && l < a.L_out;
         const int coc = ok ? co : 0;
         const int64_t idx = ok ? ((int64_t)b * a.Cout + co) * a.L_out + l : 0;
-        float bb = 0.f;                              // the per-launch kernel's summation order
-        if (a.bias) bb += a.bias[coc];
-        if (a.bias2) bb += a.bias2[coc];
-        if (io.cbias) bb += io.cbias[(int64_t)b * a.scb + coc];
-        e_bb[k] = bb;
-        e_r[k] = a.R ? ld_act<HO>(a.R + idx) : 0.f;
-        e_x[k] = ddpm ? ld_act<HO>(io.xlat + idx) : 0.f;
-        e_z[k] = noise ? io.z[idx] : 0.f;
+        e.b1[k] = *(a.bias ? a.bias + coc : dummy);
+        e.b2[k] = *(a.bias2 ? a.bias2 + coc : dummy);
+        e.b3[k] = *(io.cbias ? io.cbias + (int64_t)b * a.scb + coc : dummy);
+        e.r[k] = ld_act<HO>(a.R ? a.R + idx : dummy);
+        e.x[k] = ld_act<HO>(ddpm ? io.xlat + idx : dummy);
+        e.z[k] = *(noise ? io.z + idx : dummy);
     }
+    e.c1 = *(ddpm ? a.c1 + io.t : dummy);
+    e.c2 = *(ddpm ? a.c2 + io.t : dummy);
+    e.sg = *(ddpm ? a.sigma + io.t : dummy);
+}
+
+// The tile after its operands are staged (and the staging barrier passed): the MFMA
+// contraction split over the 4 waves, the partial tiles summed in wave order, the fused
+// epilogue.  Ends with every LDS read done by its own wave only: a caller running another tile
+// on the same LDS first passes a workgroup barrier.
+template <typename TW, int TP, typename ST>
+__device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& io, float* sm,
+                                            int pos0, int co0, int b, const EpiOps<TP>& e,
+                                            ST& st_) {
+    constexpr int NT = TP / 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4, c16 = lane & 15;
+    const bool ddpm = a.epi == LDM_CONV_EPI_DDPM;
+    const bool noise = ddpm && io.t > 0;
 
     // The contraction: this wave's chunks (16 channels x one tap) [c_beg, c_end), TWO at a time
     // on two accumulator sets (chunk pairs alternate, so the MFMA chains interleave instead of
@@ -457,17 +486,17 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = acc0[t] + acc1[t];
     __syncthreads();                    // every wave is done reading the staged operands
-    if (UNET_STAMP && stp && threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
+    st_.mark(2);
     float* red = sm;                    // [wave][t][reg][lane]
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) red[((wave * NT + t) * 4 + i) * 64 + lane] = acc[t][i];
     __syncthreads();
-    if (UNET_STAMP && stp && stp_ext && threadIdx.x == 0) stp[6] = __builtin_amdgcn_s_memrealtime();
+    st_.mark(6);
 
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {
+    for (int k = 0; k < EpiOps<TP>::NE; ++k) {
         const int o = tid + 256 * k;
         const int r = o / TP, pc = o % TP;
         const int co = co0 + r, l = pos0 + pc;
@@ -477,16 +506,174 @@ __device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
 #pragma unroll
         for (int w = 0; w < 4; ++w) v += red[((w * NT + t) * 4 + i) * 64 + ln];
         const int64_t idx = ((int64_t)b * a.Cout + co) * a.L_out + l;
-        float pre = v + e_bb[k];
-        if (a.R) pre += e_r[k];
+        float bb = 0.f;                              // the summation order of every path
+        if (a.bias) bb += e.b1[k];
+        if (a.bias2) bb += e.b2[k];
+        if (io.cbias) bb += e.b3[k];
+        float pre = v + bb;
+        if (a.R) pre += e.r[k];
         float y = pre;
-        if (ddpm)
-            y = ddpm_update(e_x[k], pre, e_z[k], a.c1[io.t], a.c2[io.t], a.sigma[io.t], noise);
+        if (ddpm) y = ddpm_update(e.x[k], pre, noise ? e.z[k] : 0.f, e.c1, e.c2, e.sg, noise);
         io.Y[idx] = y;
     }
-    if (UNET_STAMP && stp && stp_ext && threadIdx.x == 0) {
+    if (UNET_STAMP) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stp[7] = __builtin_amdgcn_s_memrealtime();
+        st_.mark(7);
+    }
+}
+
+// One output tile (16 channels x TP positions of shape b) of a conv call, the persistent
+// loop's form: stage every segment's input window and weights in LDS (stage_w / stage_x: one
+// round trip per part), the epilogue operands behind the staging barrier, then conv_finish.
+// HO: the loop's hand-off form (sc1 loads of activations written inside the launch).
+// w_staged: the weights of this (call, co0) already sit in LDS (the loop prefetches them).
+template <typename TW, int TP, bool HO>
+__device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
+                                          const ConvIO& io, float* sm, int pos0, int co0,
+                                          int b, bool w_staged = false,
+                                          uint64_t* stp = nullptr, bool stp_ext = false) {
+    for (int si = 0; si < a.n_seg; ++si) {
+        if (!w_staged) stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
+        stage_x<HO>(sm + pl.s[si].xoff, a.seg[si], si == 0 ? io.x0 : a.seg[si].X,
+                    pl.s[si], b, pos0);
+    }
+    __syncthreads();
+    StampPtr sp{stp, stp_ext};
+    sp.mark(1);
+    EpiOps<TP> e;
+    epi_load<TP, HO>(e, a, io, pos0, co0, b);
+    conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sp);
+}
+
+// ---- direct staging: the ldm_conv1d launch kernel -----------------
+// A launch is latency-bound: the generic staging above spent ~45 VALU (two integer divisions,
+// 64-bit address arithmetic) per 16-byte weight vector and per-element index arithmetic on
+// the window, at one wave per SIMD, before and after ONE round trip per part (segment weights,
+// segment window): 1.0-2.3 us per part in the stamps (profiles/r04f/stamp_conv_b1_fine.log).
+// Here make_plan has checked that every count is a power of two, so an item's indices are
+// shifts and masks of its number, the loads are raw buffer loads at 32-bit offsets, and every
+// segment's weights and window are ISSUED before any LDS store (one round trip for the whole
+// tile, the epilogue operands in flight under the stores).  The LDS image is the generic
+// staging's, value for value (same SiLU), so the contraction and the results are unchanged.
+//   weights: item i -> vector v = i & (nvec - 1) of row co = (i >> lgv) & 15, tap k = i >>
+//            (lgv + 4): 16 bytes of the packed row (co0 + co, k), stored (fp32) at
+//            woff + co (ksize cinp + 4) + k cinp + v EPV;
+//   window:  item i -> source group gi = i & (NG - 1) (4 aligned positions a0 + 4 gi), channel
+//            quad q = i >> lgng = 4 cg + g: the 4 channels 16 cg + g + 4 m (m = 0..3), i.e. the
+//            4 consecutive perm16 columns 4 q.  Four 16-byte loads (one per channel), stored as
+//            one 16-byte LDS vector per position (4 channels): 4 (8 for UP2) stores per item.
+//            Rows L_in % 4 == 0, so a group lies wholly inside or outside [0, L_in): one test.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                             0x00020000);
+}
+
+template <typename TW, int NBW>
+__device__ __forceinline__ void fast_w_issue(u32x4 (&v)[NBW], KSeg& s, KSegPlan& p, int co0,
+                                             int base) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(s.W, 0x7ffffff0u);
+    const int lgv = p.lgv, nw = p.nw;
+    const uint32_t ldw_b = (uint32_t)s.ldw * sizeof(TW), kst_b = (uint32_t)s.kstride * sizeof(TW);
+#pragma unroll
+    for (int u = 0; u < NBW; ++u) {
+        const int i = base + u * 256 + (int)threadIdx.x;
+        const uint32_t vv = i & ((1 << lgv) - 1), co = (i >> lgv) & 15, k = i >> (lgv + 4);
+        uint32_t off = (uint32_t)(co0 + co) * ldw_b + k * kst_b + vv * 16u;
+        off = i < nw ? off : 0xfffffff0u;          // absent item: out of range, no memory access
+        v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+}
+
+// Stores of absent items are skipped (exec-masked; a store needs no wait at the join): a common
+// scratch address instead made every idle lane of a small conv write the same 16 bytes, one LDS
+// bank conflict chain per instruction (~2 us per launch, profiles/r04g).
+template <typename TW, int NBW>
+__device__ __forceinline__ void fast_w_store(const u32x4 (&v)[NBW], float* sm, KSeg& s,
+                                             KSegPlan& p, int base) {
+    constexpr int EPV = 16 / sizeof(TW);
+    const int lgv = p.lgv, nw = p.nw, cinp = p.cinp, wld = s.ksize * cinp + 4;
+    float* ws = sm + p.woff;
+#pragma unroll
+    for (int u = 0; u < NBW; ++u) {
+        const int i = base + u * 256 + (int)threadIdx.x;
+        if (i >= nw) continue;
+        const int vv = i & ((1 << lgv) - 1), co = (i >> lgv) & 15, k = i >> (lgv + 4);
+        float* d = ws + co * wld + k * cinp + vv * EPV;
+        if constexpr (sizeof(TW) == 2) {
+            const u32x4 w = v[u];
+            *reinterpret_cast<f32x4*>(d) = f32x4{
+                __builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
+                __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
+            *reinterpret_cast<f32x4*>(d + 4) = f32x4{
+                __builtin_bit_cast(float, w[2] << 16), __builtin_bit_cast(float, w[2] & 0xffff0000u),
+                __builtin_bit_cast(float, w[3] << 16), __builtin_bit_cast(float, w[3] & 0xffff0000u)};
+        } else {
+            *reinterpret_cast<u32x4*>(d) = v[u];
+        }
+    }
+}
+
+// the window's source origin: a0 = the aligned group start at or below the first source
+// position (UP2: positions of the upsampled row map to source p >> 1)
+__device__ __forceinline__ int fast_x_a0(KSeg& s, int pos0) {
+    const int pstart = pos0 * s.stride - s.pad;
+    const int s0 = s.mode == LDM_CONV_UP2 ? (pstart >> 1) : pstart;   // floor (arithmetic shift)
+    return s0 & ~3;
+}
+
+template <int NBX>
+__device__ __forceinline__ void fast_x_issue(f32x4 (&v)[NBX][4], KSeg& s, KSegPlan& p,
+                                             const float* X, int b, int pos0, int base) {
+    const int L_in = s.L_in, lgng = p.lgng, nx = p.nx;
+    const __amdgpu_buffer_rsrc_t rs =
+        rsrc(X + (int64_t)b * s.C * L_in, (uint32_t)s.C * (uint32_t)L_in * 4u);
+    const int a0 = fast_x_a0(s, pos0);
+#pragma unroll
+    for (int u = 0; u < NBX; ++u) {
+        const int i = base + u * 256 + (int)threadIdx.x;
+        const int gi = i & ((1 << lgng) - 1), q = i >> lgng;
+        const int row0 = 16 * (q >> 2) + (q & 3);
+        // channels >= C lie past the buffer's end and read 0; a group left of position 0 reads
+        // the previous row (or nothing: negative offsets wrap past the end) and is masked; an
+        // absent item reads out of range (no memory access)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            uint32_t off = (uint32_t)(((row0 + 4 * m) * L_in + a0 + 4 * gi) * 4);
+            off = i < nx ? off : 0xfffffff0u;
+            v[u][m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        }
+    }
+}
+
+template <int NBX>
+__device__ __forceinline__ void fast_x_store(const f32x4 (&v)[NBX][4], float* sm, KSeg& s,
+                                             KSegPlan& p, int pos0, int base) {
+    const bool up2 = s.mode == LDM_CONV_UP2, act = s.silu_in != 0;
+    const int L_in = s.L_in, lgng = p.lgng, nx = p.nx, win = p.win, ldx = p.cinp + 4;
+    const int pstart = pos0 * s.stride - s.pad;
+    const int a0 = fast_x_a0(s, pos0);
+    float* xs = sm + p.xoff;
+#pragma unroll
+    for (int u = 0; u < NBX; ++u) {
+        const int i = base + u * 256 + (int)threadIdx.x;
+        const int gi = i & ((1 << lgng) - 1), q = i >> lgng;
+        const int sp0 = a0 + 4 * gi;
+        if (i >= nx) continue;
+        const bool inb = sp0 >= 0 && sp0 < L_in;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            f32x4 x = {v[u][0][e], v[u][1][e], v[u][2][e], v[u][3][e]};
+            if (!inb) x = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (act)
+                x = f32x4{silu_stage(x[0]), silu_stage(x[1]), silu_stage(x[2]), silu_stage(x[3])};
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                if (r == 1 && !up2) break;
+                const int j = (up2 ? 2 * (sp0 + e) + r : sp0 + e) - pstart;
+                if ((unsigned)j < (unsigned)win)
+                    *reinterpret_cast<f32x4*>(xs + j * ldx + 4 * q) = x;
+            }
+        }
     }
 }
 
@@ -502,28 +689,125 @@ __device__ uint64_t g_conv_stamp[256][8];
 __device__ unsigned g_conv_stamp_n;
 #endif
 
+#if UNET_STAMP
+__device__ __forceinline__ void stamps_flush(const StampRegs& sr) {
+    if (!sr.on) return;
+    uint64_t* p = g_conv_stamp[atomicAdd(&g_conv_stamp_n, 1u) & 255u];
+    for (int i = 0; i < 8; ++i) p[i] = sr.t[i];
+}
+#endif
+
+// The generic launch kernel: conv_tile's staging (any channel count / alignment).
 template <typename TW, int TP>
 __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const LDM_KC ConvKArgs* k = (const LDM_KC ConvKArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    uint64_t* stp = nullptr;
-#if UNET_STAMP
-    // thread 0 alone writes stamps (conv_tile checks), so only it needs the slot; no static LDS
-    // (the dynamic allocation is the whole 160 KiB)
-    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        stp = g_conv_stamp[atomicAdd(&g_conv_stamp_n, 1u) & 255u];
-        stp[0] = t0;
+    KConv& a = k->a;
+    KPlan& pl = k->pl;
+    StampRegs sr;
+    sr.on = UNET_STAMP && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 &&
+            threadIdx.x == 0;
+    sr.mark(0);
+    const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
+    const ConvIO io = conv_io(a);
+    for (int si = 0; si < a.n_seg; ++si) {
+        stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
+        if (si == 0) sr.mark(3);
+        stage_x<false>(sm + pl.s[si].xoff, a.seg[si], a.seg[si].X, pl.s[si], b, pos0);
+        if (si == 0) sr.mark(4);
     }
+    sr.mark(5);
+    __syncthreads();
+    sr.mark(1);
+    EpiOps<TP> e;
+    epi_load<TP, false>(e, a, io, pos0, co0, b);
+    conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sr);
+#if UNET_STAMP
+    stamps_flush(sr);
 #endif
-    conv_tile<TW, TP, false>(k->a, k->pl, conv_io(k->a), sm, blockIdx.x * TP, blockIdx.y * 16,
-                             blockIdx.z, false, stp, true);
+}
+
+// The direct-staging launch kernel (see fast_* above): NS segments, all staged in one round
+// trip when they fit the per-thread budgets (the first round of every segment is issued before
+// any store; a segment with more items runs extra rounds after), then conv_finish.
+template <typename TW, int TP, int NS>
+__global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const LDM_KC ConvKArgs* k = (const LDM_KC ConvKArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    KConv& a = k->a;
+    KPlan& pl = k->pl;
+    StampRegs sr;
+    sr.on = UNET_STAMP && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 &&
+            threadIdx.x == 0;
+    sr.mark(0);
+    const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
+    const ConvIO io = conv_io(a);
+    // per-thread items of a segment's first round: weights (16 B each) and window items (4 x
+    // 16 B each) -- register budgets shrink with the segment count
+    constexpr int NBW = NS <= 2 ? 4 : 2;
+    constexpr int NBX = NS == 1 ? 4 : NS <= 3 ? 2 : 1;
+    u32x4 wv[NS][NBW];
+    f32x4 xv[NS][NBX][4];
+#pragma unroll
+    for (int si = 0; si < NS; ++si) {
+        fast_w_issue<TW, NBW>(wv[si], a.seg[si], pl.s[si], co0, 0);
+        fast_x_issue<NBX>(xv[si], a.seg[si], pl.s[si], a.seg[si].X, b, pos0, 0);
+    }
+    EpiOps<TP> e;
+    epi_load<TP, false>(e, a, io, pos0, co0, b);
+    // keep every load above issued before the first use of any of them below: the scheduler
+    // otherwise pairs each segment's stores with its loads, or hoists the first bf16 unpack
+    // above the window loads -- either is a wait for the data in the middle of the issue, one
+    // round trip per part again.  (Empty asm: a memory clobber orders the loads; the register
+    // operands make every use of the loaded values come after it.)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int si = 0; si < NS; ++si) {
+#pragma unroll
+        for (int u = 0; u < NBW; ++u) asm volatile("" : "+v"(wv[si][u]));
+#pragma unroll
+        for (int u = 0; u < NBX; ++u)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) asm volatile("" : "+v"(xv[si][u][m]));
+    }
+#pragma unroll
+    for (int si = 0; si < NS; ++si) {
+        fast_w_store<TW, NBW>(wv[si], sm, a.seg[si], pl.s[si], 0);
+        fast_x_store<NBX>(xv[si], sm, a.seg[si], pl.s[si], pos0, 0);
+    }
+    sr.mark(3);
+    sr.mark(4);
+#pragma unroll
+    for (int si = 0; si < NS; ++si) {
+        for (int base = 256 * NBW; base < pl.s[si].nw; base += 256 * NBW) {
+            u32x4 v[NBW];
+            fast_w_issue<TW, NBW>(v, a.seg[si], pl.s[si], co0, base);
+            fast_w_store<TW, NBW>(v, sm, a.seg[si], pl.s[si], base);
+        }
+        for (int base = 256 * NBX; base < pl.s[si].nx; base += 256 * NBX) {
+            f32x4 v[NBX][4];
+            fast_x_issue<NBX>(v, a.seg[si], pl.s[si], a.seg[si].X, b, pos0, base);
+            fast_x_store<NBX>(v, sm, a.seg[si], pl.s[si], pos0, base);
+        }
+    }
+    sr.mark(5);
+    __syncthreads();
+    sr.mark(1);
+    conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sr);
+#if UNET_STAMP
+    stamps_flush(sr);
+#endif
 }
 
 constexpr int kMaxLdsBytes = 160 * 1024;
 
+__host__ __device__ constexpr bool pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
+inline int ilog2(int x) { int l = 0; while ((1 << l) < x) ++l; return l; }
+
 int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) {
     int off = 0, ch = 0;
+    const int epv = a.w_dtype == LDM_BF16 ? 8 : 4;
+    bool fast = true;
     for (int i = 0; i < a.n_seg; ++i) {
         const ldm_conv1d_seg_t& g = a.seg[i];
         SegPlan& p = pl->s[i];
@@ -535,12 +819,31 @@ int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) 
         off += 16 * (g.ksize * p.cinp + 4);
         p.ch0 = ch;
         ch += g.ksize * (p.cinp / 16);
+        // direct staging: power-of-two item counts, 16-byte source groups, 32-bit offsets
+        p.lgv = ilog2(p.cinp / epv);
+        p.nw = 16 * g.ksize * (p.cinp / epv);
+        const int span = g.mode == LDM_CONV_UP2 ? p.win / 2 + 3 : p.win + 2;
+        p.lgng = ilog2(span / 4 + 1);
+        p.nx = (p.cinp / 4) << p.lgng;
+        const int64_t wbytes = (int64_t)(a.Cout + 15) / 16 * 16 * g.ldw * (epv == 8 ? 2 : 4);
+        fast = fast && pow2(p.cinp) && g.L_in % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
+               ((uintptr_t)g.W & 15) == 0 && (g.ldw * (16 / epv)) % 16 == 0 &&
+               (g.kstride * (16 / epv)) % 16 == 0 &&
+               (int64_t)g.C * g.L_in * 4 < (1ll << 31) && wbytes < (1ll << 31);
     }
     pl->nchunks = ch;
+    pl->fast = fast;
     const int red = 4 * (TP / 16) * 4 * 64;
-    pl->lds_floats = (off > red ? off : red) + 4;
+    pl->lds_floats = off > red ? off : red;
     *lds_bytes = 4 * pl->lds_floats;
     return *lds_bytes <= kMaxLdsBytes ? 0 : LDM_ENOSPC;
+}
+
+template <typename TW, int TP, int NS>
+int launch_fast(const ConvKArgs& ka, dim3 grid, int lds, hipStream_t s) {
+    LDM_TRY((set_max_lds_once<&conv1d_fast_kernel<TW, TP, NS>>(kMaxLdsBytes, "conv1d")));
+    hipLaunchKernelGGL((conv1d_fast_kernel<TW, TP, NS>), grid, dim3(256), lds, s, ka);
+    return launch_status("ldm_conv1d");
 }
 
 template <typename TW, int TP>
@@ -550,11 +853,20 @@ int launch_tp(const ldm_conv1d_args_t& a, hipStream_t s) {
     LDM_REQUIRE(make_plan(a, TP, &pl, &lds) == 0, LDM_ENOSPC,
                 "conv1d: staged operands need %d B of LDS (> %d); split the channels", lds,
                 kMaxLdsBytes);
-    LDM_TRY((set_max_lds_once<&conv1d_mfma_kernel<TW, TP>>(kMaxLdsBytes, "conv1d")));
     const dim3 grid((a.L_out + TP - 1) / TP, (a.Cout + 15) / 16, a.B);
     ConvKArgs ka;
     ka.a = a;
     ka.pl = pl;
+    // dev A/B: LDM_CONV_FAST=0 forces the generic staging
+    if (pl.fast && dev_knob("LDM_CONV_FAST", 1)) {
+        switch (a.n_seg) {
+            case 1: return launch_fast<TW, TP, 1>(ka, grid, lds, s);
+            case 2: return launch_fast<TW, TP, 2>(ka, grid, lds, s);
+            case 3: return launch_fast<TW, TP, 3>(ka, grid, lds, s);
+            default: return launch_fast<TW, TP, 4>(ka, grid, lds, s);
+        }
+    }
+    LDM_TRY((set_max_lds_once<&conv1d_mfma_kernel<TW, TP>>(kMaxLdsBytes, "conv1d")));
     hipLaunchKernelGGL((conv1d_mfma_kernel<TW, TP>), grid, dim3(256), lds, s, ka);
     return launch_status("ldm_conv1d");
 }

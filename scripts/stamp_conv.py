@@ -1,7 +1,9 @@
 """Per-phase times of the 18 ldm_conv1d launches of one UNet reverse step (graph path, B = 1),
 from the diagnostic build's stamps (-DUNET_STAMP=1): workgroup (0, 0, 0) of each launch stamps
 s_memrealtime (100 MHz) at entry, after staging (barrier), after the MFMA loop (barrier), after
-the partial-tile reduction (barrier) and after its stores drained.
+the partial-tile reduction (barrier) and after its stores drained; inside the staging, after
+segment 0's weights, after segment 0's window and after the last segment (thread 0's view;
+the rest up to the barrier is waiting for the other waves).
   build:  make -C <csrc> BUILD=build_stamp OUT=../ldm_sdf/libldm_stamp.so \\
             HIPFLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -DUNET_STAMP=1"
   run:    LDM_SDF_LIB=<...>/libldm_stamp.so python scripts/stamp_conv.py [B]"""
@@ -37,14 +39,18 @@ st = buf[slots].astype(np.int64)
 names = ["conv_in", "r0.c1", "r0.c2", "down0", "r1.c1", "r1.c2", "down1", "r2.c1", "r2.c2",
          "r3.c1", "r3.c2", "up1", "r4.c1", "r4.c2", "up0", "r5.c1", "r5.c2", "conv_out"]
 print(f"B={B}: per-launch phases of workgroup (0,0,0), us (s_memrealtime, 10 ns)")
-print(f"{'conv':>9} {'stage':>7} {'mfma':>7} {'reduce':>7} {'epi+st':>7} {'total':>7} {'->next':>7}")
-tot = np.zeros(6)
+print(f"{'conv':>9} {'stage':>7} {'mfma':>7} {'reduce':>7} {'epi+st':>7} {'total':>7} {'->next':>7}"
+      f" | stage = {'w0':>6} {'x0':>6} {'segs+':>6} {'bar':>6}")
+tot = np.zeros(10)
 for i in range(18):
     r = st[18 + i]
     nxt = st[18 + i + 1][0] if i + 1 < 18 else r[7]
     d = [(r[1] - r[0]) / 100, (r[2] - r[1]) / 100, (r[6] - r[2]) / 100, (r[7] - r[6]) / 100,
-         (r[7] - r[0]) / 100, (nxt - r[7]) / 100]
+         (r[7] - r[0]) / 100, (nxt - r[7]) / 100,
+         (r[3] - r[0]) / 100, (r[4] - r[3]) / 100, (r[5] - r[4]) / 100, (r[1] - r[5]) / 100]
     tot += d
-    print(f"{names[i]:>9} " + " ".join(f"{x:7.2f}" for x in d))
-print(f"{'sum':>9} " + " ".join(f"{x:7.2f}" for x in tot))
+    print(f"{names[i]:>9} " + " ".join(f"{x:7.2f}" for x in d[:6]) + " | " +
+          " ".join(f"{x:6.2f}" for x in d[6:]))
+print(f"{'sum':>9} " + " ".join(f"{x:7.2f}" for x in tot[:6]) + " | " +
+      " ".join(f"{x:6.2f}" for x in tot[6:]))
 print(f"step span (entry of conv_in -> stores of conv_out): {(st[35][7] - st[18][0]) / 100:.1f} us")
