@@ -11,8 +11,7 @@
 //   1. classify   one thread per grid point: 3-bit mask of its owned crossing edges (+x, +y,
 //                 +z), and for the cube it anchors the 8-corner case and its triangle count,
 //                 packed in one u16 (mask | ntri << 3 | case << 8) -> 2 B/point written
-//   2. block sums per 4096-point chunk: (#vertices, #triangles) -- for N % 4 == 0 folded into
-//                 pass 1 (per 1024-point workgroup; the scan sums 4 per chunk)
+//   2. block sums per 4096-point chunk: (#vertices, #triangles)
 //   3. chunk scan  one workgroup: exclusive offsets of the chunks + the totals
 //   4. vertices   per chunk: in-chunk exclusive scan, vertex positions, per-point first
 //                 vertex index (vofs)
@@ -171,17 +170,11 @@ __device__ __forceinline__ void stage_ntri(unsigned char* s_ntri) {
 // row, rows in (k, j) order), flat over the Q * N * N quads.  Per quad it loads the 5 values
 // i0 .. i0+4 of the rows (j, k), (j+1, k), (j, k+1), (j+1, k+1) (clamped to the volume), as
 // 16-byte vectors when rows are 16-byte aligned (N % 4 == 0), and writes 4 codes.
-// VEC (N % 4 == 0): a workgroup's 256 quads are the 1024 consecutive points [1024 b, 1024 b +
-// 1024), so it also writes their (#vertices, #triangles) to bsum[b] -- pass 2 folded in (the
-// chunk scan then sums 4 such entries per 4096-point chunk: kSub).
-constexpr int kSub = kChunk / 1024;
 template <bool VEC>
 __global__ __launch_bounds__(256) void mc_classify_kernel(const float* __restrict__ vol, int N,
                                                           float iso,
-                                                          unsigned short* __restrict__ code,
-                                                          int2* __restrict__ bsum) {
+                                                          unsigned short* __restrict__ code) {
     __shared__ unsigned char s_ntri[256];
-    __shared__ int s_red[8];
     stage_ntri(s_ntri);
     const int Q = (N + 3) >> 2;
     const int64_t NN = (int64_t)N * N;
@@ -208,8 +201,7 @@ __global__ __launch_bounds__(256) void mc_classify_kernel(const float* __restric
             for (int u = 0; u < 5; ++u) v[q][u] = vol[r[q] + min(ic + u, N - 1)];
     }
     __syncthreads();                                   // s_ntri
-    const bool live = g == gc;
-    if (!VEC && !live) return;
+    if (g != gc) return;
     const bool jy = j + 1 < N, kz = k + 1 < N;
     unsigned short cd[4];
 #pragma unroll
@@ -231,34 +223,11 @@ __global__ __launch_bounds__(256) void mc_classify_kernel(const float* __restric
         cd[u] = (unsigned short)(m | (nt << 3) | (cfg << 8));
     }
     unsigned short* dst = code + r[0] + i0;
-    if (VEC) {
+    if (VEC && i0 + 4 <= N) {
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
         const u32x2 w = {(unsigned)cd[0] | (unsigned)cd[1] << 16,
                          (unsigned)cd[2] | (unsigned)cd[3] << 16};
-        if (live) *reinterpret_cast<u32x2*>(dst) = w;
-        // the workgroup's sums (a clamped quad past the end counts 0)
-        int nv = 0, ntr = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            nv += __popc(cd[u] & 7u);
-            ntr += (cd[u] >> 3) & 7u;
-        }
-        nv = live ? nv : 0;
-        ntr = live ? ntr : 0;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            nv += __shfl_xor(nv, o);
-            ntr += __shfl_xor(ntr, o);
-        }
-        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        if (lane == 0) {
-            s_red[wv] = nv;
-            s_red[4 + wv] = ntr;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0)
-            bsum[blockIdx.x] = make_int2(s_red[0] + s_red[1] + s_red[2] + s_red[3],
-                                         s_red[4] + s_red[5] + s_red[6] + s_red[7]);
+        *reinterpret_cast<u32x2*>(dst) = w;
     } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -333,41 +302,45 @@ __global__ __launch_bounds__(256) void mc_block_sums_kernel(const unsigned short
 // [t * per, (t + 1) * per), summed serially, then ONE block scan of the 256 thread sums and a
 // second serial pass writes the offsets (the previous form ran nb / 256 block scans, each with
 // its barriers: 16 us at 256^3)
-// F: bsum entries per chunk (1: pass 2's per-chunk sums; kSub: classify's per-1024-point sums,
-// entries past the last point absent: nsub bounds them)
+// The serial passes read their chunk sums kScanBatch at a time, every load of a batch issued
+// before any use (clamped index, value selected): a plain loop waited out one round trip per
+// chunk, 2 x 16 of them at 256^3 (9.4 us, profiles/r04a/mc_kernel_stats.csv).
+constexpr int kScanBatch = 8;
 __global__ __launch_bounds__(256) void mc_chunk_scan_kernel(const int2* __restrict__ bsum, int nb,
-                                                            int F, int nsub,
                                                             int2* __restrict__ boff,
                                                             int32_t* __restrict__ totals) {
     __shared__ int lds[8];
     const int per = (nb + 255) / 256;
     const int b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
-    auto chunk = [&](int b) {
-        int2 x = make_int2(0, 0);
-        for (int f = 0; f < F; ++f) {
-            const int i = b * F + f;
-            if (i < nsub) {
-                const int2 y = bsum[i];
-                x.x += y.x;
-                x.y += y.y;
-            }
-        }
-        return x;
+    auto batch = [&](int b, int2 (&x)[kScanBatch]) {
+#pragma unroll
+        for (int u = 0; u < kScanBatch; ++u) x[u] = bsum[min(b + u, b1 - 1)];
+#pragma unroll
+        for (int u = 0; u < kScanBatch; ++u)
+            if (b + u >= b1) x[u] = make_int2(0, 0);
     };
     int sv = 0, st = 0;
-    for (int b = b0; b < b1; ++b) {
-        const int2 x = chunk(b);
-        sv += x.x;
-        st += x.y;
+    for (int b = b0; b < b1; b += kScanBatch) {
+        int2 x[kScanBatch];
+        batch(b, x);
+#pragma unroll
+        for (int u = 0; u < kScanBatch; ++u) {
+            sv += x[u].x;
+            st += x[u].y;
+        }
     }
     int tv, tt;
     int cv = block_excl_scan(sv, lds, &tv);
     int ct = block_excl_scan(st, lds + 4, &tt);
-    for (int b = b0; b < b1; ++b) {
-        const int2 x = chunk(b);
-        boff[b] = make_int2(cv, ct);
-        cv += x.x;
-        ct += x.y;
+    for (int b = b0; b < b1; b += kScanBatch) {
+        int2 x[kScanBatch];
+        batch(b, x);
+#pragma unroll
+        for (int u = 0; u < kScanBatch; ++u) {
+            if (b + u < b1) boff[b + u] = make_int2(cv, ct);
+            cv += x[u].x;
+            ct += x[u].y;
+        }
     }
     if (threadIdx.x == 0) {
         totals[0] = tv;
@@ -526,7 +499,7 @@ McWs mc_ws_layout(int N, void* base) {
     w.code = reinterpret_cast<unsigned short*>(b + o);
     o += up((size_t)nb * kChunk * 2);           // padded to whole chunks (vector loads)
     w.bsum = reinterpret_cast<int2*>(b + o);
-    o += up((size_t)nb * kSub * sizeof(int2));  // per-chunk or per-1024-point sums
+    o += up((size_t)nb * sizeof(int2));
     w.boff = reinterpret_cast<int2*>(b + o);
     o += up((size_t)nb * sizeof(int2));
     w.vofs = reinterpret_cast<int32_t*>(b + o);
@@ -577,19 +550,15 @@ extern "C" int ldm_mc_count(const float* vol, int N, float level, void* ws, size
     }
     const int64_t quads = (int64_t)((N + 3) / 4) * N * N;
     const dim3 cgrid((unsigned)((quads + 255) / 256));
-    if ((N & 3) == 0) {
-        // classify writes the per-1024-point sums itself (its workgroups are those ranges)
+    if ((N & 3) == 0)
         hipLaunchKernelGGL(mc_classify_kernel<true>, cgrid, dim3(256), 0, st, vol, N, level,
-                           w.code, w.bsum);
-        hipLaunchKernelGGL(mc_chunk_scan_kernel, dim3(1), dim3(256), 0, st, w.bsum, nb, kSub,
-                           (int)cgrid.x, w.boff, counts_out);
-    } else {
+                           w.code);
+    else
         hipLaunchKernelGGL(mc_classify_kernel<false>, cgrid, dim3(256), 0, st, vol, N, level,
-                           w.code, w.bsum);
-        hipLaunchKernelGGL(mc_block_sums_kernel, dim3(nb), dim3(256), 0, st, w.code, n, w.bsum);
-        hipLaunchKernelGGL(mc_chunk_scan_kernel, dim3(1), dim3(256), 0, st, w.bsum, nb, 1, nb,
-                           w.boff, counts_out);
-    }
+                           w.code);
+    hipLaunchKernelGGL(mc_block_sums_kernel, dim3(nb), dim3(256), 0, st, w.code, n, w.bsum);
+    hipLaunchKernelGGL(mc_chunk_scan_kernel, dim3(1), dim3(256), 0, st, w.bsum, nb, w.boff,
+                       counts_out);
     return launch_status("ldm_mc_count");
 }
 

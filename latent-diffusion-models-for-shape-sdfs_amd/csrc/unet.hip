@@ -336,13 +336,13 @@ struct StampPtr {
     uint64_t* p;
     bool ext;
     __device__ __forceinline__ void mark(int k) {
-        if (UNET_STAMP && p && threadIdx.x == 0 && (ext || k <= 2))
+        if (UNET_STAMP && p && threadIdx.x == 0 && k < 8 && (ext || k <= 2))
             p[k] = __builtin_amdgcn_s_memrealtime();
     }
 };
 struct StampRegs {
     bool on;
-    uint64_t t[8];
+    uint64_t t[16];
     __device__ __forceinline__ void mark(int k) {
         if (UNET_STAMP && on) t[k] = __builtin_amdgcn_s_memrealtime();
     }
@@ -384,9 +384,10 @@ __device__ __forceinline__ void epi_load(EpiOps<TP>& e, KConv& a, const ConvIO& 
         e.x[k] = ld_act<HO>(ddpm ? io.xlat + idx : dummy);
         e.z[k] = *(noise ? io.z + idx : dummy);
     }
-    e.c1 = *(ddpm ? a.c1 + io.t : dummy);
-    e.c2 = *(ddpm ? a.c2 + io.t : dummy);
-    e.sg = *(ddpm ? a.sigma + io.t : dummy);
+    // batch-uniform: scalar loads (the tables are not written during the launch)
+    e.c1 = *(const LDM_KC float*)(ddpm ? a.c1 + io.t : dummy);
+    e.c2 = *(const LDM_KC float*)(ddpm ? a.c2 + io.t : dummy);
+    e.sg = *(const LDM_KC float*)(ddpm ? a.sigma + io.t : dummy);
 }
 
 // The tile after its operands are staged (and the staging barrier passed): the MFMA
@@ -457,6 +458,7 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
     bool h0 = c_beg < c_end, h1 = c_beg + 1 < c_end;
     if (h0) load_chunk(a0, b0);
     if (h1) load_chunk(a1, b1);
+    st_.mark(8);
     for (int ch = c_beg; h0; ch += 2) {
         // the next pair first (its LDS latency hides under this pair's MFMAs); a missing
         // second chunk is all zeros: its MFMAs add exact zeros
@@ -485,6 +487,7 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = acc0[t] + acc1[t];
+    st_.mark(9);
     __syncthreads();                    // every wave is done reading the staged operands
     st_.mark(2);
     float* red = sm;                    // [wave][t][reg][lane]
@@ -516,6 +519,7 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
         if (ddpm) y = ddpm_update(e.x[k], pre, noise ? e.z[k] : 0.f, e.c1, e.c2, e.sg, noise);
         io.Y[idx] = y;
     }
+    st_.mark(10);
     if (UNET_STAMP) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_.mark(7);
@@ -685,7 +689,7 @@ struct ConvKArgs {
 #if UNET_STAMP
 // diagnostic build: workgroup (0, 0, 0) of every ldm_conv1d launch stamps entry, staging done,
 // MFMA done, reduction done and stores drained into a ring of 256 launches (ldm_dev_conv_stamps)
-__device__ uint64_t g_conv_stamp[256][8];
+__device__ uint64_t g_conv_stamp[256][16];
 __device__ unsigned g_conv_stamp_n;
 #endif
 
@@ -693,7 +697,7 @@ __device__ unsigned g_conv_stamp_n;
 __device__ __forceinline__ void stamps_flush(const StampRegs& sr) {
     if (!sr.on) return;
     uint64_t* p = g_conv_stamp[atomicAdd(&g_conv_stamp_n, 1u) & 255u];
-    for (int i = 0; i < 8; ++i) p[i] = sr.t[i];
+    for (int i = 0; i < 16; ++i) p[i] = sr.t[i];
 }
 #endif
 
@@ -730,7 +734,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
 // The direct-staging launch kernel (see fast_* above): NS segments, all staged in one round
 // trip when they fit the per-thread budgets (the first round of every segment is issued before
 // any store; a segment with more items runs extra rounds after), then conv_finish.
-template <typename TW, int TP, int NS>
+template <typename TW, int TP, int NS, int NBW>
 __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const LDM_KC ConvKArgs* k = (const LDM_KC ConvKArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -742,10 +746,12 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     sr.mark(0);
     const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
     const ConvIO io = conv_io(a);
-    // per-thread items of a segment's first round: weights (16 B each) and window items (4 x
-    // 16 B each) -- register budgets shrink with the segment count
-    constexpr int NBW = NS <= 2 ? 4 : 2;
-    constexpr int NBX = NS == 1 ? 4 : NS <= 3 ? 2 : 1;
+    // per-thread items of a segment's first round: weights (16 B each; NBW picked per launch
+    // from the segments' counts) and window items (4 x 16 B each: TP / 16 covers 128 channels).
+    // Every slot is a load instruction even when its item is absent (out of range: no memory
+    // access, but TA issue), so the slots match the launch: 4-slot weights and windows at every
+    // size cost ~1 us per small conv (profiles/r04g).
+    constexpr int NBX = TP / 16;
     u32x4 wv[NS][NBW];
     f32x4 xv[NS][NBX][4];
 #pragma unroll
@@ -839,11 +845,20 @@ int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) 
     return *lds_bytes <= kMaxLdsBytes ? 0 : LDM_ENOSPC;
 }
 
-template <typename TW, int TP, int NS>
+template <typename TW, int TP, int NS, int NBW>
 int launch_fast(const ConvKArgs& ka, dim3 grid, int lds, hipStream_t s) {
-    LDM_TRY((set_max_lds_once<&conv1d_fast_kernel<TW, TP, NS>>(kMaxLdsBytes, "conv1d")));
-    hipLaunchKernelGGL((conv1d_fast_kernel<TW, TP, NS>), grid, dim3(256), lds, s, ka);
+    LDM_TRY((set_max_lds_once<&conv1d_fast_kernel<TW, TP, NS, NBW>>(kMaxLdsBytes, "conv1d")));
+    hipLaunchKernelGGL((conv1d_fast_kernel<TW, TP, NS, NBW>), grid, dim3(256), lds, s, ka);
     return launch_status("ldm_conv1d");
+}
+
+template <typename TW, int TP, int NS>
+int launch_fast_nbw(const ConvKArgs& ka, dim3 grid, int lds, hipStream_t s) {
+    int nw = 0;
+    for (int i = 0; i < NS; ++i) nw = ka.pl.s[i].nw > nw ? ka.pl.s[i].nw : nw;
+    if (nw <= 256) return launch_fast<TW, TP, NS, 1>(ka, grid, lds, s);
+    if (nw <= 512) return launch_fast<TW, TP, NS, 2>(ka, grid, lds, s);
+    return launch_fast<TW, TP, NS, 4>(ka, grid, lds, s);   // more: extra rounds
 }
 
 template <typename TW, int TP>
@@ -858,12 +873,11 @@ int launch_tp(const ldm_conv1d_args_t& a, hipStream_t s) {
     ka.a = a;
     ka.pl = pl;
     // dev A/B: LDM_CONV_FAST=0 forces the generic staging
-    if (pl.fast && dev_knob("LDM_CONV_FAST", 1)) {
+    if (pl.fast && a.n_seg <= 3 && dev_knob("LDM_CONV_FAST", 1)) {
         switch (a.n_seg) {
-            case 1: return launch_fast<TW, TP, 1>(ka, grid, lds, s);
-            case 2: return launch_fast<TW, TP, 2>(ka, grid, lds, s);
-            case 3: return launch_fast<TW, TP, 3>(ka, grid, lds, s);
-            default: return launch_fast<TW, TP, 4>(ka, grid, lds, s);
+            case 1: return launch_fast_nbw<TW, TP, 1>(ka, grid, lds, s);
+            case 2: return launch_fast_nbw<TW, TP, 2>(ka, grid, lds, s);
+            default: return launch_fast_nbw<TW, TP, 3>(ka, grid, lds, s);
         }
     }
     LDM_TRY((set_max_lds_once<&conv1d_mfma_kernel<TW, TP>>(kMaxLdsBytes, "conv1d")));
@@ -1098,7 +1112,7 @@ extern "C" int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s) {
 }
 
 #if UNET_STAMP
-// diagnostic build only: the conv stamp ring (256 x 8 s_memrealtime values) and its counter
+// diagnostic build only: the conv stamp ring (256 x 16 s_memrealtime values) and its counter
 extern "C" int ldm_dev_conv_stamps(uint64_t* host, unsigned* n) {
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ldm::g_conv_stamp), sizeof(ldm::g_conv_stamp)) !=
             hipSuccess ||

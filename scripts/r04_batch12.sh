@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 GPU batch 12: direct conv staging v4 (launch-sized weight slots, TP-sized window slots,
+# scalar schedule loads); MC chunk scan with batched loads -- all GPU tests, conv stamps, A/B vs the generic staging, MC kernel split,
+# the default bench.
+set -e
+O=$GRAFT_REPO_ROOT/gpurun_out/r04n
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+LIB=$GRAFT_REPO_ROOT/latent-diffusion-models-for-shape-sdfs_amd/ldm_sdf/libldm_stamp.so
+LDM_SDF_LIB=$LIB LDM_CONV_FAST=1 timeout -k 10 120 python -u scripts/stamp_conv.py 1 > $O/stamp_conv_b1_direct.log 2>&1
+LDM_SDF_LIB=$LIB LDM_CONV_FAST=0 timeout -k 10 120 python -u scripts/stamp_conv.py 1 > $O/stamp_conv_b1_generic.log 2>&1
+DEV=$GRAFT_REPO_ROOT/latent-diffusion-models-for-shape-sdfs_amd/ldm_sdf/libldm_dev.so
+for v in 0 1 0 1; do
+  LDM_SDF_LIB=$DEV LDM_CONV_FAST=$v UNET_STEPS=1000 timeout -k 10 120 python -u scripts/unet_once.py >> $O/ab_fast_b1.log 2>&1
+  echo "^ LDM_CONV_FAST=$v" >> $O/ab_fast_b1.log
+  LDM_SDF_LIB=$DEV LDM_CONV_FAST=$v UNET_B=8 UNET_STEPS=1000 timeout -k 10 120 python -u scripts/unet_once.py >> $O/ab_fast_b8.log 2>&1
+  echo "^ LDM_CONV_FAST=$v" >> $O/ab_fast_b8.log
+done
+timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mc -o mc -- python3 $GRAFT_REPO_ROOT/scripts/mc_once.py 20 > $O/mc_once.log 2>&1
+echo batch12 done

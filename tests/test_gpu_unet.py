@@ -51,13 +51,13 @@ CASES = [
                         (16, 64, 1, 1, 0, False)], 32, False, False),
     ("k4s2", 2, [(8, 130, 4, 2, 0, False)], 5, False, False),
     ("cin1_cout1", 5, [(1, 1024, 3, 1, 0, False)], 1, False, False),
-    # direct staging (ldm_conv1d's launch kernel: power-of-two channel blocks, L_in % 4 == 0;
+    # direct staging (ldm_conv1d's launch kernel: power-of-two channel blocks, L_in % 4 == 0,
     # the cases above with other sizes take the generic staging)
     ("up2_direct", 2, [(64, 64, 3, 1, 1, True)], 32, True, False),
     ("k3s2_direct", 2, [(32, 128, 3, 2, 0, True)], 48, False, True),
     ("k4s2_direct", 3, [(16, 128, 4, 2, 0, False)], 16, False, False),
     ("concat_up2_direct", 2, [(64, 32, 3, 1, 1, True), (32, 32, 3, 1, 1, True)], 24, True, False),
-    ("four_seg_direct", 2, [(32, 64, 3, 1, 0, True), (16, 64, 3, 1, 0, True),
+    ("four_seg_generic", 2, [(32, 64, 3, 1, 0, True), (16, 64, 3, 1, 0, True),
                             (16, 64, 1, 1, 0, False), (64, 64, 1, 1, 0, False)], 32, True, True),
     ("c128_tile32_direct", 16, [(128, 128, 3, 1, 0, True)], 128, True, True),
 ]
