@@ -434,26 +434,17 @@ def config5(args, rank, world, dev, group, gen):
     xT = torch.randn(nl, 1024, device=dev, generator=gen)
     noise = torch.randn(1000, nl, 1024, device=dev, generator=gen)
 
-    def timed_sampler(persistent):
-        smp = ldm_sdf.Sampler(unet, sch, nl, dtype="bf16", device=dev, persistent=persistent)
-        smp.run(xT, noise)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        reps, status = 3, []
-        for _ in range(reps):
-            lat = smp.run(xT, noise, check=False).clone()
-            if smp.loop is not None:
-                status.append(smp.loop.status())      # outside the kernel, read per rep
-        torch.cuda.synchronize()
-        return 1000 * reps / (time.perf_counter() - t0), lat, smp, status
-
-    # default Sampler path (the hipGraph of per-step launches for the UNet: DESIGN.md §9), and
-    # the one-launch loop (ldm_unet_loop) beside it on the same inputs
-    sps, lat, sampler, _ = timed_sampler(None)
-    has_loop = 1 <= nl <= 16                     # UNet1DDenoiser.make_loop's batch range
-    if has_loop:
-        sps_loop, lat_loop, _, loop_status = timed_sampler(True)
-        loop_ok = all(v == 0 for v in loop_status)
+    # the Sampler path: the hipGraph of 1000 steps x 18 ldm_conv1d launches (the
+    # round-3 one-launch loop was retired in round 4)
+    smp = ldm_sdf.Sampler(unet, sch, nl, dtype="bf16", device=dev)
+    smp.run(xT, noise)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        lat = smp.run(xT, noise).clone()
+    torch.cuda.synchronize()
+    sps = 1000 * reps / (time.perf_counter() - t0)
     latents = ldm_sdf.dist.all_gather_rows(lat[:hi - lo].clone(), nb, group=group) \
         if world > 1 else lat[:nb].clone()
     dec = ldm_sdf.SDFDecoder(1024, seed=1235)            # widen-skip (L + 3 >= H)
@@ -480,15 +471,7 @@ def config5(args, rank, world, dev, group, gen):
                                "flops_per_query": FLOPS_PER_QUERY_WIDEN,
                                "queries_per_launch": qpl, "avg_launch_ms": kms},
            "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
-           "unet_path": ("one persistent launch for all 1000 steps (ldm_unet_loop)"
-                         if sampler.loop is not None else
-                         "hipGraph of 1000 steps x 18 ldm_conv1d launches"),
-           "unet_loop_path": ({"steps_per_s": sps_loop if loop_ok else None,
-                               "path": "ldm_unet_loop: one replica of the 18-conv step per XCD, "
-                                       "XCD-local barriers, one launch for 1000 steps",
-                               "status_per_rep": loop_status,
-                               "bit_identical": bool(torch.equal(lat, lat_loop))}
-                              if has_loop else None),
+           "unet_path": "hipGraph of 1000 steps x 18 ldm_conv1d launches (direct staging)",
            "unet_conv_weight_bytes_per_step": wbytes}
     # the graph path's bound: 18 dependent launches per step, each at least one dependent graph
     # node (the conv grids are 64-128 workgroups at B = 1: ldm_conv1d's tile rule)

@@ -12,8 +12,7 @@
  *     (the shim checks alignment).  The library never allocates or frees device memory.
  *   - Every launch is asynchronous on the caller's stream; no hidden synchronisation, no
  *     hipMalloc / hipMemcpy (so calls can be captured into a hipGraph).  Exceptions, each
- *     documented at its declaration: the *_status reads and ldm_unet_loop_prepare (a one-time
- *     program upload) synchronise the stream.
+ *     documented at its declaration: the *_status reads synchronise the stream.
  *   - Return 0 on success, a negative LDM_E* code for an argument error, or a positive
  *     hipError_t.  ldm_last_error() returns a thread-local message for the last failure.
  *   - One device per process (the current HIP device, as set by torch).
@@ -28,7 +27,7 @@
 extern "C" {
 #endif
 
-#define LDM_ABI_VERSION 5
+#define LDM_ABI_VERSION 6
 
 /* dtypes */
 #define LDM_F32 0
@@ -477,43 +476,8 @@ typedef struct ldm_conv1d_args {
 } ldm_conv1d_args_t;
 int ldm_conv1d(const ldm_conv1d_args_t* a, ldm_stream_t s);
 
-/* ---- C17 sampling loop: the whole T-step UNet reverse loop as ONE launch -- */
-/* A "program" is the n_phase ldm_conv1d calls of one reverse step (the UNet: 18), as
- * ldm_conv1d would take them, plus which fields follow the step: with x2 [2][B][D] and
- * cur = step & 1, t = t_hi - step,
- *   LDM_UNET_PATCH_X      seg[0].X = x2[cur]                                (the input conv)
- *   LDM_UNET_PATCH_STEP   Y = x2[cur ^ 1], xlat = x2[cur], z = noise[t], t  (the DDPM conv)
- *   LDM_UNET_PATCH_CBIAS  cbias = cbias + t * cb_tstride   (a [T][Cout] table's base: E_i[t])
- * ldm_unet_loop_prepare checks the program (every conv must be an ldm_conv1d-valid call with
- * batch-uniform cbias, w_dtype and B equal across phases, LDS plan at 32-position tiles
- * <= 78 KiB) and uploads it into ws with a header recording n_phase, w_dtype, B (phase 0's
- * conv.B) and D (phase 0's seg[0].L_in) (synchronises the stream).  ldm_unet_loop then runs
- * `steps` reverse steps from t_hi in one launch: 512 workgroups (2 per CU, 64 per XCD), one
- * replica of the program per XCD (shapes b = xcd mod 8), an XCD-local barrier between
- * dependent convs; the convs' arithmetic is ldm_conv1d's, so the result is bit-identical to
- * n_phase * steps ldm_conv1d calls.  Result in x2[steps & 1].  LDM_EINVAL for B outside
- * 1..16; LDM_ENOSYS when the device has no 8 x 32-CU replica geometry (not an MI355X).
- * ldm_unet_loop_status: 0 completed, 1 a barrier timed out (partial latents), 2 workgroups
- * were not placed 64 per XCD (nothing computed), 3 the launch's n_phase / w_dtype / B / D
- * differ from the prepared program's (nothing computed); synchronises the stream. */
-#define LDM_UNET_PATCH_X 1
-#define LDM_UNET_PATCH_STEP 2
-#define LDM_UNET_PATCH_CBIAS 4
-#define LDM_UNET_MAX_PHASES 32
-typedef struct ldm_unet_phase {
-    ldm_conv1d_args_t conv;
-    int32_t patch, reserved;
-    int64_t cb_tstride;
-} ldm_unet_phase_t;
-size_t ldm_unet_loop_ws_bytes(int n_phase);
-int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, void* ws, size_t ws_bytes,
-                          ldm_stream_t s);
-int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* noise, int B, int D,
-                  int t_hi, int steps, void* ws, size_t ws_bytes, ldm_stream_t s);
-int ldm_unet_loop_status(const void* ws, unsigned* status_host, ldm_stream_t s);
-/* Fault-injection control of ldm_unet_loop on the current device (tests only): polls before a
- * barrier wait gives up (status 1); 0 restores the default. */
-int ldm_unet_loop_config(unsigned spin_limit);
+/* (ABI 6: the round-3 one-launch UNet sampling loop, ldm_unet_loop*, was retired -- at 0.53x the
+ * hipGraph of ldm_conv1d launches after the round-4 conv staging) */
 
 /* ---- C18 marching cubes on a decoded volume ---------------------------- */
 /* vol: fp32 [N][N][N] (z slowest, as decode writes it); a corner is inside when v < level.

@@ -1,5 +1,6 @@
-// Device-side synchronisation of the persistent XCD-replica loops (the MLP sampler's
-// sample_replica_kernel in sample_loop.hip, the 1D-UNet's unet_loop_kernel in unet.hip):
+// Device-side synchronisation of the persistent XCD-replica loop (the MLP sampler's
+// sample_replica_kernel in sample_loop.hip; the 1D-UNet's loop that also used it was retired
+// in round 4):
 // bounded spins, the start-up census that places a workgroup on its XCD, and the XCD-local
 // barrier between dependent phases.  Hand-off rules (MI355X guide, Guideline 16 table row 1):
 // every handed-off byte is stored sc1 and drained (s_waitcnt vmcnt(0)) before ONE lane of the

@@ -21,24 +21,19 @@
 //     chunks of 16) and their partial tiles are summed in a fixed order through LDS, so the
 //     result is deterministic;
 //   * every input window and weight slice of the launch is staged in LDS in ONE round trip
-//     (loads of a segment issued back to back before their LDS stores), then one barrier,
+//     (the direct staging below: every segment's loads issued before any LDS store; the
+//     generic staging, for other shapes, one round trip per segment part), then one barrier,
 //     then the MFMA loop runs from LDS only;
 //   * LDS layouts put each lane's operands for 4 consecutive MFMAs in one ds_read_b128:
 //     channels are permuted inside every group of 16 (perm16) on staging, and the weights
 //     arrive already permuted from the host packing (ldm_sdf/ops.py pack_conv_weight).
 #include "ldm_internal.h"
 #include "ddpm_common.h"
-#include "loop_sync.h"
 
 #include <string.h>
 
-#include <atomic>
-#include <mutex>
-#include <vector>
-
-// Diagnostic build only (-DUNET_STAMP=1, scripts/stamp_unet.py): thread 0 of the workgroup
-// running tile 0 of XCD 0 stamps s_memrealtime (100 MHz) at the points of every phase of the
-// SECOND step into the debug tail of the workspace, which nothing else reads.
+// Diagnostic build only (-DUNET_STAMP=1, scripts/stamp_conv.py): workgroup (0, 0, 0) of every
+// ldm_conv1d launch stamps s_memrealtime (100 MHz) at its phase boundaries (StampRegs).
 #ifndef UNET_STAMP
 #define UNET_STAMP 0
 #endif
@@ -73,9 +68,9 @@ struct ConvPlan {
 };
 
 // The device code reads a call's arguments and plan through the CONSTANT address space (the
-// kernarg segment for ldm_conv1d, the uploaded program for the loop), so every field is a
-// scalar load into SGPRs; through a generic pointer each field was a vector load with its own
-// memory wait (the loop's first version: 15.7 us per conv phase).
+// kernarg segment), so every field is a scalar load into SGPRs; through a generic pointer each
+// field was a vector load with its own memory wait (15.7 us per conv in the round-3 one-launch
+// loop, since retired: DESIGN.md §9).
 #define LDM_KC __attribute__((address_space(4)))
 typedef const LDM_KC ldm_conv1d_args_t KConv;
 typedef const LDM_KC ldm_conv1d_seg_t KSeg;
@@ -87,21 +82,6 @@ typedef const LDM_KC ConvPlan KPlan;
 // are skipped (exec-masked: a store needs no wait where the branch rejoins, and a common scratch
 // address made the idle lanes' stores one LDS bank-conflict chain).  The slot count NB is picked per segment from the
 // real item count (4 / 8 / 16 / 32), so a small segment does not pay a 32-slot unroll.
-// HO (hand-off): the input was written by another workgroup of the same launch (the
-// persistent loop): every load of it is an sc1 (L1-bypassing) load, loop_sync.h's rule.
-#ifndef UNET_PLAIN_LD
-#define UNET_PLAIN_LD 0       // diagnostic A/B only: plain loads for the hand-off (NOT coherent)
-#endif
-template <bool HO>
-__device__ __forceinline__ float ld_act(const float* p) {
-    if constexpr (HO && !UNET_PLAIN_LD)
-        return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<const unsigned*>(p),
-                                                           __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT));
-    else
-        return *p;
-}
-
 // SiLU of a staged input: x * rcp(1 + 2^(-x log2 e)) on the transcendental unit (a few
 // instructions; the IEEE expf + division form was the dominant cost of staging, which is
 // VALU-latency-bound at one wave per SIMD).  Within 2 ulp of x / (1 + e^-x); the oracle
@@ -115,7 +95,7 @@ __device__ __forceinline__ float silu_stage(float x) {
 // incrementally (no per-item division), every load of a pass issued before its LDS stores
 // (one global round trip per pass), branch-free (clamped address + select).  Channels
 // C..cinp-1 and positions outside [0, Lsrc) stage zeros.
-template <int NB, bool HO>
+template <int NB>
 __device__ __forceinline__ void stage_x_nb(float* __restrict__ xs,
                                            KSeg& s, const float* Xs, KSegPlan& p, int b,
                                            int pos0) {
@@ -139,7 +119,7 @@ __device__ __forceinline__ void stage_x_nb(float* __restrict__ xs,
             const bool in = ci < cinp;
             const bool ok = ci < C && pp >= 0 && pp < Lsrc;
             const int src = ok ? ci * L_in + (up2 ? (pp >> 1) : pp) : 0;
-            v[u] = ld_act<HO>(X + src);      // consumed only in the store pass below
+            v[u] = *(X + src);      // consumed only in the store pass below
             okm |= (uint64_t)ok << u;
             dst[u] = in ? j * ld + perm16(ci) : -1;
             // branch-free advance: a divergent branch here made the compiler drain every load
@@ -164,8 +144,8 @@ __device__ __forceinline__ void stage_x_nb(float* __restrict__ xs,
 // VALU-bound at ~38 instructions per element, one wave per SIMD).  Raw buffer loads over the
 // shape's [C][L_in] block: channels ci >= C fall outside it and read 0; positions outside
 // [0, L_in) are masked per element.  UP2 writes every source element to its two window
-// positions.  HO: sc1 loads (cache policy 16), L1-bypassing like ld_act.
-template <int NB, bool HO>
+// positions.
+template <int NB>
 __device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs,
                                                KSeg& s, const float* Xs, KSegPlan& p, int b,
                                                int pos0) {
@@ -191,7 +171,7 @@ __device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs,
         for (int u = 0; u < NB; ++u) {
             const int off = ci * L_in + a0 + 4 * g;            // < 0 only for ci = 0: OOB -> 0
             v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 rs, (uint32_t)off * 4u, 0, HO ? 16 : 0));
+                                                 rs, (uint32_t)off * 4u, 0, 0));
             cg[u] = ci < cinp ? (ci << 8) | g : -1;
             g += dr;
             const int wrap = g >= ng ? 1 : 0;
@@ -219,23 +199,22 @@ __device__ __forceinline__ void stage_x_vec_nb(float* __restrict__ xs,
     }
 }
 
-template <bool HO>
 __device__ __forceinline__ void stage_x(float* xs, KSeg& s, const float* X,
                                         KSegPlan& p, int b, int pos0) {
     if ((s.L_in & 3) == 0 && ((uintptr_t)X & 15) == 0) {
         const int ng = (p.win + 6) / 4 + 2;               // bound of the source groups per row
         const int n = (p.cinp * ng + 255) / 256;
-        if (n <= 2) stage_x_vec_nb<2, HO>(xs, s, X, p, b, pos0);
-        else if (n <= 5) stage_x_vec_nb<5, HO>(xs, s, X, p, b, pos0);
-        else if (n <= 10) stage_x_vec_nb<10, HO>(xs, s, X, p, b, pos0);
-        else stage_x_vec_nb<18, HO>(xs, s, X, p, b, pos0);
+        if (n <= 2) stage_x_vec_nb<2>(xs, s, X, p, b, pos0);
+        else if (n <= 5) stage_x_vec_nb<5>(xs, s, X, p, b, pos0);
+        else if (n <= 10) stage_x_vec_nb<10>(xs, s, X, p, b, pos0);
+        else stage_x_vec_nb<18>(xs, s, X, p, b, pos0);
         return;
     }
     const int n = (p.cinp * p.win + 255) / 256;      // items per thread
-    if (n <= 4) stage_x_nb<4, HO>(xs, s, X, p, b, pos0);
-    else if (n <= 9) stage_x_nb<9, HO>(xs, s, X, p, b, pos0);
-    else if (n <= 17) stage_x_nb<17, HO>(xs, s, X, p, b, pos0);
-    else stage_x_nb<34, HO>(xs, s, X, p, b, pos0);
+    if (n <= 4) stage_x_nb<4>(xs, s, X, p, b, pos0);
+    else if (n <= 9) stage_x_nb<9>(xs, s, X, p, b, pos0);
+    else if (n <= 17) stage_x_nb<17>(xs, s, X, p, b, pos0);
+    else stage_x_nb<34>(xs, s, X, p, b, pos0);
 }
 
 // Weights: 16-byte vector loads along a packed row (4 fp32 or 8 bf16 channels per load).
@@ -312,9 +291,8 @@ __device__ __forceinline__ void stage_w(float* ws, KSeg& s, KSegPlan& p,
     else stage_w_nb<TW, 8>(ws, s, p, co0);
 }
 
-// The operands of one conv call that the persistent loop moves with the step (the per-launch
-// kernel passes the call's own): seg[0]'s input, the per-channel bias row, and the output /
-// x_t / noise / t of the DDPM epilogue.
+// The epilogue-side operands of one conv call: seg[0]'s input, the per-channel bias row, and
+// the output / x_t / noise / t of the DDPM epilogue.
 struct ConvIO {
     const float* x0;
     const float* cbias;
@@ -328,18 +306,9 @@ __device__ __forceinline__ ConvIO conv_io(KConv& a) {
     return {a.seg[0].X, a.cbias, a.Y, a.xlat, a.z, a.t};
 }
 
-// Diagnostic stamps (UNET_STAMP builds only; every mark compiles away otherwise).  StampPtr
-// writes s_memrealtime into the loop's debug tail as it goes (marks 1 and 2; 6 and 7 with ext);
-// StampRegs keeps the launch kernel's marks in registers and writes them at the kernel's end,
-// so the slot's atomic and the stores stay out of the timed path.
-struct StampPtr {
-    uint64_t* p;
-    bool ext;
-    __device__ __forceinline__ void mark(int k) {
-        if (UNET_STAMP && p && threadIdx.x == 0 && k < 8 && (ext || k <= 2))
-            p[k] = __builtin_amdgcn_s_memrealtime();
-    }
-};
+// Diagnostic stamps (UNET_STAMP builds only; every mark compiles away otherwise): workgroup
+// (0, 0, 0) keeps s_memrealtime marks in registers and writes them at the kernel's end, so the
+// slot's atomic and the stores stay out of the timed path.
 struct StampRegs {
     bool on;
     uint64_t t[16];
@@ -362,7 +331,7 @@ struct EpiOps {
     float c1, c2, sg;
 };
 
-template <int TP, bool HO>
+template <int TP>
 __device__ __forceinline__ void epi_load(EpiOps<TP>& e, KConv& a, const ConvIO& io, int pos0,
                                          int co0, int b) {
     const int tid = threadIdx.x;
@@ -380,8 +349,8 @@ __device__ __forceinline__ void epi_load(EpiOps<TP>& e, KConv& a, const ConvIO& 
         e.b1[k] = *(a.bias ? a.bias + coc : dummy);
         e.b2[k] = *(a.bias2 ? a.bias2 + coc : dummy);
         e.b3[k] = *(io.cbias ? io.cbias + (int64_t)b * a.scb + coc : dummy);
-        e.r[k] = ld_act<HO>(a.R ? a.R + idx : dummy);
-        e.x[k] = ld_act<HO>(ddpm ? io.xlat + idx : dummy);
+        e.r[k] = *(a.R ? a.R + idx : dummy);
+        e.x[k] = *(ddpm ? io.xlat + idx : dummy);
         e.z[k] = *(noise ? io.z + idx : dummy);
     }
     // batch-uniform: scalar loads (the tables are not written during the launch)
@@ -392,8 +361,7 @@ __device__ __forceinline__ void epi_load(EpiOps<TP>& e, KConv& a, const ConvIO& 
 
 // The tile after its operands are staged (and the staging barrier passed): the MFMA
 // contraction split over the 4 waves, the partial tiles summed in wave order, the fused
-// epilogue.  Ends with every LDS read done by its own wave only: a caller running another tile
-// on the same LDS first passes a workgroup barrier.
+// epilogue.
 template <typename TW, int TP, typename ST>
 __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& io, float* sm,
                                             int pos0, int co0, int b, const EpiOps<TP>& e,
@@ -408,9 +376,9 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
     // on two accumulator sets (chunk pairs alternate, so the MFMA chains interleave instead of
     // each MFMA waiting out its predecessor's 40-cycle latency), the next pair's operands read
     // from LDS before this pair's MFMAs, and the segment geometry (plan fields: scalar loads)
-    // re-read only when a segment changes -- the loop read them per chunk and waited on every
-    // LDS read (the MFMA phase was ~25 % of the step).  The two sets are
-    // added at the end, so per output the sum order is fixed (graph == loop, bit for bit).
+    // re-read only when a segment changes -- the first form read them per chunk and waited on
+    // every LDS read (the MFMA phase was ~25 % of the step).  The two sets
+    // are added at the end, so per output the sum order is fixed (deterministic).
     f32x4 acc0[NT], acc1[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -524,29 +492,6 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_.mark(7);
     }
-}
-
-// One output tile (16 channels x TP positions of shape b) of a conv call, the persistent
-// loop's form: stage every segment's input window and weights in LDS (stage_w / stage_x: one
-// round trip per part), the epilogue operands behind the staging barrier, then conv_finish.
-// HO: the loop's hand-off form (sc1 loads of activations written inside the launch).
-// w_staged: the weights of this (call, co0) already sit in LDS (the loop prefetches them).
-template <typename TW, int TP, bool HO>
-__device__ __forceinline__ void conv_tile(KConv& a, KPlan& pl,
-                                          const ConvIO& io, float* sm, int pos0, int co0,
-                                          int b, bool w_staged = false,
-                                          uint64_t* stp = nullptr, bool stp_ext = false) {
-    for (int si = 0; si < a.n_seg; ++si) {
-        if (!w_staged) stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
-        stage_x<HO>(sm + pl.s[si].xoff, a.seg[si], si == 0 ? io.x0 : a.seg[si].X,
-                    pl.s[si], b, pos0);
-    }
-    __syncthreads();
-    StampPtr sp{stp, stp_ext};
-    sp.mark(1);
-    EpiOps<TP> e;
-    epi_load<TP, HO>(e, a, io, pos0, co0, b);
-    conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sp);
 }
 
 // ---- direct staging: the ldm_conv1d launch kernel -----------------
@@ -717,14 +662,14 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
     for (int si = 0; si < a.n_seg; ++si) {
         stage_w<TW>(sm + pl.s[si].woff, a.seg[si], pl.s[si], co0);
         if (si == 0) sr.mark(3);
-        stage_x<false>(sm + pl.s[si].xoff, a.seg[si], a.seg[si].X, pl.s[si], b, pos0);
+        stage_x(sm + pl.s[si].xoff, a.seg[si], a.seg[si].X, pl.s[si], b, pos0);
         if (si == 0) sr.mark(4);
     }
     sr.mark(5);
     __syncthreads();
     sr.mark(1);
     EpiOps<TP> e;
-    epi_load<TP, false>(e, a, io, pos0, co0, b);
+    epi_load<TP>(e, a, io, pos0, co0, b);
     conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sr);
 #if UNET_STAMP
     stamps_flush(sr);
@@ -760,7 +705,7 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
         fast_x_issue<NBX>(xv[si], a.seg[si], pl.s[si], a.seg[si].X, b, pos0, 0);
     }
     EpiOps<TP> e;
-    epi_load<TP, false>(e, a, io, pos0, co0, b);
+    epi_load<TP>(e, a, io, pos0, co0, b);
     // keep every load above issued before the first use of any of them below: the scheduler
     // otherwise pairs each segment's stores with its loads, or hoists the first bf16 unpack
     // above the window loads -- either is a wait for the data in the middle of the issue, one
@@ -894,149 +839,7 @@ int launch_conv(const ldm_conv1d_args_t& a, hipStream_t s) {
     return launch_tp<TW, 16>(a, s);
 }
 
-// ---- C17 sampling loop: the whole reverse loop as one launch ---------------------------------
-// One replica of the step's conv program per XCD (64 workgroups, two per CU, the shapes
-// b = xcd mod 8); every conv is a phase whose 16-channel x 32-position tiles (kLoopTP) the
-// replica's workgroups deal among themselves, then an XCD-local barrier (loop_sync.h) hands the
-// output to the next phase.  At the UNet's sizes (C x L = 32768 at every level) a phase is 64
-// tiles per shape: one tile per workgroup, so a step costs 18 barrier-separated tile rounds
-// instead of 18 dependent launches.  Activations are handed off with sc1 stores / sc1 loads; weights,
-// biases, tables and noise are never written inside the launch and use plain loads.
-constexpr int kStampPts = 6;
-static_assert(LDM_UNET_MAX_PHASES * kStampPts * 8 <= 4096, "stamps fit the debug tail");
-#ifndef UNET_LOOP_TP
-#define UNET_LOOP_TP 32
-#endif
-constexpr int kLoopTP = UNET_LOOP_TP;           // positions per tile
-constexpr int kLoopPerCU = kLoopTP == 64 ? 1 : 2;   // workgroups per CU
-constexpr int kLoopGrid = 256 * kLoopPerCU;      // 8 XCDs x 32 CUs x kLoopPerCU
-constexpr int kLoopLdsBytes = (kLoopPerCU == 1 ? 150 : 78) * 1024;   // every plan fits
-constexpr unsigned kLoopSpin = 1u << 22;
-
-struct LoopPhase {
-    ldm_conv1d_args_t a;
-    ConvPlan pl;
-    int32_t patch, tiles_l, tiles_c, reserved;
-    int64_t cb_tstride;
-};
-
-// Program header, written by ldm_unet_loop_prepare between the sync words and the phase table
-// (outside the region memset before each launch): the launch's arguments must match the
-// program it runs, or every workgroup returns before touching a buffer (status 3).
-struct LoopHeader {
-    int32_t magic, n_phase, w_dtype, B, D, reserved[59];
-};
-static_assert(sizeof(LoopHeader) == 256, "header keeps the phase table 256-B aligned");
-constexpr int32_t kLoopMagic = 0x554e4554;   // "UNET"
-constexpr unsigned kStatusMismatch = 3u;
-
-struct UnetLoopArgs {
-    uint64_t ph;                 // device address of the uploaded LoopPhase table
-    int n_phase;
-    float* x2;
-    const float* noise;
-    int B, D, t_hi, steps;
-    unsigned* sync;
-    unsigned spin_limit;
-    uint64_t* stamp;             // UNET_STAMP builds: the workspace's debug tail
-};
-
-template <typename TW>
-__global__ __launch_bounds__(256) void unet_loop_kernel(UnetLoopArgs la) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    __shared__ unsigned s_xcc, s_rank;
-    __shared__ int s_ok;
-    unsigned* sync = la.sync;
-    const unsigned G = gridDim.x;
-    {   // the program must be the one these arguments describe (uniform: all or none return)
-        const LDM_KC LoopHeader* hd = (const LDM_KC LoopHeader*)(la.ph - sizeof(LoopHeader));
-        const int wdt = sizeof(TW) == 2 ? LDM_BF16 : LDM_F32;
-        if (hd->magic != kLoopMagic || hd->n_phase != la.n_phase || hd->w_dtype != wdt ||
-            hd->B != la.B || hd->D != la.D) {
-            if (blockIdx.x == 0 && threadIdx.x == 0)
-                __hip_atomic_store(sync + 32 * lsync::R_STATUS, kStatusMismatch, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-    }
-    if (threadIdx.x == 0) {
-        unsigned xcc, rank;
-        s_ok = lsync::replica_census(sync, G, la.spin_limit, &xcc, &rank);
-        s_xcc = xcc;
-        s_rank = rank;
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    const int xcc = (int)s_xcc, rank = (int)s_rank, nloc = (int)G / 8;
-    const int nsh = la.B > xcc ? (la.B - 1 - xcc) / 8 + 1 : 0;   // shapes of this replica
-    if (nsh == 0) return;                                           // idle replica (B < 8)
-    const int64_t xstride = (int64_t)la.B * la.D;
-    const LDM_KC LoopPhase* ph = (const LDM_KC LoopPhase*)la.ph;
-    unsigned* status = sync + 32 * lsync::R_STATUS;
-    unsigned* gen = sync + 32 * (lsync::R_GEN + xcc);
-    unsigned phase = 0;
-    bool w_next = false;             // the first tile's weights of the coming phase are in LDS
-    for (int st = 0; st < la.steps; ++st) {
-        const int t = la.t_hi - st, cur = st & 1;
-        for (int p = 0; p < la.n_phase; ++p) {
-            const LDM_KC LoopPhase& P = ph[p];
-            ConvIO io = conv_io(P.a);
-            if (P.patch & LDM_UNET_PATCH_X) io.x0 = la.x2 + cur * xstride;
-            if (P.patch & LDM_UNET_PATCH_STEP) {
-                io.Y = la.x2 + (cur ^ 1) * xstride;
-                io.xlat = la.x2 + cur * xstride;
-                io.z = la.noise + (int64_t)t * xstride;
-                io.t = t;
-            }
-            if (P.patch & LDM_UNET_PATCH_CBIAS) io.cbias = P.a.cbias + (int64_t)t * P.cb_tstride;
-            uint64_t* stp = nullptr;
-            if (UNET_STAMP && st == 1 && xcc == 0 && rank == 0)
-                stp = la.stamp + (size_t)p * kStampPts;
-            if (UNET_STAMP && stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
-            const int per = P.tiles_l * P.tiles_c, ntile = nsh * per;
-            for (int tile = rank; tile < ntile; tile += nloc) {
-                const int j = tile / per, r = tile - j * per;
-                const int ct = r / P.tiles_l, lt = r - ct * P.tiles_l;
-                if (tile != rank) __syncthreads();   // the previous tile's LDS reads are done
-                conv_tile<TW, kLoopTP, true>(P.a, P.pl, io, sm, lt * kLoopTP, ct * 16,
-                                             xcc + 8 * j, w_next && tile == rank,
-                                             tile == rank ? stp : nullptr);
-            }
-            if (UNET_STAMP && stp && threadIdx.x == 0) stp[3] = __builtin_amdgcn_s_memrealtime();
-            // XCD-local barrier (loop_sync.h replica_sync, split): drain this workgroup's
-            // output stores, arrive, and while the other workgroups finish, stage the weights of
-            // the next phase's first tile (they do not depend on this phase) into LDS.
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();                         // every LDS read of this phase is done
-            if (UNET_STAMP && stp && threadIdx.x == 0) stp[4] = __builtin_amdgcn_s_memrealtime();
-            ++phase;
-            bool last = false;
-            if (threadIdx.x == 0) {
-                const unsigned a = __hip_atomic_fetch_add(sync + 32 * (lsync::R_ARR + xcc), 1u,
-                                                          __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                last = a + 1 == phase * (unsigned)nloc;
-                if (last)
-                    __hip_atomic_store(gen, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            const int pn = p + 1 < la.n_phase ? p + 1 : 0;
-            const LDM_KC LoopPhase& N = ph[pn];
-            w_next = (st + 1 < la.steps || pn != 0) && rank < nsh * N.tiles_l * N.tiles_c;
-            if (w_next) {
-                const int ct = (rank % (N.tiles_l * N.tiles_c)) / N.tiles_l;
-                for (int si = 0; si < N.a.n_seg; ++si)
-                    stage_w<TW>(sm + N.pl.s[si].woff, N.a.seg[si], N.pl.s[si], ct * 16);
-            }
-            if (UNET_STAMP && stp && threadIdx.x == 0) stp[5] = __builtin_amdgcn_s_memrealtime();
-            if (threadIdx.x == 0)
-                s_ok = last || lsync::spin_until(gen, phase, status, la.spin_limit);
-            __syncthreads();
-            if (!s_ok) return;
-        }
-    }
-}
-
-// The checks ldm_conv1d makes on one call (shared with the loop's program check).
+// The checks ldm_conv1d makes on one call.
 int check_conv_args(const ldm_conv1d_args_t* a) {
     LDM_REQUIRE(a && a->Y && a->B >= 1 && a->Cout >= 1 && a->L_out >= 1, LDM_EINVAL,
                 "bad conv1d args");
@@ -1067,40 +870,6 @@ int check_conv_args(const ldm_conv1d_args_t* a) {
     return 0;
 }
 
-// ldm_unet_loop_config (fault-injection tests only): the barrier spin limit per device
-constexpr int kLoopMaxDev = 64;
-std::atomic<unsigned> g_loop_spin[kLoopMaxDev];
-
-template <typename TW>
-int launch_unet_loop(const UnetLoopArgs& la, hipStream_t s) {
-    auto* k = &unet_loop_kernel<TW>;
-    constexpr int kMaxDev = 64;
-    static std::once_flag once[kMaxDev];
-    static int init_err[kMaxDev];
-    int dev = 0;
-    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev, LDM_EINVAL,
-                "ldm_unet_loop: no current device");
-    std::call_once(once[dev], [&] {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           kLoopLdsBytes);
-        int cus = 0, per_cu = 0;
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, reinterpret_cast<const void*>(k), 256, kLoopLdsBytes);
-        init_err[dev] = e != hipSuccess ? (int)e
-                        : (cus != 256 || per_cu < kLoopPerCU) ? LDM_ENOSYS : 0;
-    });
-    LDM_REQUIRE(init_err[dev] == 0, init_err[dev],
-                "ldm_unet_loop: needs 256 CUs with %d %d-byte workgroups each (MI355X): %d",
-                kLoopPerCU, kLoopLdsBytes, init_err[dev]);
-    hipError_t e = hipMemsetAsync(la.sync, 0, lsync::kSyncBytes, s);
-    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop: memset: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(k, dim3(kLoopGrid), dim3(256), kLoopLdsBytes, s, la);
-    return launch_status("ldm_unet_loop");
-}
-
 }  // namespace
 }  // namespace ldm
 
@@ -1121,116 +890,3 @@ extern "C" int ldm_dev_conv_stamps(uint64_t* host, unsigned* n) {
     return 0;
 }
 #endif
-
-extern "C" size_t ldm_unet_loop_ws_bytes(int n_phase) {
-    if (n_phase < 1 || n_phase > LDM_UNET_MAX_PHASES) return 0;
-    // sync words | program header | phase table | a 4 KiB debug tail (written only by the
-    // UNET_STAMP diagnostic build)
-    return ldm::lsync::kSyncBytes + sizeof(ldm::LoopHeader) +
-           (size_t)n_phase * sizeof(ldm::LoopPhase) + 4096;
-}
-
-extern "C" int ldm_unet_loop_prepare(const ldm_unet_phase_t* ph, int n_phase, void* ws,
-                                     size_t ws_bytes, ldm_stream_t s) {
-    using namespace ldm;
-    LDM_REQUIRE(ph && n_phase >= 1 && n_phase <= LDM_UNET_MAX_PHASES, LDM_EINVAL,
-                "ldm_unet_loop_prepare: n_phase %d", n_phase);
-    LDM_REQUIRE(ws && LDM_ALIGNED(ws, 256) && ws_bytes >= ldm_unet_loop_ws_bytes(n_phase),
-                LDM_EINVAL, "ldm_unet_loop_prepare: ws must be 256-B aligned, >= %zu bytes",
-                ldm_unet_loop_ws_bytes(n_phase));
-    std::vector<LoopPhase> h((size_t)n_phase);
-    for (int p = 0; p < n_phase; ++p) {
-        const ldm_unet_phase_t& q = ph[p];
-        LDM_TRY(check_conv_args(&q.conv));
-        LDM_REQUIRE(q.conv.w_dtype == ph[0].conv.w_dtype && q.conv.B == ph[0].conv.B,
-                    LDM_EINVAL, "ldm_unet_loop_prepare: phase %d: w_dtype / B differ from phase 0",
-                    p);
-        LDM_REQUIRE((q.patch & ~(LDM_UNET_PATCH_X | LDM_UNET_PATCH_STEP |
-                                 LDM_UNET_PATCH_CBIAS)) == 0 &&
-                        (!(q.patch & LDM_UNET_PATCH_STEP) || q.conv.epi == LDM_CONV_EPI_DDPM) &&
-                        (!(q.patch & LDM_UNET_PATCH_CBIAS) ||
-                         (q.conv.cbias && q.conv.scb == 0 && q.cb_tstride >= 0)),
-                    LDM_EINVAL, "ldm_unet_loop_prepare: phase %d: patch 0x%x", p, q.patch);
-        LoopPhase& L = h[(size_t)p];
-        memset(&L, 0, sizeof(L));
-        L.a = q.conv;
-        int lds = 0;
-        LDM_REQUIRE(make_plan(q.conv, kLoopTP, &L.pl, &lds) == 0 && lds <= kLoopLdsBytes,
-                    LDM_ENOSPC, "ldm_unet_loop_prepare: phase %d needs %d B of LDS (> %d)", p,
-                    lds, kLoopLdsBytes);
-        L.patch = q.patch;
-        L.tiles_l = (q.conv.L_out + kLoopTP - 1) / kLoopTP;
-        L.tiles_c = (q.conv.Cout + 15) / 16;
-        L.cb_tstride = q.cb_tstride;
-    }
-    LoopHeader hd;
-    memset(&hd, 0, sizeof(hd));
-    hd.magic = kLoopMagic;
-    hd.n_phase = n_phase;
-    hd.w_dtype = ph[0].conv.w_dtype;
-    hd.B = ph[0].conv.B;
-    hd.D = ph[0].conv.seg[0].L_in;
-    std::vector<char> blob(sizeof(LoopHeader) + h.size() * sizeof(LoopPhase));
-    memcpy(blob.data(), &hd, sizeof(hd));
-    memcpy(blob.data() + sizeof(hd), h.data(), h.size() * sizeof(LoopPhase));
-    char* dst = reinterpret_cast<char*>(ws) + lsync::kSyncBytes;
-    hipError_t e = hipMemcpyAsync(dst, blob.data(), blob.size(), hipMemcpyHostToDevice,
-                                  (hipStream_t)s);
-    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
-    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop_prepare: upload: %s",
-                hipGetErrorString(e));
-    return 0;
-}
-
-extern "C" int ldm_unet_loop(int n_phase, int w_dtype, float* x2, const float* noise, int B,
-                             int D, int t_hi, int steps, void* ws, size_t ws_bytes,
-                             ldm_stream_t s) {
-    using namespace ldm;
-    LDM_REQUIRE(n_phase >= 1 && n_phase <= LDM_UNET_MAX_PHASES && x2 && noise && ws &&
-                    LDM_ALIGNED(ws, 256) && ws_bytes >= ldm_unet_loop_ws_bytes(n_phase),
-                LDM_EINVAL, "ldm_unet_loop: bad program / buffers");
-    LDM_REQUIRE(B >= 1 && B <= 16 && D >= 1 && steps >= 1 && t_hi >= steps - 1, LDM_EINVAL,
-                "ldm_unet_loop: B %d (1..16), D %d, t_hi %d, steps %d", B, D, t_hi, steps);
-    LDM_REQUIRE(w_dtype == LDM_F32 || w_dtype == LDM_BF16, LDM_EINVAL,
-                "ldm_unet_loop: w_dtype %d", w_dtype);
-    UnetLoopArgs la;
-    la.sync = reinterpret_cast<unsigned*>(ws);
-    la.ph = (uint64_t)(uintptr_t)(reinterpret_cast<char*>(ws) + lsync::kSyncBytes +
-                                  sizeof(LoopHeader));
-    la.n_phase = n_phase;
-    la.x2 = x2;
-    la.noise = noise;
-    la.B = B;
-    la.D = D;
-    la.t_hi = t_hi;
-    la.steps = steps;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLoopMaxDev) dev = 0;
-    const unsigned forced = g_loop_spin[dev].load();
-    la.spin_limit = forced ? forced : kLoopSpin;
-    la.stamp = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + lsync::kSyncBytes +
-                                           sizeof(LoopHeader) +
-                                           (size_t)n_phase * sizeof(LoopPhase));
-    if (w_dtype == LDM_BF16) return launch_unet_loop<unsigned short>(la, (hipStream_t)s);
-    return launch_unet_loop<float>(la, (hipStream_t)s);
-}
-
-extern "C" int ldm_unet_loop_status(const void* ws, unsigned* status_host, ldm_stream_t s) {
-    using namespace ldm;
-    LDM_REQUIRE(ws && status_host, LDM_EINVAL, "ldm_unet_loop_status: null argument");
-    const unsigned* w = reinterpret_cast<const unsigned*>(ws) + 32 * lsync::R_STATUS;
-    hipError_t e = hipMemcpyAsync(status_host, w, sizeof(unsigned), hipMemcpyDeviceToHost,
-                                  (hipStream_t)s);
-    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)s);
-    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_unet_loop_status: %s", hipGetErrorString(e));
-    return 0;
-}
-
-extern "C" int ldm_unet_loop_config(unsigned spin_limit) {
-    using namespace ldm;
-    int dev = 0;
-    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kLoopMaxDev, LDM_EINVAL,
-                "ldm_unet_loop_config: no current device");
-    g_loop_spin[dev].store(spin_limit);
-    return 0;
-}

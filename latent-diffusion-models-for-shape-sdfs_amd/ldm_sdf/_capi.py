@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("LDM_SDF_LIB", LIB_PATH)
 HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                             "..", "..", "include", "ldm_sdf.h"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6   # 6: ldm_unet_loop* retired
 LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER, LAYOUT_SPLIT, LAYOUT_SPLIT16 = 0, 1, 2, 3
@@ -132,15 +132,6 @@ class ConvArgs(C.Structure):
                 ("c1", _vp), ("c2", _vp), ("sigma", _vp), ("t", C.c_int32)]
 
 
-UNET_PATCH_X, UNET_PATCH_STEP, UNET_PATCH_CBIAS = 1, 2, 4
-UNET_MAX_PHASES = 32
-
-
-class UnetPhase(C.Structure):
-    _fields_ = [("conv", ConvArgs), ("patch", C.c_int32), ("reserved", C.c_int32),
-                ("cb_tstride", C.c_int64)]
-
-
 # (name, restype, argtypes) -- every symbol include/ldm_sdf.h declares.
 _i, _sz, _f = C.c_int, C.c_size_t, C.c_float
 SIGNATURES = [
@@ -178,11 +169,6 @@ SIGNATURES = [
     ("ldm_colsum_segments", _i, [_fp, _i, _i, _i, _fp, _i, _vp]),
     ("ldm_latent_l2_reg", _i, [_fp, _i, _i, _f, _fp, _fp, _vp]),
     ("ldm_conv1d", _i, [C.POINTER(ConvArgs), _vp]),
-    ("ldm_unet_loop_ws_bytes", _sz, [_i]),
-    ("ldm_unet_loop_prepare", _i, [C.POINTER(UnetPhase), _i, _vp, _sz, _vp]),
-    ("ldm_unet_loop", _i, [_i, _i, _fp, _fp, _i, _i, _i, _i, _vp, _sz, _vp]),
-    ("ldm_unet_loop_status", _i, [_vp, C.POINTER(C.c_uint), _vp]),
-    ("ldm_unet_loop_config", _i, [C.c_uint]),
     ("ldm_gemm_bf16", _i, [C.POINTER(GemmArgs), _vp]),
     ("ldm_denoiser_train_ws_bytes", _sz, [C.POINTER(Denoiser), _i]),
     ("ldm_denoiser_fwd", _i, [C.POINTER(Denoiser), _fp, _vp, _i, _fp, _vp, _vp]),

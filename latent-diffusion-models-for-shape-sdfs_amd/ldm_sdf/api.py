@@ -131,7 +131,8 @@ class Sampler:
         self.loop = None
         self.loop_fallbacks = 0
         # a denoiser whose loop does not beat its per-step graph at this batch (prefer_loop(n)
-        # False: the 1D-UNet) runs the graph unless the loop is asked for
+        # False) runs the graph unless the loop is asked for; the 1D-UNet has no loop (its
+        # one-launch loop was retired in round 4 at 0.53x the graph)
         prefer = getattr(denoiser, "prefer_loop", lambda n_: True)(n)
         if make_loop is not None and (persistent or (persistent is None and prefer)):
             self.loop = make_loop(n, dtype, self.device, self.sd["desc"])
@@ -157,9 +158,8 @@ class Sampler:
         left partially updated latents; status 2 (an XCD-replica loop found its workgroups
         placed other than one replica's worth per XCD) left them untouched.  After status 2
         the MLP sampler's library has switched the device to its chip-wide loop
-        (``loop.placement_fallback``); a denoiser with no chip-wide loop (the 1D-UNet) drops
-        its loop here, so later runs stay on the per-step graph instead of retrying the
-        launch.  With ``check`` (default) the status word is read back (one stream
+        (``loop.placement_fallback``); a loop without such a fallback is dropped here, so later
+        runs stay on the per-step graph instead of retrying the launch.  With ``check`` (default) the status word is read back (one stream
         synchronisation) and such a run is redone on the per-step path, which gives the same
         numbers bit for bit; ``loop_fallbacks`` counts these.  ``check=False`` keeps the call
         asynchronous: the caller then reads ``loop.status()`` itself."""

@@ -560,57 +560,6 @@ def conv1d_launch(a: capi.ConvArgs, device) -> None:
     capi.check(capi.load().ldm_conv1d(C.byref(a), capi.stream_handle(device)), "ldm_conv1d")
 
 
-def unet_loop_prepare(calls, patches, cb_tstrides, device) -> torch.Tensor:
-    """Upload one reverse step's conv program (``ldm_unet_loop_prepare``): ``calls`` are the
-    step's ``ConvArgs`` (``UNet1DDenoiser.step_args``), ``patches`` / ``cb_tstrides`` say which
-    fields follow the step (``LDM_UNET_PATCH_*``).  Returns the workspace holding it."""
-    n = len(calls)
-    if not 1 <= n <= capi.UNET_MAX_PHASES:
-        raise capi.LdmError(f"unet loop: 1..{capi.UNET_MAX_PHASES} convs, got {n}")
-    ph = (capi.UnetPhase * n)()
-    for i, (a, pt, cs) in enumerate(zip(calls, patches, cb_tstrides)):
-        ph[i].conv, ph[i].patch, ph[i].cb_tstride = a, int(pt), int(cs)
-    nbytes = int(capi.load().ldm_unet_loop_ws_bytes(n))
-    ws = torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32)
-    capi.check(capi.load().ldm_unet_loop_prepare(ph, n, ws.data_ptr(), ws.numel() * 4,
-                                                 capi.stream_handle(ws.device)),
-               "ldm_unet_loop_prepare")
-    return ws
-
-
-def unet_loop(ws: torch.Tensor, n_phase: int, w_dtype: int, x2: torch.Tensor,
-              noise: torch.Tensor, t_hi: int, steps: int) -> None:
-    """The whole reverse loop in one launch (``ldm_unet_loop``): ``x2 [2, B, D]`` holds x_T in
-    ``x2[0]`` and the result in ``x2[steps & 1]``; ``noise [T, B, D]``."""
-    _f32(x2, noise)
-    _contig(x2, noise)
-    if x2.dim() != 3 or x2.shape[0] != 2 or noise.dim() != 3 or noise.shape[1:] != x2.shape[1:]:
-        raise capi.LdmError("unet loop: x2 [2, B, D] and noise [T, B, D]")
-    capi.check(capi.load().ldm_unet_loop(int(n_phase), int(w_dtype), x2.data_ptr(),
-                                         noise.data_ptr(), x2.shape[1], x2.shape[2], int(t_hi),
-                                         int(steps), ws.data_ptr(), ws.numel() * 4,
-                                         capi.stream_handle(x2.device)),
-               "ldm_unet_loop")
-
-
-def unet_loop_config(spin_limit: int = 0) -> None:
-    """Fault-injection control of ``ldm_unet_loop`` on the current device (tests only): the
-    barrier spin limit (0: the default)."""
-    capi.check(capi.load().ldm_unet_loop_config(int(spin_limit)), "ldm_unet_loop_config")
-
-
-def unet_loop_status(ws: torch.Tensor) -> int:
-    """0 when the last ``unet_loop`` on ``ws`` completed, 1 when a barrier timed out, 2 when
-    its workgroups were not placed 64 per XCD (nothing computed), 3 when the launch's n_phase /
-    w_dtype / B / D differ from the program prepared in ``ws`` (nothing computed).
-    Synchronises the stream."""
-    st = C.c_uint(0)
-    capi.check(capi.load().ldm_unet_loop_status(ws.data_ptr(), C.byref(st),
-                                                capi.stream_handle(ws.device)),
-               "ldm_unet_loop_status")
-    return int(st.value)
-
-
 def conv1d(segs, Y: torch.Tensor, **kw) -> torch.Tensor:
     """``Y = epi(sum_seg conv(act(X_seg); W_seg) + biases (+ R))`` -- see include/ldm_sdf.h."""
     capi.require_device(Y, *[s.X for s in segs])

@@ -195,54 +195,6 @@ class UNet1DDenoiser:
             ops.conv1d_launch(a, x.device)
         return eps
 
-    def prefer_loop(self, n: int) -> bool:
-        """Whether ``Sampler`` uses the one-launch loop by default at batch n.  Measured on the
-        MI355X (profiles/r03e/unet_loop_ab*.log): the loop is 0.79x the hipGraph
-        of per-step launches at B = 1, 1.05x at B = 8 and 0.74x at B = 16 -- its 32 CUs per
-        shape are VALU/MFMA-throughput-bound where the graph spreads each conv over the chip --
-        so the graph stays the default and the loop is opt-in (``persistent=True``)."""
-        return False
-
-    def make_loop(self, n: int, dtype: str, device, sched_desc):
-        """Callable ``loop(x2, noise, t_hi, steps)`` running the whole reverse loop as ONE
-        persistent launch (``ldm_unet_loop``: one replica of the 18-conv step per XCD, an
-        XCD-local barrier between convs; bit-identical to the per-step launches), or None when
-        the batch has no such kernel (n > 16; the per-step stepper is used then)."""
-        if not 1 <= n <= 16:
-            return None
-        device = torch.device(device)
-        dev = self.device_pack(dtype, device)
-        buf = self.buffers(n, device)
-        # placeholders for the fields that follow the step (LDM_UNET_PATCH_*): the kernel
-        # replaces them with x2[cur], x2[cur ^ 1], noise[t] and t
-        xd = torch.zeros(2, n, self.D, device=device)
-        zd = torch.zeros(n, self.D, device=device)
-        calls = self.step_args(dev, buf, xd[0], 0, out=xd[1], sched=sched_desc, z=zd)
-        patches, strides = [], []
-        for i, a in enumerate(calls):
-            pt, cs = 0, 0
-            if i == 0:
-                pt |= capi.UNET_PATCH_X
-            if i == len(calls) - 1:
-                pt |= capi.UNET_PATCH_STEP
-            if a.cbias and a.scb == 0:          # E_i[0]: the base of the [T, Cout_i] table
-                pt |= capi.UNET_PATCH_CBIAS
-                cs = a.Cout
-            patches.append(pt)
-            strides.append(cs)
-        ws = ops.unet_loop_prepare(calls, patches, strides, device)
-        w_dtype = capi.DTYPE_CODES[dtype]
-        keep = (dev, buf, xd, zd, calls)
-
-        def loop(x2, noise, t_hi, steps):
-            ops.unet_loop(ws, len(calls), w_dtype, x2, noise, t_hi, steps)
-            return keep
-        loop.status = lambda: ops.unet_loop_status(ws)
-        loop.form = lambda: "unet-replica"
-        loop.placement_fallback = False          # no chip-wide UNet loop: status 2 -> graph
-        loop.ws = ws                              # (diagnostics: scripts/stamp_unet.py)
-        return loop
-
     def make_stepper(self, n: int, dtype: str, device, sched_desc):
         """Callable ``step(x, z, t, x_out)`` = one fused reverse step (for ``api.Sampler``)."""
         dev = self.device_pack(dtype, device)

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_error_path_without_gpu():
     from ldm_sdf import _capi as capi
     lib = capi.load()
-    assert lib.ldm_abi_version() == 5
+    assert lib.ldm_abi_version() == 6
     # argument validation runs before any device work
     assert lib.ldm_grid_coords(0, 0, 0, 0.0, 0.0, None, None) == -22
     assert b"bad grid slab" in lib.ldm_last_error()
@@ -61,8 +61,6 @@ def test_struct_layouts_match_c():
              offsetof(ldm_gemm_prob_t, loss_part));
       printf("%zu %zu %zu\n", offsetof(ldm_gemm_prob_t, ws), offsetof(ldm_gemm_prob_t, ldrb),
              offsetof(ldm_gemm_prob_t, slice_b));
-      printf("%zu %zu %zu\n", sizeof(ldm_unet_phase_t), offsetof(ldm_unet_phase_t, patch),
-             offsetof(ldm_unet_phase_t, cb_tstride));
       return 0; }
     '''
     tmp = "/tmp/ldm_layout_check"
@@ -88,11 +86,4 @@ def test_struct_layouts_match_c():
                             capi.GemmProb.loss_part.offset]
     assert sizes[17:20] == [capi.GemmProb.ws.offset, capi.GemmProb.ldrb.offset,
                             capi.GemmProb.slice_b.offset]
-    assert sizes[20:23] == [ctypes.sizeof(capi.UnetPhase), capi.UnetPhase.patch.offset,
-                            capi.UnetPhase.cb_tstride.offset]
-    # argument checks of the loop entry points run before any device work
-    lib = capi.load()
-    assert lib.ldm_unet_loop_ws_bytes(0) == 0 and lib.ldm_unet_loop_ws_bytes(33) == 0
-    assert lib.ldm_unet_loop_ws_bytes(18) > 4096
-    assert lib.ldm_unet_loop(18, 1, None, None, 1, 1024, 999, 1000, None, 0, None) == -22
-    assert lib.ldm_unet_loop_prepare(None, 18, None, 0, None) == -22
+    assert len(sizes) == 20

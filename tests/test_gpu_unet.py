@@ -178,7 +178,7 @@ def test_unet_forward_vs_golden(dev):
     assert e_r <= 1e-4 and e_u <= 0.1
 
 
-@pytest.mark.parametrize("path", ["eager", "graph", "loop"])
+@pytest.mark.parametrize("path", ["eager", "graph"])
 def test_unet_sampling_10_vs_golden(dev, path):
     import ldm_sdf
     gd = dict(np.load(os.path.join(GOLD, "unet_10.npz")))
@@ -188,8 +188,7 @@ def test_unet_sampling_10_vs_golden(dev, path):
     noise = torch.zeros(1000, 2, 1024)
     noise[1000 - steps:] = torch.from_numpy(gd["noise_tail"])
     x = ldm_sdf.sample(m, sch, 2, steps=steps, dtype="fp32", x_T=torch.from_numpy(gd["x_T"]),
-                       noise=noise, device=dev, use_graph=path == "graph",
-                       persistent=path == "loop").cpu().double()
+                       noise=noise, device=dev, use_graph=path == "graph").cpu().double()
     err = float((x - torch.from_numpy(gd["traj"][-1])).abs().max())
     assert err <= 1e-4, err
 
@@ -211,95 +210,11 @@ def test_unet_sampler_graph_equals_eager_bf16(dev):
     assert bool(torch.isfinite(ra).all())
 
 
-# The persistent loop (ldm_unet_loop): the same conv arithmetic per output
-# element as the per-step launches (32-position tiles instead of 16, the same contraction split
-# and wave-order sum), so the whole trajectory must be BIT-identical to the graph path --
-# including B > 8 (two shapes per XCD replica) and the full 1000 steps.
-@pytest.mark.parametrize("dtype,n,steps", [("bf16", 1, 1000), ("bf16", 3, 40), ("bf16", 9, 25),
-                                           ("bf16", 16, 12), ("fp32", 2, 30)])
-def test_unet_loop_bitwise_equals_graph(dev, dtype, n, steps):
+def test_unet_has_no_persistent_loop(dev):
+    """The round-3 one-launch loop was retired in round 4 (0.53x the graph after the direct conv
+    staging): asking for a persistent UNet sampler fails loudly."""
     import ldm_sdf
     m = ldm_sdf.UNet1DDenoiser(seed=2468)
-    sch = ldm_sdf.DDPMSchedule()
-    g = torch.Generator(device=dev).manual_seed(n)
-    xT = torch.randn(n, 1024, device=dev, generator=g)
-    noise = torch.randn(1000, n, 1024, device=dev, generator=g)
-    lp = ldm_sdf.Sampler(m, sch, n, steps=steps, dtype=dtype, device=dev, persistent=True)
-    gr = ldm_sdf.Sampler(m, sch, n, steps=steps, dtype=dtype, device=dev, persistent=False)
-    rl = lp.run(xT, noise).clone()
-    assert lp.loop.status() == 0 and lp.loop_fallbacks == 0
-    rg = gr.run(xT, noise).clone()
-    assert bool(torch.isfinite(rl).all())
-    assert torch.equal(rl, rg), float((rl - rg).abs().max())
-    # a second run on the same workspace (sync words re-zeroed per launch) repeats it exactly
-    assert torch.equal(lp.run(xT, noise), rl)
-
-
-def test_unet_loop_rejects_bad_program(dev):
-    import ldm_sdf
-    from ldm_sdf import _capi as capi, ops
-    m = ldm_sdf.UNet1DDenoiser(seed=2468)
-    assert m.make_loop(17, "bf16", dev, ldm_sdf.DDPMSchedule().device(dev)["desc"]) is None
-    sd = ldm_sdf.DDPMSchedule().device(dev)
-    dpk = m.device_pack("bf16", dev)
-    buf = m.buffers(1, dev)
-    x = torch.zeros(2, 1, 1024, device=dev)
-    calls = m.step_args(dpk, buf, x[0], 0, out=x[1], sched=sd["desc"], z=x[0])
-    with pytest.raises(capi.LdmError, match="patch"):        # STEP patch on a non-DDPM conv
-        ops.unet_loop_prepare(calls, [capi.UNET_PATCH_STEP] + [0] * 17, [0] * 18, dev)
-    ws = ops.unet_loop_prepare(calls, [1] + [0] * 16 + [2], [0] * 18, dev)
-    with pytest.raises(capi.LdmError, match="t_hi"):
-        ops.unet_loop(ws, 18, capi.LDM_BF16, x, torch.zeros(1000, 1, 1024, device=dev), 5, 10)
-
-
-def test_unet_loop_rejects_launch_that_differs_from_program(dev):
-    """a launch whose B, n_phase or w_dtype differ from the program prepared in the
-    workspace (here at B = 1) must compute nothing and report status 3 -- before, a larger B
-    read and wrote past the program's intermediate buffers."""
-    import ldm_sdf
-    from ldm_sdf import _capi as capi, ops
-    m = ldm_sdf.UNet1DDenoiser(seed=2468)
-    sd = ldm_sdf.DDPMSchedule().device(dev)
-    dpk = m.device_pack("bf16", dev)
-    buf = m.buffers(1, dev)
-    x = torch.zeros(2, 1, 1024, device=dev)
-    calls = m.step_args(dpk, buf, x[0], 0, out=x[1], sched=sd["desc"], z=x[0])
-    ws = ops.unet_loop_prepare(calls, [1] + [0] * 16 + [2], [0] * 18, dev)
-    x4 = torch.full((2, 4, 1024), 7.0, device=dev)
-    noise4 = torch.zeros(1000, 4, 1024, device=dev)
-    for args in ((18, capi.LDM_BF16, x4, noise4),               # B 4 vs the program's 1
-                 (17, capi.LDM_BF16, x, noise4[:, :1]),         # n_phase
-                 (18, capi.LDM_F32, x, noise4[:, :1])):         # weight dtype
-        xin = args[2]
-        before = xin.clone()
-        ops.unet_loop(ws, args[0], args[1], xin, args[3].contiguous(), 999, 3)
-        assert ops.unet_loop_status(ws) == 3, args[:2]
-        assert torch.equal(xin, before)
-    # the matching launch runs
-    ops.unet_loop(ws, 18, capi.LDM_BF16, x, noise4[:, :1].contiguous(), 999, 3)
-    assert ops.unet_loop_status(ws) == 0
-
-
-def test_unet_loop_timeout_surfaces_and_falls_back(dev):
-    """A barrier that gives up (forced with a 1-poll spin limit) must surface as status 1 and
-    make Sampler re-run the sample on the per-step path: the same numbers as the graph."""
-    import ldm_sdf
-    from ldm_sdf import ops
-    m = ldm_sdf.UNet1DDenoiser(seed=2468)
-    sch = ldm_sdf.DDPMSchedule()
-    g = torch.Generator(device=dev).manual_seed(7)
-    xT = torch.randn(2, 1024, device=dev, generator=g)
-    noise = torch.randn(1000, 2, 1024, device=dev, generator=g)
-    ref = ldm_sdf.Sampler(m, sch, 2, steps=6, dtype="bf16", device=dev,
-                          persistent=False).run(xT, noise).clone()
-    lp = ldm_sdf.Sampler(m, sch, 2, steps=6, dtype="bf16", device=dev, persistent=True)
-    ops.unet_loop_config(1)
-    try:
-        with pytest.warns(RuntimeWarning, match="status 1"):
-            got = lp.run(xT, noise).clone()
-    finally:
-        ops.unet_loop_config(0)
-    assert lp.loop_fallbacks == 1
-    assert torch.equal(got, ref)
-    assert lp.loop.status() == 1           # the status word of the abandoned launch
-    assert torch.equal(lp.run(xT, noise), ref) and lp.loop.status() == 0
+    with pytest.raises(RuntimeError, match="no persistent"):
+        ldm_sdf.Sampler(m, ldm_sdf.DDPMSchedule(), 1, steps=5, dtype="bf16", device=dev,
+                        persistent=True)
