@@ -32,6 +32,8 @@
 
 #include <string.h>
 
+#include <type_traits>
+
 // Diagnostic build only (-DUNET_STAMP=1, scripts/stamp_conv.py): workgroup (0, 0, 0) of every
 // ldm_conv1d launch stamps s_memrealtime (100 MHz) at its phase boundaries (StampRegs).
 #ifndef UNET_STAMP
@@ -59,6 +61,9 @@ struct SegPlan {
     int nw;     // weight vectors of the tile: 16 rows x ksize taps x (1 << lgv)
     int lgng;   // log2 of the 4-position source groups staged per channel (>= the window's)
     int nx;     // window items (4 channels x 4 positions each): cinp / 4 << lgng
+    // the contraction's geometry packed for the launch kernel (FastGeo): ch0 | ksize << 12 |
+    // (stride - 1) << 15 | cinp << 16, and woff | xoff << 16
+    int geo0, geo1;
 };
 struct ConvPlan {
     SegPlan s[LDM_CONV_MAX_SEGS];
@@ -359,13 +364,71 @@ __device__ __forceinline__ void epi_load(EpiOps<TP>& e, KConv& a, const ConvIO& 
     e.sg = *(const LDM_KC float*)(ddpm ? a.sigma + io.t : dummy);
 }
 
+// The contraction's segment geometry, two providers for conv_finish:
+//   PlanGeo: read from the plan (scalar loads) where the contraction needs it (generic kernel);
+//   FastGeo<NS>: the NS segments' fields read at kernel entry, with the staging's own argument
+//     reads, and selected by segment with scalar selects -- read after the staging barrier they
+//     were a chain of dependent scalar loads, ~0.45 us per conv (profiles/r04g stamps).
+struct PlanGeo {
+    KConv& a;
+    KPlan& pl;
+    __device__ __forceinline__ int n_seg() const { return a.n_seg; }
+    __device__ __forceinline__ int nchunks() const { return pl.nchunks; }
+    __device__ __forceinline__ int ch0(int s) const { return pl.s[s].ch0; }
+    __device__ __forceinline__ int cinp(int s) const { return pl.s[s].cinp; }
+    __device__ __forceinline__ int ks(int s) const { return a.seg[s].ksize; }
+    __device__ __forceinline__ int st(int s) const { return a.seg[s].stride; }
+    __device__ __forceinline__ int woff(int s) const { return pl.s[s].woff; }
+    __device__ __forceinline__ int xoff(int s) const { return pl.s[s].xoff; }
+};
+
+template <int NS>
+struct FastGeo {
+    int nch, g0[NS], g1[NS];          // SegPlan::geo0 / geo1: 2 SGPRs per segment (six
+                                      // separate fields made the 3-segment kernels spill)
+    __device__ __forceinline__ void load(KPlan& pl) {
+        nch = pl.nchunks;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            g0[i] = pl.s[i].geo0;
+            g1[i] = pl.s[i].geo1;
+        }
+    }
+    // v[s] for a wave-uniform s as a select chain (an indexed register array would go to scratch)
+    __device__ __forceinline__ static int pick(const int (&v)[NS], int s) {
+        int r = v[0];
+#pragma unroll
+        for (int i = 1; i < NS; ++i) r = s == i ? v[i] : r;
+        return r;
+    }
+    __device__ __forceinline__ int n_seg() const { return NS; }
+    __device__ __forceinline__ int nchunks() const { return nch; }
+    __device__ __forceinline__ int ch0(int s) const { return pick(g0, s) & 0xfff; }
+    __device__ __forceinline__ int ks(int s) const { return (pick(g0, s) >> 12) & 7; }
+    __device__ __forceinline__ int st(int s) const { return ((pick(g0, s) >> 15) & 1) + 1; }
+    __device__ __forceinline__ int cinp(int s) const { return (unsigned)pick(g0, s) >> 16; }
+    __device__ __forceinline__ int woff(int s) const { return pick(g1, s) & 0xffff; }
+    __device__ __forceinline__ int xoff(int s) const { return (unsigned)pick(g1, s) >> 16; }
+};
+
+template <typename G>
+__device__ __forceinline__ G make_geo(KConv& a, KPlan& pl) {
+    if constexpr (std::is_same<G, PlanGeo>::value) {
+        return PlanGeo{a, pl};
+    } else {
+        G g;
+        g.load(pl);
+        return g;
+    }
+}
+
 // The tile after its operands are staged (and the staging barrier passed): the MFMA
 // contraction split over the 4 waves, the partial tiles summed in wave order, the fused
 // epilogue.
-template <typename TW, int TP, typename ST>
-__device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& io, float* sm,
-                                            int pos0, int co0, int b, const EpiOps<TP>& e,
-                                            ST& st_) {
+template <typename TW, int TP, typename GEO, typename ST>
+__device__ __forceinline__ void conv_finish(KConv& a, const GEO& geo, const ConvIO& io,
+                                            float* sm, int pos0, int co0, int b,
+                                            const EpiOps<TP>& e, ST& st_) {
     constexpr int NT = TP / 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c16 = lane & 15;
@@ -385,23 +448,23 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
         acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const int c_beg = pl.nchunks * wave / 4, c_end = pl.nchunks * (wave + 1) / 4;
+    const int nchunks = geo.nchunks(), n_seg = geo.n_seg();
+    const int c_beg = nchunks * wave / 4, c_end = nchunks * (wave + 1) / 4;
     // chunk iterator: (segment, tap, channel group) with the lane's operand offsets (floats)
     int si = 0;
-    while (si + 1 < a.n_seg && c_beg >= pl.s[si + 1].ch0) ++si;
+    while (si + 1 < n_seg && c_beg >= geo.ch0(si + 1)) ++si;
     int ng = 0, ks = 0, st = 0, cinp = 0, wrow = 0, xbase = 0, k = 0, cg = 0;
     auto set_seg = [&](int s_) {
-        KSegPlan& p = pl.s[s_];
-        cinp = p.cinp;
+        cinp = geo.cinp(s_);
         ng = cinp >> 4;
-        ks = a.seg[s_].ksize;
-        st = a.seg[s_].stride;
-        wrow = p.woff + c16 * (ks * cinp + 4) + 4 * g;
-        xbase = p.xoff + 4 * g;
+        ks = geo.ks(s_);
+        st = geo.st(s_);
+        wrow = geo.woff(s_) + c16 * (ks * cinp + 4) + 4 * g;
+        xbase = geo.xoff(s_) + 4 * g;
     };
     set_seg(si);
     {
-        int q = c_beg - pl.s[si].ch0;
+        int q = c_beg - geo.ch0(si);
         while (q >= ng) { q -= ng; ++k; }
         cg = q;
     }
@@ -413,7 +476,7 @@ __device__ __forceinline__ void conv_finish(KConv& a, KPlan& pl, const ConvIO& i
                 sm + xbase + ((t * 16 + c16) * st + k) * (cinp + 4) + cg * 16);
         if (++cg == ng) {
             cg = 0;
-            if (++k == ks && si + 1 < a.n_seg) {
+            if (++k == ks && si + 1 < n_seg) {
                 k = 0;
                 set_seg(++si);
             }
@@ -670,7 +733,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
     sr.mark(1);
     EpiOps<TP> e;
     epi_load<TP>(e, a, io, pos0, co0, b);
-    conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sr);
+    conv_finish<TW, TP>(a, PlanGeo{a, pl}, io, sm, pos0, co0, b, e, sr);
 #if UNET_STAMP
     stamps_flush(sr);
 #endif
@@ -691,6 +754,9 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     sr.mark(0);
     const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
     const ConvIO io = conv_io(a);
+    // (3 segments: the plan read lazily -- preloaded, its SGPRs pushed the kernel into scratch)
+    typedef typename std::conditional<NS <= 2, FastGeo<NS>, PlanGeo>::type Geo;
+    Geo geo = make_geo<Geo>(a, pl);
     // per-thread items of a segment's first round: weights (16 B each; NBW picked per launch
     // from the segments' counts) and window items (4 x 16 B each: TP / 16 covers 128 channels).
     // Every slot is a load instruction even when its item is absent (out of range: no memory
@@ -744,7 +810,7 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     sr.mark(5);
     __syncthreads();
     sr.mark(1);
-    conv_finish<TW, TP>(a, pl, io, sm, pos0, co0, b, e, sr);
+    conv_finish<TW, TP>(a, geo, io, sm, pos0, co0, b, e, sr);
 #if UNET_STAMP
     stamps_flush(sr);
 #endif
@@ -776,8 +842,11 @@ int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) 
         const int span = g.mode == LDM_CONV_UP2 ? p.win / 2 + 3 : p.win + 2;
         p.lgng = ilog2(span / 4 + 1);
         p.nx = (p.cinp / 4) << p.lgng;
+        p.geo0 = p.ch0 | g.ksize << 12 | (g.stride - 1) << 15 | p.cinp << 16;
+        p.geo1 = p.woff | p.xoff << 16;
         const int64_t wbytes = (int64_t)(a.Cout + 15) / 16 * 16 * g.ldw * (epv == 8 ? 2 : 4);
         fast = fast && pow2(p.cinp) && g.L_in % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
+               p.ch0 < 4096 && p.cinp < 65536 && p.woff < 65536 && p.xoff < 65536 &&
                ((uintptr_t)g.W & 15) == 0 && (g.ldw * (16 / epv)) % 16 == 0 &&
                (g.kstride * (16 / epv)) % 16 == 0 &&
                (int64_t)g.C * g.L_in * 4 < (1ll << 31) && wbytes < (1ll << 31);
