@@ -166,8 +166,39 @@ __device__ __forceinline__ TileLoc locate(KArgs* ka, int t) {
 // MFMAs and runs its epilogue (which touches no LDS), so no workgroup pays the pipeline fill of
 // a short-K tile (C19: K = 512, 8 k-steps) and the epilogue of one tile overlaps loads of the
 // next.
+// Diagnostic build only (-DGEMM_STAMP=1, scripts/stamp_gemm.py): workgroup 0 of every
+// non-persistent, LDS-DMA launch keeps s_memrealtime marks in registers -- entry, prologue
+// stages issued, first stage landed, k-loop done, epilogue issued, stores drained -- and writes
+// them at its end into a ring of 256 launches (ldm_dev_gemm_stamps).
+#ifndef GEMM_STAMP
+#define GEMM_STAMP 0
+#endif
+#if GEMM_STAMP
+__device__ uint64_t g_gemm_stamp[256][8];
+__device__ unsigned g_gemm_stamp_n;
+#endif
+struct GStamp {
+    bool on;
+    uint64_t t[8];
+    __device__ __forceinline__ void mark(int k) {
+        if (GEMM_STAMP && on) t[k] = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ void flush(int grid, int tiles) {
+#if GEMM_STAMP
+        if (!on) return;
+        uint64_t* p = g_gemm_stamp[atomicAdd(&g_gemm_stamp_n, 1u) & 255u];
+        t[6] = (uint64_t)grid;
+        t[7] = (uint64_t)tiles;
+        for (int i = 0; i < 8; ++i) p[i] = t[i];
+#endif
+    }
+};
+
 template <int BM, int BN, int STAGES, int KG, bool RS, bool PERSIST, int KB>
 __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
+    GStamp gs;
+    gs.on = GEMM_STAMP && !PERSIST && !RS && blockIdx.x == 0 && threadIdx.x == 0;
+    gs.mark(0);
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     constexpr int RM = BM / 64, RN = BN / 64, NW = 4 * KG;
     constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
@@ -768,6 +799,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         if (ss < nks)
 #pragma unroll
             for (int u = 0; u < KG; ++u) issue();
+    gs.mark(1);
 
     for (int it = 0; it < nks; ++it) {
         // RAW: this wave's pieces of super-stage it landed (SS-2 younger ones may still fly),
@@ -777,6 +809,7 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
             asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((SS - 2) * KG * G) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (GEMM_STAMP && it == 0) gs.mark(2);
         if (it + SS - 1 < nks)
 #pragma unroll
             for (int u = 0; u < KG; ++u) issue();
@@ -817,9 +850,16 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
         }
         if (RM == 1 && grp != 0) return;
     }
+    gs.mark(3);
     // the epilogue's LDS tiles overwrite ring slots other waves may still be reading
     if constexpr (KG == 1 && !RS) __syncthreads();
     epilogue(L0, KG == 1 || RM == 1 || grp == 0, KG == 1 || grp == 1);
+    if (GEMM_STAMP && !RS) {
+        gs.mark(4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gs.mark(5);
+        gs.flush(gridDim.x, tot_all);
+    }
     }
 }
 
@@ -1049,3 +1089,14 @@ extern "C" int ldm_gemm_bf16(const ldm_gemm_args_t* a, ldm_stream_t s) {
     LDM_REQUIRE(a != nullptr, LDM_EINVAL, "ldm_gemm_bf16: null args");
     return ldm::gemm_bf16(*a, (hipStream_t)s);
 }
+
+#if GEMM_STAMP
+// diagnostic build only: the GEMM stamp ring (256 x 8: six s_memrealtime marks, grid, tiles)
+extern "C" int ldm_dev_gemm_stamps(uint64_t* host, unsigned* n) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ldm::g_gemm_stamp), sizeof(ldm::g_gemm_stamp)) !=
+            hipSuccess ||
+        hipMemcpyFromSymbol(n, HIP_SYMBOL(ldm::g_gemm_stamp_n), sizeof(unsigned)) != hipSuccess)
+        return -1;
+    return 0;
+}
+#endif
