@@ -116,12 +116,20 @@ class UNet1DDenoiser:
         c0, c1, c2 = self.C
         D = self.D
         f = lambda *s: torch.empty(*s, device=device, dtype=torch.float32)  # noqa: E731
-        return {"h0": f(n, c0, D), "a0": f(n, c0, D), "s0": f(n, c0, D),
-                "d0": f(n, c1, D // 2), "a1": f(n, c1, D // 2), "s1": f(n, c1, D // 2),
-                "d1": f(n, c2, D // 4), "a2": f(n, c2, D // 4), "m0": f(n, c2, D // 4),
-                "m1": f(n, c2, D // 4), "u1": f(n, c1, D // 2), "a4": f(n, c1, D // 2),
-                "r4": f(n, c1, D // 2), "u0": f(n, c0, D), "a5": f(n, c0, D),
-                "r5": f(n, c0, D), "eps": f(n, 1, D)}
+        b = {"h0": f(n, c0, D), "a0": f(n, c0, D), "s0": f(n, c0, D),
+             "d0": f(n, c1, D // 2), "a1": f(n, c1, D // 2), "s1": f(n, c1, D // 2),
+             "d1": f(n, c2, D // 4), "a2": f(n, c2, D // 4), "m0": f(n, c2, D // 4),
+             "m1": f(n, c2, D // 4), "u1": f(n, c1, D // 2), "a4": f(n, c1, D // 2),
+             "r4": f(n, c1, D // 2), "u0": f(n, c0, D), "a5": f(n, c0, D),
+             "r5": f(n, c0, D), "eps": f(n, 1, D)}
+        if n == 1:
+            # the decoder-side skip concats [u || s] as ONE buffer whose halves the producers
+            # write: res4 / res5 then read it as one segment (one staging segment fewer in
+            # their two convs); a channel slice is contiguous only at n = 1
+            for lvl, c in ((1, c1), (0, c0)):
+                cat = f(1, 2 * c, D >> lvl)
+                b[f"cat{lvl}"], b[f"u{lvl}"], b[f"s{lvl}"] = cat, cat[:, :c], cat[:, c:]
+        return b
 
     def step_args(self, dev: Dict[str, object], buf: Dict[str, torch.Tensor], x: torch.Tensor,
                   t: int, *, out: torch.Tensor, sched=None, z: Optional[torch.Tensor] = None,
@@ -172,10 +180,10 @@ class UNet1DDenoiser:
         res(3, [b["m0"]], b["a2"], b["m1"])
         calls.append(ops.conv1d_args([S(b["m1"], dev["up1.w"], mode=UP2)], b["u1"],
                                      bias=dev["up1.b"]))
-        res(4, [b["u1"], b["s1"]], b["a4"], b["r4"])
+        res(4, [b["cat1"]] if "cat1" in b else [b["u1"], b["s1"]], b["a4"], b["r4"])
         calls.append(ops.conv1d_args([S(b["r4"], dev["up0.w"], mode=UP2)], b["u0"],
                                      bias=dev["up0.b"]))
-        res(5, [b["u0"], b["s0"]], b["a5"], b["r5"])
+        res(5, [b["cat0"]] if "cat0" in b else [b["u0"], b["s0"]], b["a5"], b["r5"])
         last = [S(b["r5"], dev["conv_out.w"], silu=True)]
         if sched is not None:
             calls.append(ops.conv1d_args(last, out.view(n, 1, self.D), bias=dev["conv_out.b"],

@@ -179,7 +179,8 @@ def test_unet_forward_vs_golden(dev):
 
 
 @pytest.mark.parametrize("path", ["eager", "graph"])
-def test_unet_sampling_10_vs_golden(dev, path):
+@pytest.mark.parametrize("n", [2, 1])       # n = 1: the skip concats as one buffer (unet.py)
+def test_unet_sampling_10_vs_golden(dev, path, n):
     import ldm_sdf
     gd = dict(np.load(os.path.join(GOLD, "unet_10.npz")))
     steps = int(gd["steps"])
@@ -187,9 +188,10 @@ def test_unet_sampling_10_vs_golden(dev, path):
     sch = ldm_sdf.DDPMSchedule()
     noise = torch.zeros(1000, 2, 1024)
     noise[1000 - steps:] = torch.from_numpy(gd["noise_tail"])
-    x = ldm_sdf.sample(m, sch, 2, steps=steps, dtype="fp32", x_T=torch.from_numpy(gd["x_T"]),
-                       noise=noise, device=dev, use_graph=path == "graph").cpu().double()
-    err = float((x - torch.from_numpy(gd["traj"][-1])).abs().max())
+    x = ldm_sdf.sample(m, sch, n, steps=steps, dtype="fp32",
+                       x_T=torch.from_numpy(gd["x_T"])[:n], noise=noise[:, :n].contiguous(),
+                       device=dev, use_graph=path == "graph").cpu().double()
+    err = float((x - torch.from_numpy(gd["traj"][-1])[:n]).abs().max())
     assert err <= 1e-4, err
 
 
