@@ -754,6 +754,7 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     sr.mark(0);
     const int pos0 = blockIdx.x * TP, co0 = blockIdx.y * 16, b = blockIdx.z;
     const ConvIO io = conv_io(a);
+    sr.mark(13);                             // entry code done (block ids, io)
     // (3 segments: the plan read lazily -- preloaded, its SGPRs pushed the kernel into scratch)
     typedef typename std::conditional<NS <= 2, FastGeo<NS>, PlanGeo>::type Geo;
     Geo geo = make_geo<Geo>(a, pl);
@@ -772,6 +773,7 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     }
     EpiOps<TP> e;
     epi_load<TP>(e, a, io, pos0, co0, b);
+    sr.mark(11);
     // keep every load above issued before the first use of any of them below: the scheduler
     // otherwise pairs each segment's stores with its loads, or hoists the first bf16 unpack
     // above the window loads -- either is a wait for the data in the middle of the issue, one
@@ -786,6 +788,10 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
         for (int u = 0; u < NBX; ++u)
 #pragma unroll
             for (int m = 0; m < 4; ++m) asm volatile("" : "+v"(xv[si][u][m]));
+    }
+    if (UNET_STAMP && sr.on) {               // diagnostic: every staging load has landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sr.mark(12);
     }
 #pragma unroll
     for (int si = 0; si < NS; ++si) {

@@ -61,3 +61,9 @@ print(f"{'sum':>9} " + " ".join(f"{x:7.2f}" for x in tot[:6]) + " | " +
       " ".join(f"{x:6.2f}" for x in tot[6:10]) + " | " + " ".join(f"{x:6.2f}" for x in tot[10:13])
       + " | " + " ".join(f"{x:6.2f}" for x in tot[13:]))
 print(f"step span (entry of conv_in -> stores of conv_out): {(st[35][7] - st[18][0]) / 100:.1f} us")
+if st[18:36, 11].any():
+    print("direct staging split (us): entry->geo | ->loads issued | ->data landed | ->stores done")
+    for i in range(18):
+        r = st[18 + i]
+        print(f"{names[i]:>9} {(r[13] - r[0]) / 100:7.2f} {(r[11] - r[13]) / 100:7.2f} "
+              f"{(r[12] - r[11]) / 100:7.2f} {(r[3] - r[12]) / 100:7.2f}")
