@@ -449,7 +449,9 @@ __device__ __forceinline__ void conv_finish(KConv& a, const GEO& geo, const Conv
         acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const int nchunks = geo.nchunks(), n_seg = geo.n_seg();
-    const int c_beg = nchunks * wave / 4, c_end = nchunks * (wave + 1) / 4;
+    // wave-uniform (scalar) chunk range: the loop below branches on it with scalar branches
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int c_beg = nchunks * wv / 4, c_end = nchunks * (wv + 1) / 4;
     // chunk iterator: (segment, tap, channel group) with the lane's operand offsets (floats)
     int si = 0;
     while (si + 1 < n_seg && c_beg >= geo.ch0(si + 1)) ++si;
@@ -468,52 +470,73 @@ __device__ __forceinline__ void conv_finish(KConv& a, const GEO& geo, const Conv
         while (q >= ng) { q -= ng; ++k; }
         cg = q;
     }
+    // The chunk iterator reads the current chunk's operands and then advances only while a
+    // chunk of this wave is left (past the end it re-reads the last one): every LDS read of the
+    // loop is unconditional, so the compiler can wait for exactly the pair an MFMA group needs
+    // while the next pair is in flight.  (The first form loaded the next pair under branches
+    // and rotated registers, so every pair waited for ALL reads, the prefetch included.)
+    int left = c_end - c_beg - 1;           // chunks after the current one
     auto load_chunk = [&](f32x4& av, f32x4 (&bv)[NT]) {
         av = *reinterpret_cast<const f32x4*>(sm + wrow + k * cinp + cg * 16);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
             bv[t] = *reinterpret_cast<const f32x4*>(
                 sm + xbase + ((t * 16 + c16) * st + k) * (cinp + 4) + cg * 16);
-        if (++cg == ng) {
-            cg = 0;
-            if (++k == ks && si + 1 < n_seg) {
-                k = 0;
-                set_seg(++si);
+        if (left > 0) {
+            --left;
+            if (++cg == ng) {
+                cg = 0;
+                if (++k == ks && si + 1 < n_seg) {
+                    k = 0;
+                    set_seg(++si);
+                }
             }
         }
     };
-    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-    f32x4 a0 = z4, a1 = z4, b0[NT], b1[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) b0[t] = b1[t] = z4;
-    bool h0 = c_beg < c_end, h1 = c_beg + 1 < c_end;
-    if (h0) load_chunk(a0, b0);
-    if (h1) load_chunk(a1, b1);
-    st_.mark(8);
-    for (int ch = c_beg; h0; ch += 2) {
-        // the next pair first (its LDS latency hides under this pair's MFMAs); a missing
-        // second chunk is all zeros: its MFMAs add exact zeros
-        f32x4 n0 = z4, n1 = z4, m0[NT], m1[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) m0[t] = m1[t] = z4;
-        const bool g0 = ch + 2 < c_end, g1 = ch + 3 < c_end;
-        if (g0) load_chunk(n0, m0);
-        if (g1) load_chunk(n1, m1);
+    auto mfma4 = [&](f32x4 (&acc)[NT], const f32x4& av, const f32x4 (&bv)[NT]) {
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                acc0[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[m], b0[t][m], acc0[t], 0, 0, 0);
-                acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[m], b1[t][m], acc1[t], 0, 0, 0);
-            }
-        a0 = n0;
-        a1 = n1;
+            for (int t = 0; t < NT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[t][m], acc[t], 0, 0, 0);
+    };
+    // two pairs in flight (ping-pong, no register copies), chunks alternating between the two
+    // accumulator sets so consecutive MFMAs are independent
+    const int n = c_end - c_beg;
+    f32x4 pa0, pa1, pb0, pb1, qa0[NT], qa1[NT], qb0[NT], qb1[NT];
+    if (n > 0) {
+        load_chunk(pa0, qa0);
+        load_chunk(pa1, qa1);
+    }
+    st_.mark(8);
+    for (int i = 0; i < n; i += 4) {
+        load_chunk(pb0, qb0);               // chunks i + 2, i + 3
+        load_chunk(pb1, qb1);
+        if (i + 1 < n) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            b0[t] = m0[t];
-            b1[t] = m1[t];
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    acc0[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[m], qa0[t][m], acc0[t], 0, 0, 0);
+                    acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[m], qa1[t][m], acc1[t], 0, 0, 0);
+                }
+        } else {
+            mfma4(acc0, pa0, qa0);
         }
-        h0 = g0;
+        if (i + 2 >= n) break;
+        load_chunk(pa0, qa0);               // chunks i + 4, i + 5
+        load_chunk(pa1, qa1);
+        if (i + 3 < n) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    acc0[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pb0[m], qb0[t][m], acc0[t], 0, 0, 0);
+                    acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pb1[m], qb1[t][m], acc1[t], 0, 0, 0);
+                }
+        } else {
+            mfma4(acc0, pb0, qb0);
+        }
     }
     f32x4 acc[NT];
 #pragma unroll
