@@ -1025,7 +1025,7 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     //    2048);
     //  * else 64 x 64 on a 3-deep 64-k ring (48 KiB: 3 workgroups per CU, so config 2's
     //    768-tile backward launches run in ONE wave of workgroups; the 128-deep 2-stage tile at
-    //    2 per CU left half a wave: the step 0.348 -> 0.317-0.326 ms, scripts/train_tiles2.sh,
+    //    2 per CU left half a wave: the step 0.348 -> 0.317-0.326 ms, scripts/rounds/train_tiles2.sh,
     //    profiles/r02h/train_tiles2.log).
     const int forced = dev_knob("LDM_GEMM_TILE", 0);
     int tile = a.tile;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 3: split-K bound estimate for config 2's GEMM shapes (1024-row padded batch)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out/r03d
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && mkdir -p gpurun_out/r03d
 o=gpurun_out/r03d/gemm_splitk.log; : > $o
 for sh in 1024,1024,2048 1024,1024,1024 1024,1024,4096; do
   for sk in 1 2 4; do

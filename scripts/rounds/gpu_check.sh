@@ -3,7 +3,7 @@
 # Stops at the first crash/timeout (exit 124/134/137/139 or signal) so nothing else touches a
 # possibly-faulted GPU.  Logs go to gpurun_out/.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139|13[0-9]|14[0-9]) return 0;; *) return 1;; esac; }
 run() {  # name timeout cmd...

@@ -2,7 +2,7 @@
 # PMC passes over the decoder workload (scripts/decode_once.py).  One counter group per
 # rocprofv3 run (no trace domains with --pmc).  Output: gpurun_out/pmc/<pass>/...
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/pmc}
 WORKLOAD=${WORKLOAD:-scripts/decode_once.py}

@@ -1,5 +1,5 @@
 # config-2 training: GEMM tile per launch size class (LDM_GEMM_TILE_SMALL/MID/BIG; 0 = auto)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && mkdir -p gpurun_out
 for cfg in "0 4 4" "0 4 1" "0 1 1" "0 4 5" "0 4 8" "0 5 5" "0 11 4" "0 4 4"; do
   set -- $cfg
   echo "small $1 mid $2 big $3"
