@@ -482,12 +482,40 @@ def config5(args, rank, world, dev, group, gen):
             "bound": "launch-chain", "achieved": sps, "peak": 1.0 / model_step,
             "unit": "steps/s", "frac": sps * model_step, "launches_per_step": 18,
             "node_ns": node["node_ns"], "node_grid": node["grid"], "source": node["source"],
-            "note": "peak = 1 / (18 x the measured latency of one dependent node of a captured "
-                    "chain of empty kernels at the convs' grid size); frac = that model step "
-                    "time / the measured step time of the default (graph) path"}
+            "measured_in_this_run": False,
+            "note": "a launch-chain MODEL, not a hardware roofline: peak = 1 / (18 x the latency "
+                    "of one dependent node of a captured chain of empty kernels at the convs' "
+                    "grid size, measured by scripts/microbench/graph_chain_latency.hip on an "
+                    "MI355X in an earlier run, read from `source`); frac = that model step time / "
+                    "the measured step time of the default (graph) path"}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)
     return res
+
+
+def bench_decode_b1(args, rank, world, dev, group, decoder, desc, gen):
+    """SURVEY §8(d) "B = 1 for the headline number": one shape's ``--grid``^3 decode (16.8 M
+    queries at 256^3), z-slab over the ranks, ``--dtype``; kernel time from HIP events on its
+    stream; max-over-ranks wall time of 3 timed decodes after 1 warm-up."""
+    from ldm_sdf import ops
+    N = args.grid
+    lat1 = torch.randn(1, 256, device=dev, generator=gen) * 0.1
+    out1 = torch.empty(1, N, N, N, device=dev)
+    slab = SlabTimer(desc, lambda: ops.decoder_fold(desc, lat1), N,
+                     torch.cuda.current_stream(dev))
+    reps = 3
+    el = run_decode_steps(slab, 1, N, steps=reps, warmup=1, world=world, group=group,
+                          device=dev, out=out1, sync=torch.cuda.synchronize,
+                          on_timed=lambda: setattr(slab, "timed", True))
+    kms, qpl = slab.kernel_stats()
+    ach = FLOPS_PER_QUERY * qpl / (kms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    return {"metric": f"SDF queries/sec, ONE shape on a {N}^3 grid", "value": N ** 3 * reps / el,
+            "unit": "queries/s", "ms_per_decode": el / reps * 1e3, "dtype": args.dtype,
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                         "frac": ach / peak, "kernel": "dec_fs_kernel",
+                         "queries_per_launch": qpl, "avg_launch_ms": kms},
+            "target_ms_at_40pct": N ** 3 * FLOPS_PER_QUERY / (0.4 * peak * 1e12) * 1e3}
 
 
 def graph_node_latency(grid: int = 128):
@@ -544,6 +572,9 @@ def main():
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
+        # RCCL fails fast: an error / timeout on one rank aborts the communicator instead of
+        # leaving the others blocked in a collective (SURVEY §5 "Fault/elastic")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD
 
@@ -574,6 +605,9 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
     traffic, traffic_src = decoder_traffic(qpl)
 
+    # SURVEY §8(d)'s single-shape headline: ONE shape's 256^3 grid (16.8 M queries), same kernel
+    b1 = bench_decode_b1(args, rank, world, dev, group, decoder, desc, gen)
+
     res = None
     if rank == 0:
         res = {
@@ -582,9 +616,13 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": args.dtype, "data": "synthetic (latents N(0,0.1^2) seed 0, He-normal decoder seed 1234)",
-            "config": {"workload": f"config4: decode B={B} shapes on a {N}^3 grid, z-slab sharded "
-                                   f"over {world} rank(s) + per-shape RCCL all-gathers of the "
-                                   "volume",
+            "config": {"workload": (f"config4: decode B={B} shapes on a {N}^3 grid, z-slab "
+                                    f"sharded over {world} ranks + RCCL all-gathers of the "
+                                    "volume (each group of ceil(B/8) shapes' per-shape gathers "
+                                    "as one coalesced collective, overlapping the next group)")
+                                   if world > 1 else
+                                   (f"config4: decode B={B} shapes on a {N}^3 grid on 1 rank "
+                                    "(the whole grid is the one slab: no gather)"),
                        "batch": B, "grid": N, "latent_dim": 256, "decoder": "DeepSDF 8x512 skip@4",
                        "parallelism": f"zslab{world}"},
             "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
@@ -594,6 +632,7 @@ def main():
                          "flops_per_query": FLOPS_PER_QUERY,
                          "queries_per_launch": qpl, "avg_launch_ms": kms,
                          "launches_per_step": len(slab.events) // max(1, args.steps)},
+            "decode_b1": b1,
         }
     if not args.no_ddpm:
         r = bench_ddpm(args, rank, world, dev, group, gen, decoder)
@@ -682,22 +721,66 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
     xg = sampler_g.run(xT, noise).clone()
     sps_graph = timed(lambda: sampler_g.run(xT, noise))
     same = bool(torch.equal(sampler.run(xT, noise), xg))
-    e2e, c3_dtype = None, None
+    e2e, c3_dtype, c3 = None, None, {}
+    # config 3 samples with the same random time MLP and residual blocks but identity in/out
+    # projections (tests/test_gpu_ddpm.py bounded_denoiser_params): an untrained random
+    # denoiser drives x to ~1e8 over 1000 steps, whose decode is meaningless (every 16-bit
+    # dtype saturates); here the sampled latents stay O(1) (RMS ~0.45), the regime the 16-bit
+    # decode is calibrated for.  The sampling work per step is the same network.
+    den_c3 = bounded_denoiser(den)
     if not args.no_config3:      # config 3: sample(8) -> decode 128^3, end to end
         # the decoder's packed weights are a one-time setup (like loading the model): both
         # 16-bit packs exist before the clock starts, whichever dtype="auto" then picks
         for dt in ("bf16", "fp16"):
             decoder.device_pack(dt, dev)
-        if world > 1:
-            dist.barrier(group)
+
+        def clock():
+            if world > 1:
+                dist.barrier(group)
+            torch.cuda.synchronize()
+            return time.perf_counter()
+
+        def e2e_call():
+            lat_ = ldm_sdf.sample(den_c3, sch, nb, dtype="bf16", device=dev, group=group,
+                                  generator=gen)
+            dt_ = ldm_sdf.resolve_decode_dtype(args.dtype if args.dtype != "bf16" else "auto",
+                                               lat_)
+            ldm_sdf.decode(decoder, lat_, 128, dtype=dt_, group=group)
+            return dt_
+
+        # (1) the first API call of the process for this shape (fresh Sampler: its buffers,
+        # loop program, first launches of the 128^3 decode) -- what one-shot use pays
+        t2 = clock()
+        c3_dtype = e2e_call()
         torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        lat = ldm_sdf.sample(den, sch, nb, dtype="bf16", device=dev, group=group,
-                             generator=gen)
-        c3_dtype = ldm_sdf.resolve_decode_dtype("auto", lat)
-        ldm_sdf.decode(decoder, lat, 128, dtype=c3_dtype, group=group)
-        torch.cuda.synchronize()
-        e2e = time.perf_counter() - t2
+        first = time.perf_counter() - t2
+        # (2) the same API call again (fresh Sampler, warm process), 3 reps, median
+        warm = []
+        for _ in range(3):
+            t2 = clock()
+            e2e_call()
+            torch.cuda.synchronize()
+            warm.append(time.perf_counter() - t2)
+        # (3) steady state: one Sampler kept across calls (no per-call setup), run + decode
+        smp3 = ldm_sdf.Sampler(den_c3, sch, nl, dtype="bf16", device=dev)
+        x3 = torch.randn(nl, 256, device=dev, generator=gen)
+        n3 = torch.randn(1000, nl, 256, device=dev, generator=gen)
+        smp3.run(x3, n3)
+        steady = []
+        for _ in range(3):
+            t2 = clock()
+            lat3 = smp3.run(x3, n3)
+            lat3 = ldm_sdf.dist.all_gather_rows(lat3.clone(), nb, group=group) \
+                if world > 1 else lat3
+            ldm_sdf.decode(decoder, lat3, 128, dtype=c3_dtype, group=group)
+            torch.cuda.synchronize()
+            steady.append(time.perf_counter() - t2)
+        warm.sort()
+        steady.sort()
+        e2e = warm[1]
+        c3 = {"config3_first_call_s": first, "config3_api_call_s": warm,
+              "config3_steady_s": steady, "config3_setup_s": warm[1] - steady[1],
+              "config3_first_call_overhead_s": first - warm[1]}
     wbytes = 2 * (den.H * den.D * 2 + den.n_blocks * den.H * den.H) + 2 * nl * den.D * 4
     valid = not loop_status
     hand = handoff_latency()
@@ -750,10 +833,30 @@ def bench_ddpm(args, rank, world, dev, group, gen, decoder):
                                  "in registers, so it is grid-barrier-latency-bound "
                                  "(DESIGN.md §5)"},
             "config3_sample_plus_decode128_s": e2e,
-            "config3": (f"sample(8) (1000 bf16 steps, fresh Sampler: includes its setup) -> "
-                        f"decode(128^3, {c3_dtype}: dtype='auto' for these latents, "
-                        f"api.resolve_decode_dtype), wall time" if e2e is not None else None),
-            "config3_decode_dtype": c3_dtype if e2e is not None else None}
+            "config3": (f"sample(8) (1000 bf16 steps) -> decode(128^3, {c3_dtype}: dtype='auto' "
+                        f"for these latents, api.resolve_decode_dtype), wall time; "
+                        f"config3_sample_plus_decode128_s = median of 3 API calls in a warm "
+                        f"process (each builds a fresh Sampler); config3_steady_s = one Sampler "
+                        f"reused (run + decode); config3_first_call_s = the process's first "
+                        f"call (first launches of the 128^3 decode and the loop)"
+                        if e2e is not None else None),
+            "config3_decode_dtype": c3_dtype if e2e is not None else None, **c3}
+
+
+def bounded_denoiser(den):
+    """``den`` with identity in/out projections (W_in = [I; 0], W_out = [I, 0], zero in/out
+    biases) and its blocks and time MLP unchanged: every reverse step contracts, so sampled
+    latents stay O(1) (tests/test_gpu_ddpm.py bounded_denoiser_params)."""
+    import ldm_sdf
+    p = {k: v.detach().cpu().clone() for k, v in den.params.items()}
+    D, H = den.D, den.H
+    p["Win"] = torch.zeros(H, D)
+    p["Win"][:D] = torch.eye(D)
+    p["Wout"] = torch.zeros(D, H)
+    p["Wout"][:, :D] = torch.eye(D)
+    p["bin"] = torch.zeros(H)
+    p["bout"] = torch.zeros(D)
+    return ldm_sdf.MLPDenoiser(D=D, H=H, n_blocks=den.n_blocks, TE=den.TE, T=den.T, params=p)
 
 
 def bench_train(args, dev, gen):

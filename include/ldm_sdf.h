@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define LDM_ABI_VERSION 6
+#define LDM_ABI_VERSION 7
 
 /* dtypes */
 #define LDM_F32 0
@@ -43,8 +43,8 @@ extern "C" {
 /* workspace ops for ldm_workspace_bytes() */
 #define LDM_OP_DECODER_GRID 1
 #define LDM_OP_DECODER_POINTS 2
-/* ldm_workspace_bytes() returns the largest per-layout need (split / split16), enough for every
-   layout; ldm_workspace_bytes_layout() gives the layout's own size */
+/* ldm_workspace_bytes() returns the need of the (one) 16-bit layout, LDM_LAYOUT_SPLIT;
+   ldm_workspace_bytes_layout() gives a layout's own size (0 for removed layouts) */
 
 typedef void* ldm_stream_t; /* hipStream_t; NULL = the null stream */
 
@@ -60,23 +60,23 @@ typedef struct ldm_decoder {
     int32_t hidden;       /* H (512) */
     int32_t skip_width;   /* 253 or 512 */
     int32_t latent_dim;   /* L */
-    int32_t n_stages;     /* bf16/f16: k-steps of one wave's weight stream (split 384 / 448,
-                             split16 192 / 224 at skip width 253 / 512); f32: 0 */
-    const void* weights;  /* bf16/f16: per-wave stream blob (ldm_sdf/pack.py pack_split /
-                             pack_split16); f32: fp32 blob */
+    int32_t n_stages;     /* bf16/f16: k-steps of one wave's weight stream (384 / 448 at skip
+                             width 253 / 512); f32: 0 */
+    const void* weights;  /* bf16/f16: per-wave stream blob (ldm_sdf/pack.py pack_split,
+                             DESIGN.md §4); f32: fp32 blob */
     const float* wz;      /* fp32 [2][H][L]  latent columns of layer 0 and layer 4 */
     const float* bz;      /* fp32 [2][H]     biases of layer 0 and layer 4 */
     const float* wxyz;    /* fp32 [2][H][3]  xyz columns of layer 0 and layer 4 */
     const float* w_last;  /* fp32 [H] final 512->1 weights (bf16/f16: MFMA-row permuted) */
     float b_last;         /* final bias */
-    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_SPLIT (default) or _SPLIT16 */
+    int32_t layout;       /* bf16/f16 weight layout: LDM_LAYOUT_SPLIT */
 } ldm_decoder_t;
 
 /* Stage-blob layouts of the MFMA decoder. */
 #define LDM_LAYOUT_PASS8 0   /* removed in ABI 5 (superseded by SPLIT): LDM_ENOSYS */
 #define LDM_LAYOUT_QUARTER 1 /* removed in ABI 5 (superseded by SPLIT): LDM_ENOSYS */
 #define LDM_LAYOUT_SPLIT 2   /* features split over the 4 waves, per-wave weight streams */
-#define LDM_LAYOUT_SPLIT16 3 /* the split work division on 16x16x32 MFMAs, fp32 biases */
+#define LDM_LAYOUT_SPLIT16 3 /* removed in ABI 7 (5.5 % slower than SPLIT): LDM_ENOSYS */
 
 /* DDPM tables, fp32 device arrays of length T. */
 typedef struct ldm_sched {

@@ -36,11 +36,7 @@ extern "C" size_t ldm_workspace_bytes(int op, int B, int n, int dtype) {
     switch (op) {
         case LDM_OP_DECODER_GRID:
         case LDM_OP_DECODER_POINTS:
-        {   // enough for every layout
-            const size_t a = ldm::decoder_workspace_bytes(B, dtype, LDM_LAYOUT_SPLIT);
-            const size_t b = ldm::decoder_workspace_bytes(B, dtype, LDM_LAYOUT_SPLIT16);
-            return a > b ? a : b;
-        }
+            return ldm::decoder_workspace_bytes(B, dtype, LDM_LAYOUT_SPLIT);
         default:
             return 0;
     }

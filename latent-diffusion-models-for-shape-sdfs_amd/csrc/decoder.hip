@@ -1,7 +1,8 @@
 // DeepSDF decoder on MI355X (gfx950): SURVEY.md §8(a) rows A1 (grid coords), A2 (latent
 // fold) and A3 (fused 9-layer MLP), in grid mode and point-list mode.  This unit holds the
-// ABI entry points and their dispatch; the 16-bit MFMA kernels live in decoder_fs.hip (the
-// "split" layout, default) and decoder_fs16.hip ("split16", 16x16x32 MFMAs).
+// ABI entry points and their dispatch; the 16-bit MFMA kernel lives in decoder_fs.hip (the
+// "split" layout; the round-3 "split16" variant on 16x16x32 MFMAs measured 5.5 % slower and was
+// deleted in ABI 7).
 //
 // The reference ships no implementation (/root/reference/README.md:1 is its only line); the
 // math follows oracle/ref_cpu.py (decoder_forward_folded, grid_coords_np, latent_fold).
@@ -194,13 +195,13 @@ int check_decoder(const ldm_decoder_t* w) {
     LDM_REQUIRE(LDM_ALIGNED(w->weights, 16) && LDM_ALIGNED(w->w_last, 16), LDM_EALIGN,
                 "decoder weights must be 16-byte aligned");
     if (w->dtype != LDM_F32) {
-        LDM_REQUIRE(w->layout != LDM_LAYOUT_PASS8 && w->layout != LDM_LAYOUT_QUARTER, LDM_ENOSYS,
-                    "decoder layout %d (pass8 / quarter) was removed in ABI 5: pack the weights "
-                    "in LDM_LAYOUT_SPLIT", w->layout);
-        LDM_REQUIRE(w->layout == LDM_LAYOUT_SPLIT || w->layout == LDM_LAYOUT_SPLIT16,
-                    LDM_EINVAL, "bad decoder layout %d", w->layout);
-        const int want = w->layout == LDM_LAYOUT_SPLIT ? decoder_fs_n_stages(w->skip_width)
-                                                       : decoder_fs16_n_stages(w->skip_width);
+        LDM_REQUIRE(w->layout != LDM_LAYOUT_PASS8 && w->layout != LDM_LAYOUT_QUARTER &&
+                        w->layout != LDM_LAYOUT_SPLIT16,
+                    LDM_ENOSYS, "decoder layout %d (pass8 / quarter: removed in ABI 5; split16: "
+                    "removed in ABI 7) -- pack the weights in LDM_LAYOUT_SPLIT", w->layout);
+        LDM_REQUIRE(w->layout == LDM_LAYOUT_SPLIT, LDM_EINVAL, "bad decoder layout %d",
+                    w->layout);
+        const int want = decoder_fs_n_stages(w->skip_width);
         LDM_REQUIRE(w->n_stages == want, LDM_EINVAL, "n_stages %d != %d for skip width %d",
                     w->n_stages, want, w->skip_width);
     }
@@ -236,9 +237,6 @@ int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int
                            points ? 1 : 0);
         return launch_status("ldm_decoder_fwd(f32)");
     }
-    if (w->layout == LDM_LAYOUT_SPLIT16)
-        return decoder_fs16_fwd(w, beta, xyz, B, npts, N, k0, vs, origin, out, ws, ws_bytes, s,
-                                num_cus());
     return decoder_fs_fwd(w, beta, xyz, B, npts, N, k0, vs, origin, out, ws, ws_bytes, s,
                           num_cus());
 }
@@ -246,8 +244,8 @@ int decoder_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int
 }  // namespace
 
 size_t decoder_workspace_bytes(int B, int dtype, int layout) {
-    if (dtype == LDM_F32) return 0;
-    return layout == LDM_LAYOUT_SPLIT16 ? decoder_fs16_aux_bytes(B) : decoder_fs_aux_bytes(B);
+    if (dtype == LDM_F32 || layout != LDM_LAYOUT_SPLIT) return 0;
+    return decoder_fs_aux_bytes(B);
 }
 
 }  // namespace ldm

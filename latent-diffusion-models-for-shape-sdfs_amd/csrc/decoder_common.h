@@ -1,4 +1,4 @@
-// Device helpers shared by the decoder kernels (decoder.hip, decoder_fs.hip, decoder_fs16.hip).
+// Device helpers shared by the decoder kernels (decoder.hip, decoder_fs.hip).
 #pragma once
 #include "ldm_internal.h"
 

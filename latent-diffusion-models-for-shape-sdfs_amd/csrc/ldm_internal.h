@@ -88,13 +88,6 @@ int decoder_fs_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, 
                    int N, int k0, float vs, float origin, float* out, void* ws, size_t ws_bytes,
                    hipStream_t s, int num_cus);
 
-// feature-split decoder on 16x16x32 MFMAs (decoder_fs16.hip)
-size_t decoder_fs16_aux_bytes(int B);
-int decoder_fs16_n_stages(int skip_width);
-int decoder_fs16_fwd(const ldm_decoder_t* w, const float* beta, const float* xyz, int B, int npts,
-                     int N, int k0, float vs, float origin, float* out, void* ws, size_t ws_bytes,
-                     hipStream_t s, int num_cus);
-
 // matrix-core path of ldm_linear (linear_mfma.hip)
 int linear_mfma(const ldm_linear_args_t& a, hipStream_t s);
 int64_t linear_mfma_ws_floats(const ldm_linear_args_t& a);   // split-K workspace

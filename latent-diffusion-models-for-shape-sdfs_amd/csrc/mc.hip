@@ -27,10 +27,13 @@ namespace ldm {
 namespace {
 
 // ------------------------------------------------------------------------------ case table
-struct McTables {
+// 16-byte aligned: the kernels stage the tables into LDS as u32x4 / unsigned words
+struct alignas(16) McTables {
     signed char tri[256][16];
     unsigned char ntri[256];
 };
+static_assert(alignof(McTables) >= 16 && offsetof(McTables, ntri) % 16 == 0,
+              "McTables: the LDS staging reads tri / ntri as 16-byte vectors");
 
 // corner c: offset (c & 1, c >> 1 & 1, c >> 2 & 1); edge e = 4a + m along axis a from the
 // corner whose other two bits (lower axis first) are m.

@@ -878,7 +878,9 @@ int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) 
                p.ch0 < 4096 && p.cinp < 65536 && p.woff < 65536 && p.xoff < 65536 &&
                ((uintptr_t)g.W & 15) == 0 && (g.ldw * (16 / epv)) % 16 == 0 &&
                (g.kstride * (16 / epv)) % 16 == 0 &&
-               (int64_t)g.C * g.L_in * 4 < (1ll << 31) && wbytes < (1ll << 31);
+               // the window offsets run over PADDED channel rows (row0 + 4m < cinp) in signed
+               // 32-bit arithmetic, and the weight resource spans 0x7ffffff0 bytes
+               (int64_t)p.cinp * g.L_in * 4 < (1ll << 31) && wbytes <= 0x7ffffff0ll;
     }
     pl->nchunks = ch;
     pl->fast = fast;

@@ -19,11 +19,11 @@ LIB_PATH = os.environ.get("LDM_SDF_LIB", LIB_PATH)
 HEADER_PATH = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                             "..", "..", "include", "ldm_sdf.h"))
 
-ABI_VERSION = 6   # 6: ldm_unet_loop* retired
+ABI_VERSION = 7   # 6: ldm_unet_loop* retired; 7: split16 removed, ldm_denoiser_train_step_dag
 LDM_F32, LDM_BF16, LDM_F16 = 0, 1, 2
 LDM_OP_DECODER_GRID, LDM_OP_DECODER_POINTS = 1, 2
 LAYOUT_PASS8, LAYOUT_QUARTER, LAYOUT_SPLIT, LAYOUT_SPLIT16 = 0, 1, 2, 3
-LAYOUT_CODES = {"split": LAYOUT_SPLIT, "split16": LAYOUT_SPLIT16}   # pass8 / quarter: removed, ABI 5
+LAYOUT_CODES = {"split": LAYOUT_SPLIT}   # pass8 / quarter: removed in ABI 5, split16 in ABI 7
 EPI_BIAS, EPI_SILU, EPI_RESID_SILU, EPI_ACCUM, EPI_ADD_R, EPI_RELU, EPI_MASK_R = range(7)
 COMPUTE_FP32, COMPUTE_BF16 = 0, 1
 COMPUTE_CODES = {"fp32": COMPUTE_FP32, "bf16": COMPUTE_BF16}

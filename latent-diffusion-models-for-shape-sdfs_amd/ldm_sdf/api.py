@@ -33,16 +33,35 @@ from .models import DDPMSchedule, MLPDenoiser, SDFDecoder
 # 0.1 / 0.5, inside its 2e-3 bound) at the same MFMA rate, so dtype="auto" decodes latents
 # whose largest per-shape RMS exceeds BF16_MAX_LATENT_RMS in fp16.
 BF16_MAX_LATENT_RMS = 0.2
+# fp16's calibration ends here (CPU oracle at the fp16 contract: 1.4e-3 at RMS 0.5, 2.0e-3 --
+# SURVEY §8(c)'s fp16 bound -- at 1.0; larger latents also approach fp16's 65504 range): above
+# it "auto" decodes in exact fp32
+FP16_MAX_LATENT_RMS = 1.0
+# "auto" costs one device->host read of the latents' RMS; it is cached per latents tensor
+# (identity, storage, in-place version), so repeated decodes of the same latents do not sync
+_AUTO_CACHE: Dict[tuple, str] = {}
 
 
 def resolve_decode_dtype(dtype: str, latents: torch.Tensor) -> str:
-    """``dtype`` itself, or for "auto" bf16 when every shape's latent RMS is within the bf16
-    calibration (``BF16_MAX_LATENT_RMS``), else fp16 (one device->host read)."""
+    """``dtype`` itself, or for "auto": bf16 when every shape's latent RMS is within the bf16
+    calibration (``BF16_MAX_LATENT_RMS``), fp16 up to ``FP16_MAX_LATENT_RMS``, else fp32 -- one
+    device->host read per latents tensor (cached while the tensor is unmodified).  Pass an
+    explicit dtype to keep a decode free of host synchronisation (graph capture)."""
     if dtype != "auto":
         return dtype
+    key = (id(latents), latents.data_ptr(), latents._version, tuple(latents.shape),
+           str(latents.device))
+    hit = _AUTO_CACHE.get(key)
+    if hit is not None:
+        return hit
     lat = latents.float().reshape(latents.shape[0] if latents.dim() > 1 else 1, -1)
     rms = float(lat.pow(2).mean(dim=1).sqrt().max())
-    return "bf16" if rms <= BF16_MAX_LATENT_RMS else "fp16"
+    pick = "bf16" if rms <= BF16_MAX_LATENT_RMS else "fp16" if rms <= FP16_MAX_LATENT_RMS \
+        else "fp32"
+    if len(_AUTO_CACHE) > 64:
+        _AUTO_CACHE.clear()
+    _AUTO_CACHE[key] = pick
+    return pick
 
 
 def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
@@ -53,7 +72,8 @@ def decode(decoder: SDFDecoder, latents: torch.Tensor, resolution: int, *,
     Layout ``[B, z, y, x]`` (z slowest).  With an initialised process group the grid is
     z-slab sharded over its ranks and all-gathered (every rank returns the full volume).
     ``dtype``: "fp32" (exact), "bf16", "fp16" or "auto" (``resolve_decode_dtype``: bf16 for
-    latents at the calibrated scale, fp16 above it, so the result stays inside §8(c)'s bound).
+    latents at the calibrated scale, fp16 above it, fp32 past fp16's calibration, so the result
+    stays inside §8(c)'s bound).
     """
     capi.require_device(latents)
     if latents.dim() == 1:
@@ -332,8 +352,10 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         state.adam = {n: (torch.zeros_like(v), torch.zeros_like(v))
                       for n, v in state.masters.items()}
         state.hparams = dict(lr=lr, weight_decay=weight_decay)
+    # gradients live in ONE flat buffer (one view per parameter): the data-parallel all-reduce
+    # then reduces that buffer in place, with no per-step concatenation or copy back
     grads = state.adam_grads if state.adam_grads is not None else \
-        {n: torch.empty_like(v) for n, v in state.masters.items()}
+        ldist.flat_buffers({n: tuple(v.shape) for n, v in state.masters.items()}, device)[1]
     T = schedule.T
     # single rank, built-in AdamW: the fused C step (no gradient all-reduce to wait for)
     fused = dtype == "bf16" and state.optimizer is None and world == 1 and fused_step

@@ -30,7 +30,6 @@ every operand row is a multiple of 16 bytes and the matrix-core path can use vec
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -118,7 +117,8 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
                            skip: int = 4, delta: float = CLAMP_DIST,
                            reg_lambda: float = CODE_REG_LAMBDA, epoch: int = 100,
                            dtype: str = "bf16",
-                           grads: Optional[Dict[str, torch.Tensor]] = None
+                           grads: Optional[Dict[str, torch.Tensor]] = None,
+                           wgrad_tile: Optional[int] = None
                            ) -> Tuple[torch.Tensor, Dict[str, torch.Tensor], torch.Tensor]:
     """One forward/backward of the DeepSDF objective on a batch of S shapes x P samples.
 
@@ -137,7 +137,8 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
                             f"sdf{tuple(sdf.shape)}")
     if dtype == "bf16":
         return _train_step_gemm_bf16(masters, z, xyz, sdf, L=L, H=H, skip=skip, delta=delta,
-                                     reg_lambda=reg_lambda, epoch=epoch, grads=grads)
+                                     reg_lambda=reg_lambda, epoch=epoch, grads=grads,
+                                     wgrad_tile=WGRAD_TILE if wgrad_tile is None else wgrad_tile)
     dev = z.device
     cp = capi.COMPUTE_CODES[dtype]
     wdt = torch.bfloat16 if dtype == "bf16" else torch.float32
@@ -213,13 +214,14 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
 
 _KQ = 128          # row padding of the sample axis (the K of the weight-gradient products)
 # ldm_gemm_bf16 tile of the weight-gradient products (128 x 128: each slice walks KT = 8192
-# samples, long enough for the bigger tile's per-CU operand economy; tuning: AD_WG_TILE)
-_WG_TILE = int(os.environ.get("AD_WG_TILE", "3"))
+# samples, long enough for the bigger tile's per-CU operand economy); tuning runs pass
+# ``wgrad_tile`` to autodecoder_train_step (the product reads no environment variable)
+WGRAD_TILE = 3
 _KSEG = 64         # column padding of [z || xyz] (a GEMM K segment)
 
 
 def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda, epoch,
-                          grads):
+                          grads, wgrad_tile=WGRAD_TILE):
     """bf16 matrix-core step on ``ldm_gemm_bf16`` (include/ldm_sdf.h).
 
     Every activation is kept once in bf16, in both layouts: ``h_l`` [Np, w] (the A operand of
@@ -346,7 +348,7 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
     cs = torch.empty(nrow32, H, **f32)
     ops.gemm([ops.gemm_problem([(g8b, W8T)], Np, H, mode="relu_bwd", M_valid=N, Rb=h[7],
                                Cb=g_cur, CbT=gT_cur, colsum=cs, ct_blk=KT)])
-    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"], 0)], tile=_WG_TILE)
+    ops.gemm([wgrad(g8row, hT[7], 1, H, gw["W8"], 0)], tile=wgrad_tile)
     colsums = {7: cs}
     gcs = {}                                       # g_l per 32-row block sums (bias / latent)
     Gs = {}                                        # per-shape column sums of g_skip and g_0
@@ -376,7 +378,7 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
             probs.append(wgrad(onehot, gT_cur, S, H, Gs[l], len(probs)))
         # weight gradients (long K per slice): larger tiles than the 1M-row G W product, so
         # their own launch
-        ops.gemm(probs, tile=_WG_TILE)
+        ops.gemm(probs, tile=wgrad_tile)
         if l > 0:
             win = h[l - 1].shape[1]
             WdT = WT["W4h"] if l == skip else WT[f"W{l}"]          # [win, wout]

@@ -14,10 +14,21 @@ exercised by CPU ``gloo`` tests with the oracle as the slab function.
 from __future__ import annotations
 
 import math
-from typing import Callable, Optional, Tuple
+import os
+import warnings
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+def init_process_group(backend: str = "nccl", **kw) -> None:
+    """``torch.distributed.init_process_group`` with RCCL set to fail fast: an RCCL error or
+    timeout on one rank aborts the communicator (``TORCH_NCCL_ASYNC_ERROR_HANDLING=1``, SURVEY
+    §5 "Fault/elastic") instead of leaving the other ranks blocked in a collective.  A value the
+    caller already exported is kept."""
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    dist.init_process_group(backend, **kw)
 
 
 def world_and_rank(group=None) -> Tuple[int, int]:
@@ -95,16 +106,63 @@ def decode_sharded(compute_slab: Callable[..., None], B: int, N: int,
     return vol
 
 
+# How a group's per-shape gathers go out: "coalesced" (one grouped collective through torch's
+# coalescing manager, the default) or "per_shape" (one async all_gather_into_tensor per shape).
+# The coalescing manager is a private torch API: if entering it raises on this backend, the
+# mode falls back to "per_shape" for the rest of the process (same bytes, more launches).
+_GATHER_MODE = {"mode": "coalesced"}
+
+
+def set_gather_mode(mode: str) -> None:
+    """Select ``_gather_group``'s form ("coalesced" or "per_shape"); both assemble the same
+    volume bit for bit (tests/test_dist_gloo.py)."""
+    if mode not in ("coalesced", "per_shape"):
+        raise ValueError("gather mode must be 'coalesced' or 'per_shape'")
+    _GATHER_MODE["mode"] = mode
+
+
+def gather_mode() -> str:
+    return _GATHER_MODE["mode"]
+
+
+class _Works:
+    """Handles of per-shape async collectives, waited on together."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self) -> None:
+        for w in self.works:
+            w.wait()
+
+
 def _gather_group(dsts, local: torch.Tensor, group):
     """One coalesced collective for a group's per-shape gathers: the group's
     ``all_gather_into_tensor(dst_b, local[b])`` calls are issued inside torch's coalescing
     manager, which hands them to the backend as ONE grouped operation (RCCL: one
-    ``ncclGroupStart/End`` launch instead of one launch per shape), asynchronously.  Returns
-    the handle to wait on."""
-    with dist._coalescing_manager(group=group, async_ops=True) as cm:
-        for b, dst in dsts:
-            dist.all_gather_into_tensor(dst, local[b], group=group)
-    return cm
+    ``ncclGroupStart/End`` launch instead of one launch per shape), asynchronously.  If the
+    manager cannot be entered (a private API: absent or refused by the backend), the same
+    gathers go out as per-shape async collectives (``set_gather_mode``).  Returns the handle
+    to wait on."""
+    if _GATHER_MODE["mode"] == "coalesced":
+        try:
+            cm = dist._coalescing_manager(group=group, async_ops=True)
+            ctx = cm.__enter__()
+        except (AttributeError, NotImplementedError, RuntimeError, TypeError) as e:
+            warnings.warn(f"dist: coalesced all-gather unavailable ({e!r}); per-shape gathers "
+                          "from now on", RuntimeWarning)
+            _GATHER_MODE["mode"] = "per_shape"
+        else:
+            try:
+                for b, dst in dsts:
+                    dist.all_gather_into_tensor(dst, local[b], group=group)
+            except BaseException:
+                cm.__exit__(*__import__("sys").exc_info())
+                raise
+            cm.__exit__(None, None, None)
+            return ctx
+    return _Works([dist.all_gather_into_tensor(dst, local[b], group=group, async_op=True)
+                   for b, dst in dsts])
 
 
 def batch_shard(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -143,9 +201,56 @@ def allreduce_sum_(tensors, group=None) -> None:
     _allreduce_(tensors, group, mean=False)
 
 
+def flat_buffers(shapes: Dict[str, Tuple[int, ...]], device, dtype=torch.float32
+                 ) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """One flat buffer and a view of it per named shape, in order, each view starting at a
+    16-byte multiple (so the views stay valid operands of the aligned C ABI).  Gradients kept
+    in such views are all-reduced as the flat buffer itself: no per-step ``torch.cat`` of 40 MB
+    and no copy back (``_allreduce_``)."""
+    per = 16 // torch.empty((), dtype=dtype).element_size()
+    offs, n = [], 0
+    for shp in shapes.values():
+        offs.append(n)
+        n += -(-math.prod(shp) // per) * per
+    flat = torch.zeros(n, device=device, dtype=dtype)
+    views = {k: flat[o:o + math.prod(shp)].view(shp)
+             for (k, shp), o in zip(shapes.items(), offs)}
+    return flat, views
+
+
+def _flat_base(tensors: List[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The 1-D buffer the tensors are consecutive views of (``flat_buffers`` layout, gaps of
+    padding allowed), or None."""
+    if not tensors:
+        return None
+    base = tensors[0]._base
+    if base is None or base.dim() != 1 or not base.is_contiguous():
+        return None
+    es = base.element_size()
+    start = base.data_ptr()
+    pos = 0
+    for t in tensors:
+        if t._base is not base or not t.is_contiguous():
+            return None
+        o = (t.data_ptr() - start) // es
+        if o < pos or (o - pos) * es >= 16:    # only alignment padding may lie between views
+            return None
+        pos = o + t.numel()
+    return base[:pos]
+
+
 def _allreduce_(tensors, group, mean: bool) -> None:
     world, _ = world_and_rank(group)
     if world == 1:
+        return
+    tensors = list(tensors)
+    flat = _flat_base(tensors)
+    if flat is not None:
+        # views of one persistent buffer: reduce it in place (padding between views is zero on
+        # every rank and stays zero)
+        dist.all_reduce(flat, group=group)
+        if mean:
+            flat.div_(world)
         return
     flat = torch.cat([t.reshape(-1) for t in tensors])
     dist.all_reduce(flat, group=group)

@@ -80,7 +80,8 @@ class SDFDecoder:
         return (self.hidden == 512 and self.n_hidden == 8 and self.skip == 4
                 and self.skip_width in (253, 512))
 
-    # the feature-split kernel (csrc/decoder_fs.hip); "split16" (decoder_fs16.hip) is selectable
+    # the feature-split kernel (csrc/decoder_fs.hip; the 16x16x32 "split16" variant was deleted
+    # in ABI 7, 5.5 % slower)
     DEFAULT_LAYOUT = "split"
 
     def invalidate(self) -> None:
@@ -270,25 +271,43 @@ class MLPDenoiser:
         rebuilds from the trained weights; the working copies (and graphs that captured their
         addresses) stay valid.
 
-        Retention: the tables of the PREVIOUS generation only stay allocated, so a graph
-        captured outside ``Sampler`` on them is still safe to replay once (until the next
-        ``train``).  ``Sampler`` itself re-packs and re-captures on a ``table_gen`` change
-        before its next launch, so it never needs older tables; keeping every generation
-        pinned 4 x [T, H] fp32 per ``train`` call."""
+        Retention: the tables of the PREVIOUS generation stay allocated here; beyond that,
+        every stepper / loop closure (``make_stepper`` / ``make_loop``) holds the tensors its
+        descriptor pointed at when it was made, so a graph captured from one replays on valid
+        (old) memory however many ``train`` calls later, and calling a stale closure raises
+        ``LdmError``.  ``Sampler`` re-packs and re-captures on a ``table_gen``
+        change before its next launch."""
         for dev in self._dev.values():
             old = [dev.pop(f"etab{k}") for k in range(self.n_blocks) if f"etab{k}" in dev]
             if old:
                 dev["_stale_etab"] = old      # replaces (frees) the generation before it
         self.table_gen += 1
 
+    def _pinned_pack(self, dtype: str, device):
+        """(desc, keep, gen): the pack's descriptor, the device tensors its pointers name (held by
+        a stepper / loop closure, so a graph captured from the closure never replays on freed
+        memory, whatever ``invalidate_tables`` drops later), and the table generation."""
+        pack = self.device_pack(dtype, device)
+        keep = [v for k, v in pack.items() if isinstance(v, torch.Tensor)]
+        return pack["desc"], keep, self.table_gen
+
+    def _check_gen(self, gen: int, what: str) -> None:
+        if self.table_gen != gen:
+            raise capi.LdmError(f"{what}: the denoiser was trained or re-packed since this "
+                                "callable was made (its E tables / weights are stale); make a "
+                                "new one (Sampler does so itself)")
+
     def make_stepper(self, n: int, dtype: str, device, sched_desc):
-        """Callable ``step(x, z, t, x_out)``: one fused reverse step (``ldm_sample_step``)."""
+        """Callable ``step(x, z, t, x_out)``: one fused reverse step (``ldm_sample_step``).
+        Raises ``LdmError`` once the denoiser's tables changed under it (``table_gen``)."""
         from . import ops
-        desc = self.device_pack(dtype, device)["desc"]
+        desc, keep, gen = self._pinned_pack(dtype, device)
         ws = torch.empty(2 * n * self.H, device=device)
 
         def step(x, z, t, x_out):
+            self._check_gen(gen, "sampling stepper")
             ops.sample_step(desc, sched_desc, x, z, t, x_out, ws)
+        step.keep = keep
         return step
 
     def make_loop(self, n: int, dtype: str, device, sched_desc):
@@ -296,14 +315,16 @@ class MLPDenoiser:
         persistent launch (``ldm_sample_loop``), or None when the shape has no persistent
         kernel (the per-step stepper is used then)."""
         from . import ops
-        desc = self.device_pack(dtype, device)["desc"]
+        desc, keep, gen = self._pinned_pack(dtype, device)
         if not ops.sample_loop_supported(desc, n):
             return None
         ws = ops.sample_loop_workspace(desc, n, device)
 
         def loop(x2, noise, t_hi, steps):
+            self._check_gen(gen, "sampling loop")
             ops.sample_loop(desc, sched_desc, x2, noise, t_hi, steps, ws)
             return ws
+        loop.keep = keep
         loop.status = lambda: ops.sample_loop_status(desc, ws, n)
         loop.form = ops.sample_loop_last_form     # which kernel the last launch ran
         # status 2 (replica placement mismatch) switches this device to the chip-wide loop

@@ -3,9 +3,8 @@
 Canonical DeepSDF weights (``[out, in]`` per linear, weight-norm already folded -- see
 ``fold_weight_norm``) are turned into what ``libldm_sdf.so`` streams:
 
-* bf16/f16 MFMA kernels: per-wave weight streams of ``v_mfma_f32_32x32x16`` A fragments
-  ("split", csrc/decoder_fs.hip, ``pack_split``) or ``16x16x32`` ones ("split16",
-  csrc/decoder_fs16.hip, ``pack_split16``), each fragment stored ``[lane l][element j]``.
+* bf16/f16 MFMA kernel: per-wave weight streams of ``v_mfma_f32_32x32x16`` A fragments
+  ("split", csrc/decoder_fs.hip, ``pack_split``), each fragment stored ``[lane l][element j]``.
   ``PERM`` is the row order in which a 32x32 accumulator, converted pairwise to 16-bit,
   becomes the next layer's B fragment (cdna_hip_programming.md §3, 'accumulator tile as the
   next MFMA's operand').  Bias (and xyz for layers 0/4) enter as an *aux* k-step whose columns
@@ -47,9 +46,8 @@ def n_stages(skip_width: int, layout: str = "split") -> int:
     """``ldm_decoder_t.n_stages`` of a 16-bit blob in ``layout`` (split: k-steps per wave)."""
     if layout == "split":
         return split_stream_steps(skip_width)
-    if layout == "split16":
-        return split16_stream_steps(skip_width)
-    raise ValueError(f"unknown decoder layout {layout!r} (pass8 / quarter were removed)")
+    raise ValueError(f"unknown decoder layout {layout!r} (pass8 / quarter were removed in ABI "
+                     "5, split16 in ABI 7)")
 
 
 def _round(x: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
@@ -187,85 +185,6 @@ def pack_split(pieces: Dict[str, torch.Tensor], dt: torch.dtype) -> Tuple[torch.
     return torch.cat([stream.reshape(-1), aux.reshape(-1)]), nsteps
 
 
-# ------------------------------------------------------------------------------------------
-# "split16" layout (csrc/decoder_fs16.hip): the split work division on
-# v_mfma_f32_16x16x32.  Operand maps (16x16x32): lane l of an A fragment holds row l & 15,
-# k = 8 (l >> 4) + e; of a B fragment column l & 15, same k; accumulator register v of lane l
-# is row 4 (l >> 4) + v, column l & 15.  A tile is 8 point chunks of 16; wave w owns the
-# output rows of split_row_base as 4 m-chunks of 16 per part; a k-step is 32 input features.
-# The activations sit in 16 LDS positions: after a two-part layer, position 8u + 2w' + q holds
-# features 128 w' + 64 u + 32 q + f(k), after DeepSDF's one-part layer 3 (skip 253) position
-# 8 + 2w' + q holds 64 w' + 32 q + f(k), with f(8h + e) = 16 (e >> 2) + 4h + (e & 3) (an
-# accumulator pair of m-chunks 2q, 2q + 1 becoming a B fragment).  Step j of a part reads
-# position pos0 + j.  Biases are fp32, added in the epilogue.
-# ------------------------------------------------------------------------------------------
-def split16_nk(layer: int, skip_width: int) -> int:
-    """k-steps (32 features each) of one part of ``layer`` (the aux step not counted)."""
-    return 0 if layer == 0 else (skip_pad(skip_width) // 32 if layer == 4 else 16)
-
-
-def split16_pos0(layer: int, skip_width: int) -> int:
-    return 8 if layer == 4 and skip_pad(skip_width) == 256 else 0
-
-
-def split16_feature(layer: int, pos: np.ndarray, k: np.ndarray, skip_width: int) -> np.ndarray:
-    """Input feature of ``layer`` at LDS position ``pos``, B-fragment row ``k``."""
-    h, e = k >> 3, k & 7
-    off = 16 * (e >> 2) + 4 * h + (e & 3)
-    if layer == 4 and skip_pad(skip_width) == 256:       # produced by the one-part layer 3
-        wq = pos - 8
-        return 64 * (wq >> 1) + 32 * (wq & 1) + off
-    return 128 * ((pos & 7) >> 1) + 64 * (pos >> 3) + 32 * (pos & 1) + off
-
-
-def split16_stream_steps(skip_width: int) -> int:
-    return sum(split16_nk(l, skip_width) for (l, _) in split_parts(skip_width))
-
-
-def pack_split16(pieces: Dict[str, torch.Tensor], dt: torch.dtype) -> Tuple[torch.Tensor, int]:
-    """Split16 blob: ``stream [4 waves][n_steps][4 frags][64 lanes][8]`` (dt) then fp32
-    ``bias [4 waves][n_parts][4 h][4 i][4 v]`` (row ``row_base + 16 i + 4 h + v``; zero for
-    layers 0 and 4, whose bias is in the folded latent of the aux step), viewed as dt.  Stream
-    element (wave w, step s = part (l, p)'s step j, m-chunk i, lane ln, elem e) =
-    ``W_l[row_base + 16 i + (ln & 15), split16_feature(l, pos0 + j, 8 (ln >> 4) + e)]``."""
-    sw = pieces["skip_width"]
-    S = skip_pad(sw)
-    parts = split_parts(sw)
-    nsteps = split16_stream_steps(sw)
-    lanes = np.arange(64)
-    kk = 8 * (lanes >> 4)[:, None] + np.arange(8)[None, :]                      # [64, 8]
-    padded = {}
-    for l in range(1, 8):
-        w = pieces["main"][l]
-        M = S if l == 3 else H
-        K = S if l == 4 else H
-        wp = torch.zeros(M, K, dtype=torch.float64)
-        wp[:w.shape[0], :w.shape[1]] = w
-        padded[l] = _round(wp, dt)
-    stream = torch.zeros(SPLIT_WAVES, nsteps, 4, 64, 8, dtype=dt)
-    bias = torch.zeros(SPLIT_WAVES, len(parts), 4, 4, 4, dtype=torch.float32)
-    hh, ii, vv = np.meshgrid(np.arange(4), np.arange(4), np.arange(4), indexing="ij")
-    for w in range(SPLIT_WAVES):
-        s0 = 0
-        for pi, (l, p) in enumerate(parts):
-            rb = split_row_base(l, p, w, sw)
-            if l not in (0, 4):
-                bp = torch.zeros(S if l == 3 else H, dtype=torch.float64)
-                bp[:pieces["bias"][l].shape[0]] = pieces["bias"][l]
-                bias[w, pi] = bp[torch.from_numpy(rb + 16 * ii + 4 * hh + vv)].to(torch.float32)
-            nk = split16_nk(l, sw)
-            if nk == 0:
-                continue
-            pos = split16_pos0(l, sw) + np.arange(nk)                                # [nk]
-            cols = torch.from_numpy(split16_feature(l, pos[:, None, None], kk[None], sw))
-            rows = torch.from_numpy(rb + 16 * np.arange(4)[:, None] + (lanes & 15)[None, :])
-            # [nk, 4, 64, 8]: W[rows[i, ln], cols[j, ln, e]]
-            stream[w, s0:s0 + nk] = padded[l][rows[None, :, :, None], cols[:, None, :, :]]
-            s0 += nk
-        assert s0 == nsteps
-    return torch.cat([stream.reshape(-1), bias.reshape(-1).view(dt)]), nsteps
-
-
 def permute_w_last_split(w_last: torch.Tensor) -> torch.Tensor:
     """Final-layer weights in the split kernel's accumulator order:
     ``wl[w][p][i][h][v] = w8[128 w + 64 p + 32 i + (v & 3) + 8 (v >> 2) + 4 h]``."""
@@ -289,8 +208,7 @@ def pack_f32_blob(pieces: Dict[str, torch.Tensor]) -> torch.Tensor:
 def pack_decoder(weights, biases, latent_dim: int, dtype: str,
                  layout: str = "split") -> Dict[str, object]:
     """All host-side arrays of an ``ldm_decoder_t`` for ``dtype`` in {fp32, bf16, fp16}; the
-    16-bit weights in ``layout`` ("split": csrc/decoder_fs.hip, the default; "split16":
-    csrc/decoder_fs16.hip)."""
+    16-bit weights in ``layout`` ("split": csrc/decoder_fs.hip, the only one since ABI 7)."""
     pieces = canonical_pieces(weights, biases, latent_dim)
     out = {
         "skip_width": pieces["skip_width"],
@@ -305,12 +223,6 @@ def pack_decoder(weights, biases, latent_dim: int, dtype: str,
         out["weights"] = pack_f32_blob(pieces)
         out["w_last"] = pieces["w_last"].to(torch.float32).contiguous()
         out["n_stages"] = 0
-    elif dtype in ("bf16", "fp16") and layout == "split16":
-        dt = torch.bfloat16 if dtype == "bf16" else torch.float16
-        blob, nst = pack_split16(pieces, dt)
-        out["weights"] = blob.contiguous()
-        out["w_last"] = pieces["w_last"].to(torch.float32).contiguous()   # natural order
-        out["n_stages"] = nst
     elif dtype in ("bf16", "fp16") and layout == "split":
         dt = torch.bfloat16 if dtype == "bf16" else torch.float16
         blob, nst = pack_split(pieces, dt)
@@ -319,7 +231,7 @@ def pack_decoder(weights, biases, latent_dim: int, dtype: str,
         out["n_stages"] = nst
     elif dtype in ("bf16", "fp16"):
         raise ValueError(f"unknown decoder layout {layout!r} (pass8 / quarter were removed in "
-                         "ABI 5; use 'split')")
+                         "ABI 5, split16 in ABI 7; use 'split')")
     else:
         raise ValueError(f"unknown decoder dtype {dtype!r}")
     return out

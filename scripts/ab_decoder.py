@@ -14,9 +14,9 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 R = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 # variants: "s" = split layout (default kernel), "s<V>" (V = 1..3) = split with kernel variant
-# FV = V (LDM_FS_V, needs the `make DEV=1` library: csrc/decoder_fs.hip), "s16" = split16
-VARIANTS = os.environ.get("AB_VARIANTS", "s,s16").split(",")
-LAYOUT = {v: ("split16" if v == "s16" else "split") for v in VARIANTS}
+# FV = V (LDM_FS_V, needs the `make DEV=1` library: csrc/decoder_fs.hip)
+VARIANTS = os.environ.get("AB_VARIANTS", "s,s2").split(",")
+LAYOUT = {v: "split" for v in VARIANTS}
 FLOPS = 3146752
 dev = torch.device("cuda", 0)
 dec = ldm_sdf.SDFDecoder(256, seed=1234)

@@ -1,8 +1,8 @@
 """CPU emulation of the MFMA decoder kernel's data flow (TEST INFRASTRUCTURE).
 
-Follows csrc/decoder_fs.hip (split layout) and csrc/decoder_fs16.hip (split16) at the
+Follows csrc/decoder_fs.hip (split layout) at the
 fragment level -- the packed per-wave weight streams, the per-shape aux fragments, the B
-fragment built from xyz, the v_mfma_f32_32x32x16 / 16x16x32 operand/result lane maps
+fragment built from xyz, the v_mfma_f32_32x32x16 operand/result lane maps
 (cdna_hip_programming.md §3), the accumulator -> next-B-fragment conversion with 16-bit
 rounding + ReLU and the fused fp32 final layer -- so the host packer (ldm_sdf/pack.py) is
 validated against the oracle without a GPU.  Accumulation is fp64 here,
@@ -143,118 +143,4 @@ def emulate_split(packed: dict, beta: np.ndarray, xyz: np.ndarray, dtype: str) -
                 act = new_act
             tot = part_acc[:, :32] + part_acc[:, 32:]                # [n, 32]
             out[b, g0:g0 + 128] = np.tanh(tot.reshape(-1) + packed["b_last"])
-    return out
-
-
-# ---- split16 layout (csrc/decoder_fs16.hip): v_mfma_f32_16x16x32 maps ----------------------
-# A: Am[r][k] = frag[lane = r + 16 (k // 8)][k % 8] (B likewise with r -> column); accumulator
-# register v of lane l = row 4 (l >> 4) + v, column l & 15.
-_K32 = np.arange(32)
-_LANE16 = np.arange(16)[:, None] + 16 * (_K32[None, :] // 8)             # [16 r, 32 k]
-_ELEM16 = np.broadcast_to(_K32[None, :] % 8, (16, 32))
-
-
-def frag16_to_A(frag: np.ndarray) -> np.ndarray:
-    """frag [64, 8] -> A[16 rows, 32 k]."""
-    return frag[_LANE16, _ELEM16]
-
-
-def acc16_pair_to_B(C0: np.ndarray, C1: np.ndarray, bias0, bias1, dt) -> np.ndarray:
-    """The epilogue unit of decoder_fs16.hip: accumulators of m-chunks 2q (C0) and 2q+1 (C1)
-    [16 rows, 16 cols] + fp32 bias rows, 16-bit rounding, ReLU -> one B matrix [32 k, 16]:
-    k = 8h + e holds row 4h + (e & 3) of C0 (e < 4) or C1 (e >= 4)."""
-    Bm = np.zeros((32, 16))
-    for h in range(4):
-        for e in range(8):
-            C, b = (C0, bias0) if e < 4 else (C1, bias1)
-            r = 4 * h + (e & 3)
-            y = (C[r, :] + b[r]).astype(np.float32)
-            Bm[8 * h + e] = np.maximum(round_dt(y, dt), 0.0)
-    return Bm
-
-
-def emulate_split16(packed: dict, beta: np.ndarray, xyz: np.ndarray, dtype: str) -> np.ndarray:
-    """Dataflow replay of the split16 layout (csrc/decoder_fs16.hip) from the packed blob: per
-    part, the aux step (layers 0 / 4: [wx,wy,wz,wx,wy,wz,beta_hi,beta_lo] x [xyz hi/lo, 1, 1]),
-    then k-step j = A fragments of the wave's stream x the B fragments at LDS position
-    pos0 + j; the epilogue adds the blob's fp32 bias (rows 16i + 4h + v at float 16h + 4i + v),
-    rounds, ReLUs and writes position 8u + 2w + q (layer 3 at skip 253: 8 + 2w + q); layer 7
-    folds into the fp32 dot product with w_last (natural order).  xyz [B, P, 3], P a multiple
-    of 128 -> sdf [B, P]."""
-    dt = torch.bfloat16 if dtype == "bf16" else torch.float16
-    sw = packed["skip_width"]
-    S = pack.skip_pad(sw)
-    parts = pack.split_parts(sw)
-    nst = packed["n_stages"]
-    blob = packed["weights"]
-    ns = 4 * nst * 4 * 64 * 8
-    stream = blob[:ns].to(torch.float64).numpy().reshape(4, nst, 4, 64, 8)
-    bias = blob[ns:].contiguous().view(torch.float32).to(torch.float64).numpy()
-    bias = bias.reshape(4, len(parts), 4, 4, 4)                       # [w][pi][h][i][v]
-    wl = packed["w_last"].numpy().astype(np.float64)
-    wxyz = packed["wxyz"].numpy().astype(np.float64)
-    B, P, _ = xyz.shape
-    out = np.zeros((B, P))
-    for b in range(B):
-        for g0 in range(0, P, 128):
-            auxB = []
-            for n in range(8):
-                x = xyz[b, g0 + 16 * n:g0 + 16 * n + 16].astype(np.float32)
-                hi = round_dt(x, dt)
-                lo = round_dt(x.astype(np.float64) - hi, dt)
-                m = np.zeros((32, 16))
-                m[0:3], m[3:6], m[6:8] = hi.T, lo.T, 1.0
-                auxB.append(m)
-            act = {}
-            fin = np.zeros(128)
-            pos_w = [0] * 4
-            for layer in range(8):
-                new_act = {}
-                for w in range(4):
-                    for pi, (l, p) in enumerate(parts):
-                        if l != layer:
-                            continue
-                        rb = pack.split_row_base(l, p, w, sw)
-                        rows = rb + 16 * np.arange(4)[:, None] + np.arange(16)[None, :]   # [i, r]
-                        if l in (0, 4):
-                            li = 0 if l == 0 else 1
-                            C = []
-                            for i in range(4):
-                                f = rows[i]
-                                A = np.zeros((16, 32))
-                                hb = round_dt(beta[b, li, f], dt)
-                                A[:, 0:3] = round_dt(wxyz[li][f], dt)
-                                A[:, 3:6] = round_dt(wxyz[li][f], dt)
-                                A[:, 6] = hb
-                                A[:, 7] = round_dt(beta[b, li, f] - hb, dt)
-                                C.append([A @ auxB[n] for n in range(8)])
-                        else:
-                            C = [[np.zeros((16, 16)) for _ in range(8)] for _ in range(4)]
-                        nk = pack.split16_nk(l, sw)
-                        p0 = pack.split16_pos0(l, sw)
-                        for j in range(nk):
-                            fr = stream[w, pos_w[w] + j]
-                            for i in range(4):
-                                A = frag16_to_A(fr[i])
-                                for n in range(8):
-                                    C[i][n] = C[i][n] + A @ act[p0 + j][n]
-                        pos_w[w] += nk
-                        # bias rows of m-chunk i: row r = 4h + v <- float [h][i][v]
-                        bi = [np.array([bias[w, pi, r >> 2, i, r & 3] for r in range(16)])
-                              for i in range(4)]
-                        if l == 0:
-                            bi = [np.zeros(16)] * 4
-                        if l == 7:
-                            for i in range(4):
-                                for n in range(8):
-                                    y = np.maximum(C[i][n] + bi[i][:, None], 0.0)
-                                    fin[16 * n:16 * n + 16] += (y * wl[rows[i]][:, None]).sum(0)
-                            continue
-                        late = 8 if (l == 3 and S == 256) else 8 * p
-                        for q in range(2):
-                            new_act[late + 2 * w + q] = [
-                                acc16_pair_to_B(C[2 * q][n], C[2 * q + 1][n], bi[2 * q],
-                                                bi[2 * q + 1], dt) for n in range(8)]
-                act = new_act
-            out[b, g0:g0 + 128] = np.tanh(fin + packed["b_last"])
     return out

@@ -31,14 +31,14 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_error_path_without_gpu():
     from ldm_sdf import _capi as capi
     lib = capi.load()
-    assert lib.ldm_abi_version() == 6
+    assert lib.ldm_abi_version() == 7
     # argument validation runs before any device work
     assert lib.ldm_grid_coords(0, 0, 0, 0.0, 0.0, None, None) == -22
     assert b"bad grid slab" in lib.ldm_last_error()
     assert lib.ldm_decoder_grid_fwd(None, None, 1, 8, 0, 8, 0.1, -1.0, None, None, 0, None) != 0
-    assert lib.ldm_workspace_bytes(1, 4, 256, 1) == 4 * 8 * 8192            # max over layouts
+    assert lib.ldm_workspace_bytes(1, 4, 256, 1) == 4 * 4 * 8192            # the split layout
     assert lib.ldm_workspace_bytes_layout(1, 4, 256, 1, 2) == 4 * 4 * 8192   # split layout
-    assert lib.ldm_workspace_bytes_layout(1, 4, 256, 1, 3) == 4 * 8 * 8192   # split16 layout
+    assert lib.ldm_workspace_bytes_layout(1, 4, 256, 1, 3) == 0   # split16: removed in ABI 7
 
 
 def test_struct_layouts_match_c():

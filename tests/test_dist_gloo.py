@@ -88,6 +88,47 @@ def _volume_oracle(rank, world):
     return float((vol - full).abs().max())
 
 
+def _volume_modes(rank, world):
+    """The z-slab gather in both forms (one coalesced collective per group, per-shape async
+    collectives): bitwise the same volume (uneven N, 5 shapes in groups of 2)."""
+    from ldm_sdf import dist as D
+    B, N = 5, 13
+
+    def slab(k0, k1, dst, b0, b1):
+        g = torch.Generator().manual_seed(1000 * b0 + k0)
+        dst.copy_(torch.randn(dst.shape, generator=g))
+
+    out = {}
+    for mode in ("coalesced", "per_shape"):
+        D.set_gather_mode(mode)
+        out[mode] = D.decode_sharded(slab, B, N, torch.device("cpu"), shapes_per_group=2)
+    D.set_gather_mode("coalesced")
+    return bool(torch.equal(out["coalesced"], out["per_shape"]))
+
+
+def _flat_allreduce(rank, world):
+    """Gradients kept as views of one flat buffer (dist.flat_buffers) are all-reduced in place,
+    without a concatenated copy; a non-flat list still takes the copy path; same values."""
+    from ldm_sdf.dist import _flat_base, allreduce_mean_, flat_buffers
+    shapes = {"a": (3, 5), "b": (7,), "c": (2, 2, 3)}
+    flat, v = flat_buffers(shapes, torch.device("cpu"))
+    ok = _flat_base(list(v.values())) is not None and _flat_base([v["a"], v["c"]]) is None
+    ok = ok and all(t.data_ptr() % 16 == 0 for t in v.values())
+    loose = {}
+    for i, (k, t) in enumerate(v.items()):
+        t.copy_(torch.arange(t.numel()).view(t.shape).float() * (rank + 1) + i)
+        loose[k] = t.clone()
+    ptr = flat.data_ptr()
+    allreduce_mean_(list(v.values()))
+    allreduce_mean_(list(loose.values()))
+    ok = ok and flat.data_ptr() == ptr
+    ok = ok and all(torch.equal(v[k], loose[k]) for k in v)
+    # padding between views stays zero
+    used = sum(t.numel() for t in v.values())
+    ok = ok and float(flat.abs().sum()) == float(sum(t.abs().sum() for t in v.values()))
+    return bool(ok) and used < flat.numel()
+
+
 def _rows(rank, world):
     from ldm_sdf.dist import all_gather_rows, batch_shard
     n = 7
@@ -152,6 +193,17 @@ def test_zslab_oracle_matches_single_rank():
 def test_uneven_batch_gather(world):
     res = _run("_rows", world)
     assert all(res[r] is True for r in range(world)), res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_modes_bitwise(world):
+    res = _run("_volume_modes", world)
+    assert all(res[r] is True for r in range(world)), res
+
+
+def test_flat_grad_allreduce():
+    res = _run("_flat_allreduce", 2)
+    assert all(res[r] is True for r in range(2)), res
 
 
 def test_grad_allreduce_mean():

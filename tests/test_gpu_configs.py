@@ -1,8 +1,8 @@
 """The BASELINE.json configs at their own sizes, on the MI355X, against the oracle.
 
 * config 2 -- the bf16 DDPM training step at batch 1000 on 1k latents (`BASELINE.json:8`);
-* config 3 -- 1000-step bf16 sampling of 8 latents -> bf16 decode of a 128^3 grid
-  (`BASELINE.json:9`);
+* config 3 -- 1000-step bf16 sampling of 8 latents -> 16-bit decode of a 128^3 grid
+  (`BASELINE.json:9`; bf16 / fp16 as dtype="auto" picks for the latents' scale);
 * config 5 -- fp16 decode of a 512^3 grid with the widen-skip decoder, L = 1024
   (`BASELINE.json:11`; the UNet sampling half is pinned in test_gpu_unet.py).
 
@@ -69,13 +69,15 @@ def test_config2_train_step_bf16_batch1000(dev):
 
 
 def test_config3_sample8_then_decode128(dev):
-    """Config 3 end to end: sample(8) (1000 bf16 steps, the default persistent loop) ->
-    decode(128^3, bf16).  The latents are checked against the fp64 oracle on the bf16-rounded
-    weights (relative 2e-5, see test_gpu_ddpm.py), and the volume on 600 random points per
-    shape against the fp64 oracle decoder fed those same latents.  The untrained synthetic
-    denoiser drives the latents to ~1e8, where every SDF saturates at +-1, so the volume is
-    also checked for latents brought to the decoder's operating range (each shape's sampled
-    code rescaled to RMS 0.1, the synthetic-latent scale of SURVEY.md §8(d))."""
+    """Config 3 end to end with the untrained synthetic denoiser: sample(8) (1000 bf16 steps,
+    the default persistent loop) -> decode(128^3, bf16).  The latents are checked against the
+    fp64 oracle on the bf16-rounded weights (relative 2e-5, see test_gpu_ddpm.py).  That
+    denoiser drives the latents to ~1e8, where every SDF saturates at +-1, so dtype="auto"
+    refuses the 16-bit kernels there (fp32, api.FP16_MAX_LATENT_RMS) and the volume is checked
+    for the sampled codes brought to the decoder's operating range (each rescaled to RMS 0.1,
+    the synthetic-latent scale of SURVEY.md §8(d)) on 600 random points per shape against the
+    fp64 oracle decoder.  The fp16 "auto" path on latents AS SAMPLED (bounded regime, not
+    saturated) is test_gpu_ddpm.py::test_config3_bounded_sample8_then_decode128_unscaled."""
     import ldm_sdf
     from oracle import ref_cpu as R
     from tests.test_gpu_ddpm import _bf16_rounded_params, _oracle_sample
@@ -92,9 +94,11 @@ def test_config3_sample8_then_decode128(dev):
     dec = ldm_sdf.SDFDecoder(256, weights=pd.weights, biases=pd.biases)
     N = 128
     grid = torch.from_numpy(R.grid_coords_np(N)).double()
+    assert ldm_sdf.resolve_decode_dtype("auto", lat) == "fp32"
     scaled = lat / lat.pow(2).mean(dim=1, keepdim=True).sqrt() * 0.1
-    for z in (lat, scaled):
-        vol = ldm_sdf.decode(dec, z, N, dtype="bf16")
+    assert ldm_sdf.resolve_decode_dtype("auto", scaled) == "bf16"
+    for z in (scaled,):
+        vol = ldm_sdf.decode(dec, z, N)
         assert vol.shape == (8, N, N, N) and bool(torch.isfinite(vol).all())
         idx = torch.randint(0, N ** 3, (8, 600), generator=gen)
         got = vol.reshape(8, -1)[torch.arange(8)[:, None], idx.to(dev)].cpu().double()

@@ -67,33 +67,23 @@ def test_fold_matches_oracle(dev, decoder, small):
     assert (beta - want).abs().max() < 1e-5
 
 
-@pytest.mark.parametrize("layout", ["split", "split16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
-def test_decode_grid_32_vs_golden(dev, decoder, small, dtype, layout):
+def test_decode_grid_32_vs_golden(dev, decoder, small, dtype):
     import ldm_sdf
     z = torch.from_numpy(small["z"]).to(dev)
-    decoder.DEFAULT_LAYOUT = layout
-    try:
-        sdf = ldm_sdf.decode(decoder, z, 32, dtype=dtype).cpu().double().numpy()
-    finally:
-        del decoder.DEFAULT_LAYOUT          # back to the class default
+    sdf = ldm_sdf.decode(decoder, z, 32, dtype=dtype).cpu().double().numpy()
     want = small["sdf_grid"].reshape(2, 32, 32, 32)
     err = np.abs(sdf - want).max()
     assert err <= TOL[dtype], (dtype, err)
     assert np.isfinite(sdf).all()
 
 
-@pytest.mark.parametrize("layout", ["split", "split16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp16", "bf16"])
-def test_decode_points_ragged_vs_golden(dev, decoder, small, dtype, layout):
+def test_decode_points_ragged_vs_golden(dev, decoder, small, dtype):
     import ldm_sdf
     z = torch.from_numpy(small["z"]).to(dev)
     pts = torch.from_numpy(small["pts"]).to(dev)          # [2, 1000, 3], 1000 % 128 != 0
-    decoder.DEFAULT_LAYOUT = layout
-    try:
-        got = ldm_sdf.decode_points(decoder, z, pts, dtype=dtype).cpu().double().numpy()
-    finally:
-        del decoder.DEFAULT_LAYOUT          # back to the class default
+    got = ldm_sdf.decode_points(decoder, z, pts, dtype=dtype).cpu().double().numpy()
     err = np.abs(got - small["sdf_pts"]).max()
     assert err <= TOL[dtype], (dtype, err)
 
@@ -120,9 +110,7 @@ def test_widen_skip_fp16(dev):
     assert dec.widen_skip and dec.skip_width == 512
     z = torch.from_numpy(g["z"]).to(dev)
     pts = torch.from_numpy(g["pts"]).to(dev)
-    for dt, lay in (("fp16", "split"), ("fp16", "split16"), ("bf16", "split"),
-                    ("bf16", "split16"), ("fp32", "split")):
-        dec.DEFAULT_LAYOUT = lay
+    for dt, lay in (("fp16", "split"), ("bf16", "split"), ("fp32", "split")):
         got = ldm_sdf.decode_points(dec, z, pts, dtype=dt).cpu().double().numpy()
         assert np.abs(got - g["sdf_pts"]).max() <= TOL[dt], (dt, lay)
         lowp = R.decoder_forward_lowp(p, z.cpu().double(), pts.cpu().double(),
@@ -132,8 +120,7 @@ def test_widen_skip_fp16(dev):
 
 
 @pytest.mark.parametrize("dtype,layout", [("fp32", "split"), ("bf16", "split"),
-                                          ("bf16", "split16"), ("fp16", "split"),
-                                          ("fp16", "split16")])
+                                          ("fp16", "split")])
 def test_slab_equals_slice_bitwise(dev, decoder, small, dtype, layout):
     """Each point's value is independent of its tile/slab: slabs are bitwise slices."""
     from ldm_sdf import ops
@@ -150,19 +137,14 @@ def test_slab_equals_slice_bitwise(dev, decoder, small, dtype, layout):
     assert torch.equal(one[0], full[1])
 
 
-@pytest.mark.parametrize("layout", ["split", "split16"])
-def test_many_tiles_persistent_loop_subset(dev, decoder, layout):
+def test_many_tiles_persistent_loop_subset(dev, decoder):
     """64^3 x 3 shapes = 6144 tiles (> 1 per CU): spot-check vs the oracle on a subset."""
     import ldm_sdf
     from oracle import ref_cpu as R
     g = torch.Generator().manual_seed(3)
     z = torch.randn(3, 256, generator=g) * 0.1
     N = 64
-    decoder.DEFAULT_LAYOUT = layout
-    try:
-        sdf = ldm_sdf.decode(decoder, z.to(dev), N, dtype="bf16").cpu()
-    finally:
-        del decoder.DEFAULT_LAYOUT          # back to the class default
+    sdf = ldm_sdf.decode(decoder, z.to(dev), N, dtype="bf16").cpu()
     idx = torch.randint(0, N ** 3, (3, 600), generator=g)
     grid = torch.from_numpy(R.grid_coords_np(N))
     p = R.make_decoder_params(seed=1234)
@@ -191,11 +173,10 @@ def test_errors_are_loud(dev, decoder):
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("scale", [0.1, 0.5])
-def test_split_vs_lowp_oracle_and_split16(dev, decoder, dtype, scale):
-    """The feature-split kernels (decoder_fs.hip, decoder_fs16.hip) on 3 shapes x 1000 random
-    points (8 tiles per shape, ragged): each within 2e-3 of the 16-bit precision-contract oracle
-    (fp32 summation order and rounding-tie flips only), and of each other (they sum the k-steps
-    in another order), at the synthetic latent scale and at 5x it."""
+def test_split_vs_lowp_oracle(dev, decoder, dtype, scale):
+    """The feature-split kernel (decoder_fs.hip) on 3 shapes x 1000 random points (8 tiles per
+    shape, ragged): within the 16-bit precision-contract oracle's rounding (fp32 summation order
+    and rounding-tie flips only), at the synthetic latent scale and at 5x it."""
     import ldm_sdf
     from oracle import ref_cpu as R
     g = torch.Generator().manual_seed(17)
@@ -203,24 +184,34 @@ def test_split_vs_lowp_oracle_and_split16(dev, decoder, dtype, scale):
     pts = torch.rand(3, 1000, 3, generator=g) * 2 - 1
     p = R.make_decoder_params(seed=1234)
     dt = torch.bfloat16 if dtype == "bf16" else torch.float16
-    out = {}
-    for lay in ("split", "split16"):
-        decoder.DEFAULT_LAYOUT = lay
-        try:
-            out[lay] = ldm_sdf.decode_points(decoder, z.to(dev), pts.to(dev),
-                                             dtype=dtype).cpu().double()
-        finally:
-            del decoder.DEFAULT_LAYOUT
+    out = {"split": ldm_sdf.decode_points(decoder, z.to(dev), pts.to(dev),
+                                          dtype=dtype).cpu().double()}
     lowp = R.decoder_forward_lowp(p, z.double(), pts.double(), dt)
     # fp32 sums in another order + a rare activation rounding the other way at a 16-bit tie
     # (one ulp of one activation, ~1e-3 downstream; more such ties at larger latents):
     # the median stays at fp32 noise, the max within a third of the rounding error itself
     bound = 3e-3 if scale <= 0.1 else 6e-3
-    for lay in ("split", "split16"):
+    for lay in ("split",):
         d_lo = (out[lay] - lowp).abs()
         e_lo, m_lo = float(d_lo.max()), float(d_lo.median())
         print(f"{lay} {dtype} z*{scale}: vs lowp max {e_lo:.2e} median {m_lo:.2e}")
         assert m_lo <= 2e-5, (lay, m_lo)
         assert e_lo <= bound, (lay, e_lo)
-    e_x = float((out["split"] - out["split16"]).abs().max())
-    assert e_x <= bound, e_x
+
+
+def test_removed_layouts_fail_loudly(dev, decoder):
+    """pass8 / quarter (ABI 5) and split16 (ABI 7) descriptors get LDM_ENOSYS, not a kernel."""
+    from ldm_sdf import _capi as capi, ops
+    from ldm_sdf import LdmError
+    pk = decoder.device_pack("bf16", dev)
+    beta = ops.decoder_fold(pk["desc"], torch.zeros(1, 256, device=dev))
+    keep = pk["desc"].layout
+    try:
+        for lay in (0, 1, 3):
+            pk["desc"].layout = lay
+            with pytest.raises(LdmError):
+                ops.decoder_grid_fwd(pk["desc"], beta, 8, 0, 8)
+    finally:
+        pk["desc"].layout = keep
+    with pytest.raises(ValueError):
+        decoder.device_pack("bf16", dev, layout="split16")

@@ -113,27 +113,3 @@ def test_split_layout_emulation_matches_lowp_oracle(dtype, sw):
     lowp = R.decoder_forward_lowp(p, z, xyz.double(), dt).numpy()
     d = np.abs(emu - lowp)
     assert np.median(d) < 1e-6 and d.max() < 1e-3, (np.median(d), d.max())
-
-
-@pytest.mark.parametrize("dtype,sw", [("bf16", 253), ("fp16", 512)])
-def test_split16_layout_emulation_matches_lowp_oracle(dtype, sw):
-    """The split16 layout (csrc/decoder_fs16.hip, 16x16x32 MFMAs, fp32 epilogue biases)
-    replayed on the CPU from the packed blob: the 16-bit precision-contract oracle's numbers
-    (its hi + lo biases differ from the exact fp32 bias by < 2^-16 relative), and the stream
-    length the kernel expects (g_nsteps)."""
-    from tests.mfma_emulator import emulate_split16
-    L = 256 if sw == 253 else 1024
-    p = R.make_decoder_params(L=L, widen_skip=(sw == 512), seed=1234)
-    g = torch.Generator().manual_seed(6)
-    z = torch.randn(2, L, generator=g, dtype=torch.float64) * 0.1
-    xyz = (torch.rand(2, 128, 3, generator=g, dtype=torch.float64) * 2 - 1).float()
-    dt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
-    packed = pack.pack_decoder(p.weights, p.biases, L, dtype, layout="split16")
-    assert packed["n_stages"] == (192 if sw == 253 else 224)
-    nbias = 4 * (15 if sw == 253 else 16) * 64
-    assert packed["weights"].numel() == 4 * packed["n_stages"] * 4 * 64 * 8 + 2 * nbias
-    beta = R.latent_fold(p, z).float().numpy()
-    emu = emulate_split16(packed, beta, xyz.numpy(), dtype)
-    lowp = R.decoder_forward_lowp(p, z, xyz.double(), dt).numpy()
-    d = np.abs(emu - lowp)
-    assert np.median(d) < 1e-5 and d.max() < 1e-3, (np.median(d), d.max())
