@@ -261,6 +261,34 @@ int ldm_denoiser_train_step_adamw(const ldm_denoiser_t* w, const ldm_sched_t* sc
                                   double lr, double beta1, double beta2, double eps_adam,
                                   double weight_decay, int step, const float* d_hyper,
                                   ldm_stream_t s, ldm_stream_t side);
+/* The whole step in ONE persistent launch (round 5, ABI 7; csrc/train_dag.hip):
+ * with side == NULL (or == s), ldm_denoiser_train_step_adamw runs the step's job DAG -- input
+ * preparation, every GEMM tile of the launch path with the same epilogues, the bias sums and every
+ * AdamW tile -- in one launch whose workgroups take jobs as their inputs become ready (per 64-row
+ * band for the residual chain, per problem for weight gradients and updates).  Results are those
+ * of the launch path bit for bit.  The first call for a (descriptor, workspace, gradients, AdamW
+ * table, B) configuration builds its job table on the host and uploads it into `saved` (one
+ * stream synchronisation; not inside a graph capture); later calls launch at once.  Waits are
+ * bounded: ldm_denoiser_train_status reads (and clears) the status word of `saved`: 0 ok, 1 a
+ * wait timed out (the step's results are garbage), 3 the table in `saved` was built for other
+ * inputs (nothing computed).  ldm_train_step_config selects the form per device:
+ * LDM_TRAIN_AUTO (default: the DAG whenever the configuration has one), LDM_TRAIN_LAUNCHES (the
+ * launch path), LDM_TRAIN_DAG (required: LDM_ENOSYS otherwise); spin_limit: microseconds one dependency wait
+ * may take before the launch gives up (0 = default, 2 s). */
+#define LDM_TRAIN_AUTO 0
+#define LDM_TRAIN_LAUNCHES 1
+#define LDM_TRAIN_DAG 2
+int ldm_train_step_config(int form, unsigned spin_limit);
+int ldm_train_step_last_form(void);   /* the form the last step on this device ran (0: none) */
+int ldm_denoiser_train_status(const ldm_denoiser_t* w, int B, void* saved, unsigned* status_host,
+                              ldm_stream_t s);
+/* Diagnostics (host only, no device work): the job table of this configuration as text into
+ * buf[len] -- per node its type, jobs, k-steps, counters and dependencies, then the queues.
+ * 1: the configuration has no one-launch form. */
+int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ldm_sched_t* sc, int B,
+                                    void* saved, const ldm_denoiser_grads_t* grads,
+                                    const ldm_adamw_tensor_t* tensors, int n, char* buf,
+                                    size_t len);
 /* d_hyper (may be NULL): a DEVICE array of the 7 AdamW scalars ldm_adamw_hyper computes for
  * (lr, beta1, beta2, eps_adam, weight_decay, step); the kernels read them from there instead
  * of the arguments, so a hipGraph captured once replays every step (the caller refills it).

@@ -1,0 +1,114 @@
+// One 64 x 64 tile of the multi-tensor AdamW update (ldm_adamw_multi, denoiser_train.hip), shared
+// with the persistent training-step kernel (train_dag.hip) so both update every parameter with
+// the same instructions (the update is ldm_adamw_step's, operation for operation: ddpm_common.h
+// adamw_update).  The transposed bf16 copy goes through an LDS tile so its stores are 32-byte
+// row runs.
+#pragma once
+#include "ldm_internal.h"
+#include "ddpm_common.h"
+
+namespace ldm {
+
+// adamw_hyper's 7 scalars: [1 - lr wd, 1 - beta1, beta2, 1 - beta2, eps, lr / bc1, sqrt(bc2)]
+struct AdamHyper {
+    float decay, omb1, b2, omb2, eps, step_size, bc2_sqrt;
+};
+
+// Tile `tl` (row-major over the tensor's 64 x 64 tiles; a 1-D tensor is one row) of tensor T:
+// each thread 4 rows x 4 consecutive columns.  TT: ldm_adamw_tensor_t in any address space.
+template <typename TT>
+__device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
+                                           unsigned short (&sT)[64][64 + 8], int tl) {
+    const int rows = T.rows, cols = T.cols;
+    const int tcn = (cols + 63) / 64;
+    const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
+    const int tid = threadIdx.x;
+    const int cq = (tid & 15) * 4;
+    const float decay = hy.decay, omb1 = hy.omb1, b2 = hy.b2, omb2 = hy.omb2, eps = hy.eps,
+                step_size = hy.step_size, bc2_sqrt = hy.bc2_sqrt;
+    float* __restrict__ P = T.p;
+    const float* __restrict__ Gp = T.g;
+    float* __restrict__ M = T.m;
+    float* __restrict__ V = T.v;
+    // every load of the thread's 4 rows x 4 columns first (16-byte vectors when the row is
+    // aligned and whole), then the updates, then the stores: one memory round trip
+    const bool vec = (cols & 3) == 0 && c0 + cq + 4 <= cols;
+    f32x4 p4[4], g4[4], m4[4], v4[4];
+    int64_t off[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = min(r0 + (tid >> 4) + 16 * i, rows - 1);
+        off[i] = (int64_t)r * cols + c0 + cq;
+        if (vec) {
+            p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
+            g4[i] = *reinterpret_cast<const f32x4*>(Gp + off[i]);
+            m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
+            v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t x = c0 + cq + e < cols ? off[i] + e : off[i];
+                p4[i][e] = P[x]; g4[i][e] = Gp[x]; m4[i][e] = M[x]; v4[i][e] = V[x];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rl = (tid >> 4) + 16 * i;
+        const bool rin = r0 + rl < rows;
+        unsigned short q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float pi = p4[i][e], mi = m4[i][e], vi = v4[i][e];
+            adamw_update(pi, g4[i][e], mi, vi, decay, omb1, b2, omb2, eps, step_size, bc2_sqrt);
+            p4[i][e] = pi; m4[i][e] = mi; v4[i][e] = vi;
+            const unsigned u = __builtin_bit_cast(unsigned, pi);
+            q[e] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+            sT[cq + e][rl] = rin ? q[e] : (unsigned short)0;
+        }
+        if (!rin) continue;
+        if (vec) {
+            *reinterpret_cast<f32x4*>(P + off[i]) = p4[i];
+            *reinterpret_cast<f32x4*>(M + off[i]) = m4[i];
+            *reinterpret_cast<f32x4*>(V + off[i]) = v4[i];
+            if (T.p_bf16) {
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 w = {(unsigned)q[0] | ((unsigned)q[1] << 16),
+                                 (unsigned)q[2] | ((unsigned)q[3] << 16)};
+                *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(T.p_bf16) + off[i]) = w;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (c0 + cq + e >= cols) continue;
+                P[off[i] + e] = p4[i][e]; M[off[i] + e] = m4[i][e]; V[off[i] + e] = v4[i][e];
+                if (T.p_bf16) reinterpret_cast<unsigned short*>(T.p_bf16)[off[i] + e] = q[e];
+            }
+        }
+    }
+    if (!T.p_bf16_t) return;
+    __syncthreads();
+    // transposed: [c][r], 16 consecutive rows per thread (4 threads per column)
+    const int cl = tid >> 2, rb = (tid & 3) * 16;
+    const int c = c0 + cl;
+    if (c >= cols) return;
+    unsigned short* dst = reinterpret_cast<unsigned short*>(T.p_bf16_t) + (int64_t)c * rows;
+    if ((rows & 7) == 0 && r0 + rb + 16 <= rows) {
+        u32x4 w0, w1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            w0[e] = (unsigned)sT[cl][rb + 2 * e] | ((unsigned)sT[cl][rb + 2 * e + 1] << 16);
+            w1[e] = (unsigned)sT[cl][rb + 8 + 2 * e] | ((unsigned)sT[cl][rb + 9 + 2 * e] << 16);
+        }
+        *reinterpret_cast<u32x4*>(dst + r0 + rb) = w0;
+        *reinterpret_cast<u32x4*>(dst + r0 + rb + 8) = w1;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int r = r0 + rb + e;
+            if (r < rows) dst[r] = sT[cl][rb + e];
+        }
+    }
+}
+
+}  // namespace ldm

@@ -18,13 +18,22 @@
 // by the producing epilogue (M_valid = B), so K = Bp weight-gradient products see zeros there.
 #include "ldm_internal.h"
 #include "ddpm_common.h"
+#include "adamw_tile.h"
+#include "train_dag.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
+
+#include <mutex>
+#include <unordered_map>
+#include <vector>
 
 namespace ldm {
 
 int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s);
+int gemm_tile_choice(const ldm_gemm_args_t& a);
+int gemm_tile_kgroup_period(int tile);
 
 namespace {
 
@@ -47,6 +56,8 @@ struct TrainWs {
     bf16_t *go_b, *go_T, *dtemb_b, *dtemb_T, *gt_T, *dh0_b, *dh0_T;
     float *a_t, *h_f[LDM_MAX_BLOCKS], *a_f[LDM_MAX_BLOCKS], *dh[2];
     float *p_bt1, *p_bt2, *p_bin, *p_bblk[LDM_MAX_BLOCKS], *p_bout, *loss_part;
+    dag::Table* dag_table;      // the persistent step's job table (train_dag.h) and sync words
+    unsigned* dag_sync;
     size_t bytes;
 };
 
@@ -83,6 +94,8 @@ TrainWs layout(const ldm_denoiser_t* w, int B, void* base) {
     for (int k = 0; k < L.nb; ++k) L.p_bblk[k] = f32(R * H);
     L.p_bout = f32(R * D);
     L.loss_part = f32(R * (D / 32));
+    L.dag_table = reinterpret_cast<dag::Table*>(take(dag::table_bytes()));
+    L.dag_sync = reinterpret_cast<unsigned*>(take(dag::sync_bytes(dag::kMaxCounters)));
     L.bytes = off;
     return L;
 }
@@ -186,10 +199,18 @@ void seg(ldm_gemm_prob_t& p, const void* A, int64_t lda, const void* B, int64_t 
     ldm_gemm_seg_t& s = p.seg[p.n_seg++];
     s.A = A; s.B = B; s.lda = lda; s.ldb = ldb; s.K = K;
 }
-int launch(std::initializer_list<ldm_gemm_prob_t> ps, hipStream_t s) {
+// With a recorder the launches are not made but recorded, one group per launch (build_dag).
+struct Recorder {
+    std::vector<ldm_gemm_args_t> launches;
+};
+int launch(std::initializer_list<ldm_gemm_prob_t> ps, hipStream_t s, Recorder* rec = nullptr) {
     ldm_gemm_args_t a;
     memset(&a, 0, sizeof(a));
     for (const auto& p : ps) a.prob[a.n_prob++] = p;
+    if (rec) {
+        rec->launches.push_back(a);
+        return 0;
+    }
     return gemm_bf16(a, s);
 }
 
@@ -216,7 +237,7 @@ int check_desc(const ldm_denoiser_t* w, int B, bool bwd) {
 
 // Forward GEMMs; out-projection: LOSS against `eps_target` (fused step) or STORE to eps_out.
 int forward(const ldm_denoiser_t* w, const TrainWs& L, const float* eps_target,
-            float* eps_out, float loss_scale, hipStream_t s) {
+            float* eps_out, float loss_scale, hipStream_t s, Recorder* rec = nullptr) {
     const int Bp = L.Bp, B = L.B, D = L.D, H = L.H, TE = L.TE;
     ldm_gemm_prob_t f1 = prob(Bp, H, B);                         // u = SiLU(Wt1 e + bt1)
     seg(f1, L.e_b, TE, w->w_t1, TE, TE);
@@ -226,12 +247,12 @@ int forward(const ldm_denoiser_t* w, const TrainWs& L, const float* eps_target,
     seg(f3, L.xt_b, D, w->w_in, D, D);
     f3.bias = w->b_in;
     f3.C = L.h_f[0]; f3.ldc = H; f3.Cb = L.h_b[0]; f3.ldcb = H; f3.CbT = L.h_T[0]; f3.ldct = Bp;
-    LDM_TRY(launch({f1, f3}, s));
+    LDM_TRY(launch({f1, f3}, s, rec));
     ldm_gemm_prob_t f2 = prob(Bp, H, B);                         // temb = Wt2 u + bt2
     seg(f2, L.u_b, H, w->w_t2, H, H);
     f2.bias = w->b_t2;
     f2.Cb = L.temb_b; f2.ldcb = H; f2.CbT = L.temb_T; f2.ldct = Bp;
-    LDM_TRY(launch({f2}, s));
+    LDM_TRY(launch({f2}, s, rec));
     const bf16_t* const* Wb = reinterpret_cast<const bf16_t* const*>(w->w_blk);
     for (int k = 0; k < L.nb; ++k) {                              // h <- h + SiLU([h||temb] Wblk^T + b)
         ldm_gemm_prob_t fb = prob(Bp, H, B);
@@ -241,7 +262,7 @@ int forward(const ldm_denoiser_t* w, const TrainWs& L, const float* eps_target,
         fb.R = L.h_f[k]; fb.ldr = H; fb.P = L.a_f[k]; fb.ldp = H;
         if (k + 1 < L.nb) { fb.C = L.h_f[k + 1]; fb.ldc = H; }
         fb.Cb = L.h_b[k + 1]; fb.ldcb = H; fb.CbT = L.h_T[k + 1]; fb.ldct = Bp;
-        LDM_TRY(launch({fb}, s));
+        LDM_TRY(launch({fb}, s, rec));
     }
     if (eps_target) {                                            // eps_hat -> eps-MSE gradient
         ldm_gemm_prob_t fo = prob(Bp, D, B);
@@ -250,12 +271,12 @@ int forward(const ldm_denoiser_t* w, const TrainWs& L, const float* eps_target,
         fo.P_in = eps_target; fo.ldp_in = D;
         fo.Cb = L.go_b; fo.ldcb = D; fo.CbT = L.go_T; fo.ldct = Bp;
         fo.colsum = L.p_bout; fo.loss_part = L.loss_part;
-        LDM_TRY(launch({fo}, s));
+        LDM_TRY(launch({fo}, s, rec));
     } else if (eps_out) {
         ldm_gemm_prob_t fo = prob(Bp, D, B);
         seg(fo, L.h_b[L.nb], H, w->w_out, H, H);
         fo.bias = w->b_out; fo.C = eps_out; fo.ldc = D;
-        LDM_TRY(launch({fo}, s));
+        LDM_TRY(launch({fo}, s, rec));
     }
     return 0;
 }
@@ -271,7 +292,7 @@ struct StepHook {
     void* ctx;
 };
 int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads_t* gr,
-             float* dx, hipStream_t s, const StepHook* hook = nullptr) {
+             float* dx, hipStream_t s, const StepHook* hook = nullptr, Recorder* rec = nullptr) {
     const int Bp = L.Bp, B = L.B, D = L.D, H = L.H, TE = L.TE, nb = L.nb;
     const bf16_t* const* Wt = reinterpret_cast<const bf16_t* const*>(w->wt_blk);
     {
@@ -284,7 +305,7 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
         dh.C = L.dh[0]; dh.ldc = H;
         dh.Cb = L.g_b[nb - 1]; dh.ldcb = H; dh.CbT = L.g_T[nb - 1]; dh.ldct = Bp;
         dh.colsum = L.p_bblk[nb - 1];
-        LDM_TRY(launch({dwo, dh}, s));
+        LDM_TRY(launch({dwo, dh}, s, rec));
     }
     int cur = 0;
     for (int k = nb - 1; k >= 0; --k) {
@@ -307,7 +328,7 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
             dh.Cb = L.dh0_b; dh.ldcb = H; dh.CbT = L.dh0_T; dh.ldct = Bp;
             dh.colsum = L.p_bin;
         }
-        LDM_TRY(launch({dw, du, dh}, s));
+        LDM_TRY(launch({dw, du, dh}, s, rec));
         cur ^= 1;
     }
     {
@@ -317,7 +338,7 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
         dt.colsum = L.p_bt2;
         // alone in its launch: 256 tiles, every K a multiple of 128 -> the 128-deep 2-group
         // tile (with dWin's 64 tiles beside it the launch fell to 64 x 64 tiles: 30.8 us)
-        LDM_TRY(launch({dt}, s));
+        LDM_TRY(launch({dt}, s, rec));
         if (hook) LDM_TRY(hook->fn(hook->ctx, 0, s));
     }
     {
@@ -328,7 +349,7 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
         seg(gt, L.dtemb_b, H, w->wt_t2, H, H);
         gt.mode = LDM_GEMM_DGRAD_SILU; gt.P_in = L.a_t; gt.ldp_in = H;
         gt.CbT = L.gt_T; gt.ldct = Bp; gt.colsum = L.p_bt1;
-        LDM_TRY(launch({dw2, gt}, s));
+        LDM_TRY(launch({dw2, gt}, s, rec));
     }
     {
         ldm_gemm_prob_t dw1 = prob(H, TE, H);                    // dWt1 = gt^T e
@@ -343,9 +364,9 @@ int backward(const ldm_denoiser_t* w, const TrainWs& L, const ldm_denoiser_grads
             ldm_gemm_prob_t px = prob(B, D, B);                  // dx = dh0 Win
             seg(px, L.dh0_b, H, w->wt_in, H, H);
             px.C = dx; px.ldc = D;
-            LDM_TRY(launch({dw1, dwi, px}, s));
+            LDM_TRY(launch({dw1, dwi, px}, s, rec));
         } else {
-            LDM_TRY(launch({dw1, dwi}, s));
+            LDM_TRY(launch({dw1, dwi}, s, rec));
         }
     }
     if (hook) LDM_TRY(hook->fn(hook->ctx, 1, s));
@@ -489,8 +510,6 @@ struct AdamJobs {
 };
 
 typedef const __attribute__((address_space(4))) AdamJobs KJobs;
-template <typename KJ>
-__device__ __forceinline__ void adamw_tile(KJ* kj, unsigned short (&sT)[64][64 + 8], int tile);
 
 __global__ __launch_bounds__(256) void adamw_multi_kernel(AdamJobs jobs) {
     typedef KJobs KJ;
@@ -500,108 +519,15 @@ __global__ __launch_bounds__(256) void adamw_multi_kernel(AdamJobs jobs) {
     // another stream (ldm_denoiser_train_step_adamw); uncapped, one tile per workgroup
     for (int tile = blockIdx.x; tile < kj->first[kj->n]; tile += gridDim.x) {
         __syncthreads();                   // the previous tile's transposed reads of sT are done
-        adamw_tile(kj, sT, tile);
-    }
-}
-
-template <typename KJ>
-__device__ __forceinline__ void adamw_tile(KJ* kj, unsigned short (&sT)[64][64 + 8], int tile) {
-    int j = 0;
-    for (int i = 1; i < kj->n; ++i)
-        if (tile >= kj->first[i]) j = i;
-    const __attribute__((address_space(4))) ldm_adamw_tensor_t& T = kj->t[j];
-    const int rows = T.rows, cols = T.cols;
-    const int tl = tile - kj->first[j], tcn = (cols + 63) / 64;
-    const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
-    const int tid = threadIdx.x;
-    const int cq = (tid & 15) * 4;
-    const float* dh = kj->dh;
-    const float decay = dh ? dh[0] : kj->decay, omb1 = dh ? dh[1] : kj->omb1;
-    const float b2 = dh ? dh[2] : kj->b2, omb2 = dh ? dh[3] : kj->omb2;
-    const float eps = dh ? dh[4] : kj->eps, step_size = dh ? dh[5] : kj->step_size;
-    const float bc2_sqrt = dh ? dh[6] : kj->bc2_sqrt;
-    float* __restrict__ P = T.p;
-    const float* __restrict__ Gp = T.g;
-    float* __restrict__ M = T.m;
-    float* __restrict__ V = T.v;
-    // every load of the thread's 4 rows x 4 columns first (16-byte vectors when the row is
-    // aligned and whole), then the updates, then the stores: one memory round trip
-    const bool vec = (cols & 3) == 0 && c0 + cq + 4 <= cols;
-    f32x4 p4[4], g4[4], m4[4], v4[4];
-    int64_t off[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = min(r0 + (tid >> 4) + 16 * i, rows - 1);
-        off[i] = (int64_t)r * cols + c0 + cq;
-        if (vec) {
-            p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
-            g4[i] = *reinterpret_cast<const f32x4*>(Gp + off[i]);
-            m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
-            v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t x = c0 + cq + e < cols ? off[i] + e : off[i];
-                p4[i][e] = P[x]; g4[i][e] = Gp[x]; m4[i][e] = M[x]; v4[i][e] = V[x];
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int rl = (tid >> 4) + 16 * i;
-        const bool rin = r0 + rl < rows;
-        unsigned short q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            float pi = p4[i][e], mi = m4[i][e], vi = v4[i][e];
-            adamw_update(pi, g4[i][e], mi, vi, decay, omb1, b2, omb2, eps, step_size, bc2_sqrt);
-            p4[i][e] = pi; m4[i][e] = mi; v4[i][e] = vi;
-            const unsigned u = __builtin_bit_cast(unsigned, pi);
-            q[e] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-            sT[cq + e][rl] = rin ? q[e] : (unsigned short)0;
-        }
-        if (!rin) continue;
-        if (vec) {
-            *reinterpret_cast<f32x4*>(P + off[i]) = p4[i];
-            *reinterpret_cast<f32x4*>(M + off[i]) = m4[i];
-            *reinterpret_cast<f32x4*>(V + off[i]) = v4[i];
-            if (T.p_bf16) {
-                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                const u32x2 w = {(unsigned)q[0] | ((unsigned)q[1] << 16),
-                                 (unsigned)q[2] | ((unsigned)q[3] << 16)};
-                *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(T.p_bf16) + off[i]) = w;
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (c0 + cq + e >= cols) continue;
-                P[off[i] + e] = p4[i][e]; M[off[i] + e] = m4[i][e]; V[off[i] + e] = v4[i][e];
-                if (T.p_bf16) reinterpret_cast<unsigned short*>(T.p_bf16)[off[i] + e] = q[e];
-            }
-        }
-    }
-    if (!T.p_bf16_t) return;
-    __syncthreads();
-    // transposed: [c][r], 16 consecutive rows per thread (4 threads per column)
-    const int cl = tid >> 2, rb = (tid & 3) * 16;
-    const int c = c0 + cl;
-    if (c >= cols) return;
-    unsigned short* dst = reinterpret_cast<unsigned short*>(T.p_bf16_t) + (int64_t)c * rows;
-    if ((rows & 7) == 0 && r0 + rb + 16 <= rows) {
-        u32x4 w0, w1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            w0[e] = (unsigned)sT[cl][rb + 2 * e] | ((unsigned)sT[cl][rb + 2 * e + 1] << 16);
-            w1[e] = (unsigned)sT[cl][rb + 8 + 2 * e] | ((unsigned)sT[cl][rb + 9 + 2 * e] << 16);
-        }
-        *reinterpret_cast<u32x4*>(dst + r0 + rb) = w0;
-        *reinterpret_cast<u32x4*>(dst + r0 + rb + 8) = w1;
-    } else {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int r = r0 + rb + e;
-            if (r < rows) dst[r] = sT[cl][rb + e];
-        }
+        int j = 0;
+        for (int i = 1; i < kj->n; ++i)
+            if (tile >= kj->first[i]) j = i;
+        const float* dh = kj->dh;
+        const AdamHyper hy = {dh ? dh[0] : kj->decay, dh ? dh[1] : kj->omb1,
+                              dh ? dh[2] : kj->b2,    dh ? dh[3] : kj->omb2,
+                              dh ? dh[4] : kj->eps,   dh ? dh[5] : kj->step_size,
+                              dh ? dh[6] : kj->bc2_sqrt};
+        adamw_tile(kj->t[j], hy, sT, tile - kj->first[j]);
     }
 }
 }  // namespace
@@ -709,6 +635,348 @@ int adam_hook(void* ctx, int point, hipStream_t s) {
 }  // namespace
 }  // namespace ldm
 
+// ---- the persistent step (train_dag.hip) ----------------------------------------------------
+// The DAG is derived from the launch path itself: forward() / backward() run with a Recorder,
+// so the GEMM problems (operands, epilogues, layouts) are the launch path's, and each keeps the
+// k-group split of the tile its launch would run (gemm_tile_choice): bit-identical results.
+namespace ldm {
+namespace {
+
+struct TrainCfg {
+    int form = LDM_TRAIN_AUTO;
+    unsigned spin = 0;
+    int last = 0;
+    unsigned dbg = 0;           // ldm_dev_train_dag_flags (diagnostics only)
+};
+TrainCfg& train_cfg() {
+    static TrainCfg cfg[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    return cfg[dev];
+}
+
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const unsigned char* c = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= c[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+// the LDS-transposed epilogue's vector conditions (gemm_bf16.hip epi(): `ok`), for every block
+bool lds_epilogue_ok(const ldm_gemm_prob_t& P) {
+    auto al = [](const void* p, int a) { return ((uintptr_t)p & (uintptr_t)(a - 1)) == 0; };
+    return P.N % 64 == 0 && P.k_split <= 1 && (!P.C || (al(P.C, 16) && P.ldc % 4 == 0)) &&
+           (!P.P || (al(P.P, 16) && P.ldp % 4 == 0)) &&
+           (P.mode == LDM_GEMM_ACCUM || !P.R || (al(P.R, 16) && P.ldr % 4 == 0)) &&
+           (!P.P_in || (al(P.P_in, 16) && P.ldp_in % 4 == 0)) &&
+           (!P.Cb || (al(P.Cb, 8) && P.ldcb % 4 == 0)) &&
+           (!P.Rb || (al(P.Rb, 8) && P.ldrb % 4 == 0)) && (!P.bias || al(P.bias, 16));
+}
+
+struct DagHost {
+    uint64_t hash = 0;
+    dag::Table tab;
+    std::vector<uint32_t> entries;
+};
+
+// Builds the job table of one step; returns 1 (and builds nothing) when this configuration has
+// no DAG form -- the caller then runs the launch path.
+int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
+              const ldm_denoiser_grads_t* gr, const ldm_adamw_tensor_t* tensors, int n,
+              float nf, int grid, DagHost& H) {
+    using namespace dag;
+    const int nb = L.nb;
+    Recorder rec;
+    const float* kEps = reinterpret_cast<const float*>((uintptr_t)256);   // eps: a launch arg
+    LDM_TRY(forward(w, L, kEps, nullptr, 2.f / nf, nullptr, &rec));
+    LDM_TRY(backward(w, L, gr, nullptr, nullptr, nullptr, &rec));
+    if ((int)rec.launches.size() != 2 * nb + 7) return 1;
+    Table& T = H.tab;
+    memset(&T, 0, sizeof(T));
+    int nctr = 0;
+    bool ok = true;
+    auto add = [&](Node nd) -> int {
+        if (T.n_nodes >= kMaxNodes) {          // (~50 nodes at 4 blocks; 8 blocks fit too)
+            ok = false;
+            return kMaxNodes - 1;
+        }
+        nd.out_band = -1;
+        if (nd.type == N_GEMM || nd.type == N_PREP) {
+            nd.out_band = nctr;
+            nctr += nd.tiles_m;
+        }
+        nd.out_all = nctr++;
+        T.node[T.n_nodes] = nd;
+        return T.n_nodes++;
+    };
+    auto dep = [&](int c, int p, bool band) {
+        Node& C = T.node[c];
+        const Node& Pn = T.node[p];
+        C.dep_ctr[C.ndep] = band ? Pn.out_band : Pn.out_all;
+        C.dep_band[C.ndep] = band ? 1 : 0;
+        C.dep_target[C.ndep] = band ? (unsigned)Pn.tiles_n : (unsigned)(Pn.tiles_m * Pn.tiles_n);
+        ++C.ndep;
+    };
+    auto gemm = [&](int li, int pi) -> int {
+        const ldm_gemm_args_t& a = rec.launches[li];
+        const ldm_gemm_prob_t& P = a.prob[pi];
+        Node nd;
+        memset(&nd, 0, sizeof(nd));
+        nd.type = N_GEMM;
+        nd.P = P;
+        nd.tiles_m = (P.M + 63) / 64;
+        nd.tiles_n = P.N / 64;
+        for (int g = 0; g < P.n_seg; ++g) nd.nk += P.seg[g].K / 64;
+        nd.kgp = gemm_tile_kgroup_period(gemm_tile_choice(a));
+        nd.adam = -1;
+        if (P.P_in == kEps) {
+            nd.pin_eps = 1;
+            nd.P.P_in = nullptr;
+        }
+        ok = ok && lds_epilogue_ok(nd.P) && P.ct_blk == 0 && nd.tiles_m * nd.tiles_n <= 65535;
+        return add(nd);
+    };
+    // tensor of each gradient (AdamW), -1 if not in the table
+    auto tens = [&](const float* g) {
+        for (int i = 0; i < n; ++i)
+            if (tensors[i].g == g) return i;
+        return -1;
+    };
+    std::vector<bool> used(n, false);
+    auto sum = [&](const float* src, float* dst, int rows, int len, int ld, float scale,
+                   const float* g) -> int {
+        Node nd;
+        memset(&nd, 0, sizeof(nd));
+        nd.type = N_SUM;
+        nd.tiles_m = nd.tiles_n = 1;
+        nd.src = src; nd.dst = dst; nd.rows = rows; nd.len = len; nd.ld = ld; nd.scale = scale;
+        nd.adam = g ? tens(g) : -1;
+        if (nd.adam >= 0) {
+            const ldm_adamw_tensor_t& t = tensors[nd.adam];
+            ok = ok && !t.p_bf16 && !t.p_bf16_t && (int64_t)t.rows * t.cols == len;
+            used[nd.adam] = true;
+        }
+        return add(nd);
+    };
+    auto adam = [&](const float* g, int col_off, int col_tiles) -> int {
+        const int ti = tens(g);
+        if (ti < 0) return -1;
+        const ldm_adamw_tensor_t& t = tensors[ti];
+        Node nd;
+        memset(&nd, 0, sizeof(nd));
+        nd.type = N_ADAM;
+        nd.adam = ti;
+        nd.col_off = col_off;
+        nd.tiles_m = (t.rows + 63) / 64;
+        nd.tiles_n = col_tiles ? col_tiles : (t.cols + 63) / 64;
+        used[ti] = true;
+        return add(nd);
+    };
+    // ---- nodes in priority order (topological: every dependency is an earlier node) --------
+    const int base = nb + 3, H_ = L.H;
+    Node pr;
+    memset(&pr, 0, sizeof(pr));
+    pr.type = N_PREP;
+    pr.tiles_m = L.Bp / 64;
+    pr.tiles_n = 1;
+    pr.adam = -1;
+    pr.sab = sc->sqrt_ab; pr.s1mab = sc->sqrt_1mab; pr.emb = w->emb_table;
+    pr.B = L.B; pr.Bp = L.Bp; pr.D = L.D; pr.TE = L.TE;
+    pr.xt_b = L.xt_b; pr.xt_T = L.xt_T; pr.e_b = L.e_b; pr.e_T = L.e_T;
+    const int prep = add(pr);
+    const int f1 = gemm(0, 0), f3 = gemm(0, 1);
+    dep(f1, prep, true);
+    dep(f3, prep, true);
+    const int f2 = gemm(1, 0);
+    dep(f2, f1, true);
+    std::vector<int> fb(nb);
+    for (int k = 0; k < nb; ++k) {
+        fb[k] = gemm(2 + k, 0);
+        dep(fb[k], k == 0 ? f3 : fb[k - 1], true);
+        dep(fb[k], f2, true);
+    }
+    const int fo = gemm(2 + nb, 0);
+    dep(fo, fb[nb - 1], true);
+    const int dhout = gemm(base, 1);
+    dep(dhout, fo, true);
+    dep(sum(L.p_bout, gr->b_out, L.Bp / 32, L.D, L.D, 1.f, gr->b_out), fo, false);
+    dep(sum(L.loss_part, nullptr, (L.Bp / 32) * (L.D / 32), 1, 1, 1.f / nf, nullptr), fo,
+        false);
+    const int dwo = gemm(base, 0);
+    dep(dwo, fo, false);
+    std::vector<int> Dk(nb), dwk(nb), duk(nb);
+    std::vector<bool> wdone(nb, false);
+    bool wout_done = false;
+    auto adam_w = [&](int k) {            // W_k's update: its gradient and dh_k (reads W_k^T)
+        const int a = adam(gr->w_blk[k], 0, H_ / 64);
+        if (a >= 0) {
+            dep(a, dwk[k], false);
+            dep(a, Dk[k], false);
+        }
+        wdone[k] = true;
+    };
+    auto adam_wout = [&]() {
+        const int a = adam(gr->w_out, 0, 0);
+        if (a >= 0) {
+            dep(a, dwo, false);
+            dep(a, dhout, false);
+        }
+        wout_done = true;
+    };
+    for (int i = 0; i < nb; ++i) {
+        const int k = nb - 1 - i;
+        const int gprod = k == nb - 1 ? dhout : Dk[k + 1];      // produced g_k and p_bblk[k]
+        Dk[k] = gemm(base + 1 + i, 2);
+        dep(Dk[k], gprod, true);
+        dwk[k] = gemm(base + 1 + i, 0);
+        dep(dwk[k], gprod, false);
+        duk[k] = gemm(base + 1 + i, 1);
+        dep(duk[k], gprod, false);
+        dep(sum(L.p_bblk[k], gr->b_blk[k], L.Bp / 32, H_, H_, 1.f, gr->b_blk[k]), gprod, false);
+        if (k + 1 < nb) adam_w(k + 1);
+        if (k == nb - 2) adam_wout();
+    }
+    if (!wout_done) adam_wout();
+    dep(sum(L.p_bin, gr->b_in, L.Bp / 32, H_, H_, 1.f, gr->b_in), Dk[0], false);
+    const int dt = gemm(base + 1 + nb, 0);
+    dep(dt, nb >= 2 ? Dk[1] : dhout, true);      // the producer of g_0 (the chain covers g_k>0)
+    adam_w(0);
+    const int gt = gemm(base + 2 + nb, 1);
+    dep(gt, dt, true);
+    const int dwi = gemm(base + 3 + nb, 1);
+    dep(dwi, Dk[0], false);
+    const int dw2 = gemm(base + 2 + nb, 0);
+    dep(dw2, dt, false);
+    dep(sum(L.p_bt2, gr->b_t2, L.Bp / 32, H_, H_, 1.f, gr->b_t2), dt, false);
+    for (int k = nb - 1; k >= 0; --k) {      // U_k's update: its gradient and dtemb (reads U_k^T)
+        const int a = adam(gr->w_blk[k], H_ / 64, H_ / 64);
+        if (a >= 0) {
+            dep(a, duk[k], false);
+            dep(a, dt, false);
+        }
+    }
+    const int dw1 = gemm(base + 3 + nb, 0);
+    dep(dw1, gt, false);
+    dep(sum(L.p_bt1, gr->b_t1, L.Bp / 32, H_, H_, 1.f, gr->b_t1), gt, false);
+    int a = adam(gr->w_in, 0, 0);
+    if (a >= 0) dep(a, dwi, false);
+    a = adam(gr->w_t2, 0, 0);
+    if (a >= 0) {
+        dep(a, dw2, false);
+        dep(a, gt, false);
+    }
+    a = adam(gr->w_t1, 0, 0);
+    if (a >= 0) dep(a, dw1, false);
+    for (int i = 0; i < n; ++i) ok = ok && used[i];         // every tensor is one of ours
+    for (int i = 0; i < n; ++i) T.tensor[i] = tensors[i];
+    if (!ok || nctr > kMaxCounters) return 1;
+    // every dependency points at an earlier node (the deadlock-freedom argument)
+    for (int c = 0; c < T.n_nodes; ++c)
+        for (int d = 0; d < T.node[c].ndep; ++d)
+            LDM_REQUIRE(T.node[c].dep_ctr[d] < T.node[c].out_band ||
+                            T.node[c].dep_ctr[d] < T.node[c].out_all,
+                        LDM_EINVAL, "train dag: node %d depends on a later node", c);
+    // ---- jobs -> queues: row bands of the batch stay on one queue (2 of the 16 bands each),
+    // other nodes in contiguous chunks, single jobs round-robin
+    std::vector<uint32_t> q[kQueues];
+    int rr = 0;
+    for (int i = 0; i < T.n_nodes; ++i) {
+        const Node& nd = T.node[i];
+        const int jobs = nd.tiles_m * nd.tiles_n;
+        const bool rows = nd.type == N_PREP || (nd.type == N_GEMM && nd.P.M == L.Bp);
+        for (int j = 0; j < jobs; ++j) {
+            int qq;
+            if (jobs == 1) qq = rr++ % kQueues;
+            else if (rows) qq = (j / nd.tiles_n) * kQueues / nd.tiles_m;
+            else qq = (int)((int64_t)j * kQueues / jobs);
+            q[qq].push_back((uint32_t)i << 16 | (uint32_t)j);
+        }
+    }
+    H.entries.clear();
+    for (int qq = 0; qq < kQueues; ++qq) {
+        T.qoff[qq] = (int)H.entries.size();
+        T.qlen[qq] = (int)q[qq].size();
+        H.entries.insert(H.entries.end(), q[qq].begin(), q[qq].end());
+    }
+    if ((int)H.entries.size() > kMaxEntries) return 1;
+    T.n_counters = nctr;
+    T.n_entries = (int)H.entries.size();
+    T.n_tensors = n;
+    T.grid = grid;
+    return 0;
+}
+
+// The step as one launch.  Returns 1 when the configuration has no DAG form (nothing done).
+int dag_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, const float* eps,
+             const int32_t* t, int B, void* saved, const ldm_denoiser_grads_t* grads,
+             float* loss_out, const ldm_adamw_tensor_t* tensors, int n, const float* hy7,
+             const float* d_hyper, unsigned spin, unsigned dbg, hipStream_t s) {
+    const TrainWs L = layout(w, B, saved);
+    int grid = 0;
+    LDM_TRY(dag::dag_grid(&grid));
+    // the table depends on every pointer and size it names: hash them (the kernel refuses a
+    // table built for other inputs: status 3)
+    uint64_t h = 1469598103934665603ull;
+    h = fnv(h, w, sizeof(*w));
+    h = fnv(h, sc, sizeof(*sc));
+    h = fnv(h, grads, sizeof(*grads));
+    h = fnv(h, tensors, sizeof(*tensors) * (size_t)n);
+    h = fnv(h, &B, sizeof(B));
+    h = fnv(h, &grid, sizeof(grid));
+    h = fnv(h, &L.dag_table, sizeof(L.dag_table));
+    const size_t tb = sizeof(dag::Table);
+    h = fnv(h, &tb, sizeof(tb));
+    static std::mutex mu;
+    static std::unordered_map<const void*, DagHost*> cache;      // by device table address
+    DagHost* hc = nullptr;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        DagHost*& slot = cache[L.dag_table];
+        if (!slot) slot = new DagHost();       // kept for the process: the async upload reads it
+        hc = slot;
+    }
+    if (hc->hash != h) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        LDM_REQUIRE(hipStreamIsCapturing(s, &cs) == hipSuccess &&
+                        cs == hipStreamCaptureStatusNone,
+                    LDM_EINVAL, "ldm_denoiser_train_step_adamw (dag): the first step of a "
+                    "configuration uploads its job table; run it once before graph capture");
+        const int r = build_dag(w, sc, L, grads, tensors, n, (float)B * (float)w->D, grid, *hc);
+        if (r != 0) {
+            hc->hash = 0;
+            return r;
+        }
+        hc->tab.hash = h;
+        hipError_t e = hipMemcpyAsync(L.dag_table, &hc->tab, sizeof(dag::Table),
+                                      hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(L.dag_table + 1, hc->entries.data(),
+                               hc->entries.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(L.dag_sync, 0, dag::sync_bytes(dag::kMaxCounters), s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);      // once per configuration
+        LDM_REQUIRE(e == hipSuccess, (int)e, "train dag: table upload: %s",
+                    hipGetErrorString(e));
+        hc->hash = h;
+    }
+    dag::LaunchArgs a;
+    memset(&a, 0, sizeof(a));
+    a.tab = L.dag_table;
+    a.sync = L.dag_sync;
+    a.hash = h;
+    a.x0 = x0; a.eps = eps; a.t = t; a.loss_out = loss_out;
+    a.d_hyper = d_hyper;
+    for (int i = 0; i < 7; ++i) a.hy[i] = hy7[i];
+    a.spin_limit = spin ? spin : 2000000u;        // microseconds a wait may take: 2 s
+    a.dbg = dbg;
+    return dag::dag_launch(a, grid, s);
+}
+
+}  // namespace
+}  // namespace ldm
+
 extern "C" int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double lr,
                                double beta1, double beta2, double eps, double weight_decay,
                                int step, ldm_stream_t s) {
@@ -735,6 +1003,26 @@ extern "C" int ldm_denoiser_train_step_adamw(
     LDM_REQUIRE(tensors && n >= 1 && n <= LDM_ADAMW_MAX_TENSORS && step >= 1, LDM_EINVAL,
                 "ldm_denoiser_train_step_adamw: 1..%d tensors, step >= 1",
                 LDM_ADAMW_MAX_TENSORS);
+    // the persistent step (one launch, train_dag.hip) unless configured off, a side stream was
+    // asked for, or this configuration has no DAG form (then the launches below)
+    TrainCfg& cfg = train_cfg();
+    LDM_REQUIRE(cfg.form != LDM_TRAIN_DAG || side == nullptr || side == s, LDM_ENOSYS,
+                "ldm_denoiser_train_step_adamw: the one-launch step (LDM_TRAIN_DAG, required) "
+                "has no side-stream form");
+    if ((side == nullptr || side == s) && cfg.form != LDM_TRAIN_LAUNCHES) {
+        float h7[7];
+        adamw_hyper(lr, beta1, beta2, eps_adam, weight_decay, step, h7);
+        const int r = dag_step(w, sc, x0, eps, t, B, saved, grads, loss_out, tensors, n, h7,
+                               d_hyper, cfg.spin, cfg.dbg, (hipStream_t)s);
+        if (r == 0) {
+            cfg.last = LDM_TRAIN_DAG;
+            return 0;
+        }
+        if (r != 1) return r;
+        LDM_REQUIRE(cfg.form != LDM_TRAIN_DAG, LDM_ENOSYS, "ldm_denoiser_train_step_adamw: no "
+                    "one-launch form for this configuration (LDM_TRAIN_DAG was required)");
+    }
+    cfg.last = LDM_TRAIN_LAUNCHES;
     AdamSplit A;
     memset(&A, 0, sizeof(A));
     A.lr = lr; A.beta1 = beta1; A.beta2 = beta2; A.eps = eps_adam; A.wd = weight_decay;
@@ -779,4 +1067,82 @@ extern "C" int ldm_denoiser_train_step_adamw(
 extern "C" void ldm_adamw_hyper(double lr, double beta1, double beta2, double eps,
                                 double weight_decay, int step, float* out7) {
     ldm::adamw_hyper(lr, beta1, beta2, eps, weight_decay, step, out7);
+}
+
+extern "C" int ldm_train_step_config(int form, unsigned spin_limit) {
+    LDM_REQUIRE(form >= LDM_TRAIN_AUTO && form <= LDM_TRAIN_DAG, LDM_EINVAL,
+                "ldm_train_step_config: form %d", form);
+    TrainCfg& c = train_cfg();
+    c.form = form;
+    c.spin = spin_limit;
+    return 0;
+}
+
+extern "C" int ldm_train_step_last_form(void) { return train_cfg().last; }
+
+extern "C" int ldm_denoiser_train_status(const ldm_denoiser_t* w, int B, void* saved,
+                                         unsigned* status_host, ldm_stream_t s) {
+    LDM_REQUIRE(w && B >= 1 && saved && status_host && w->n_blocks >= 1 &&
+                    w->n_blocks <= LDM_MAX_BLOCKS,
+                LDM_EINVAL, "ldm_denoiser_train_status: bad arguments");
+    const TrainWs L = layout(w, B, saved);
+    unsigned* st = L.dag_sync + dag::kSyncStatus * dag::kCtrStride;
+    hipStream_t hs = (hipStream_t)s;
+    hipError_t e = hipMemcpyAsync(status_host, st, sizeof(unsigned), hipMemcpyDeviceToHost, hs);
+    if (e == hipSuccess) e = hipStreamSynchronize(hs);
+    if (e == hipSuccess && *status_host != 0)       // every word cleared for the next launch
+        e = hipMemsetAsync(L.dag_sync, 0, dag::sync_bytes(dag::kMaxCounters), hs);
+    if (e == hipSuccess) e = hipStreamSynchronize(hs);
+    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_denoiser_train_status: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// Diagnostics: the job table a step of this configuration runs, as text (one line per node:
+// type, jobs, k-steps, k-group period, counters, dependencies; then the queue lengths), built
+// on the host exactly as the step builds it.  Returns 1 if the configuration has no DAG form.
+extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ldm_sched_t* sc,
+                                               int B, void* saved,
+                                               const ldm_denoiser_grads_t* grads,
+                                               const ldm_adamw_tensor_t* tensors, int n,
+                                               char* buf, size_t len) {
+    LDM_TRY(check_desc(w, B, true));
+    LDM_TRY(check_grads(w, grads));
+    LDM_REQUIRE(sc && saved && buf && len > 0 && tensors && n >= 1 &&
+                    n <= LDM_ADAMW_MAX_TENSORS, LDM_EINVAL,
+                "ldm_denoiser_train_dag_describe: bad arguments");
+    const TrainWs L = layout(w, B, saved);
+    int grid = 0;
+    if (dag::dag_grid(&grid) != 0) grid = -1;        // (no device: the table alone)
+    DagHost* h = new DagHost();
+    const int r = build_dag(w, sc, L, grads, tensors, n, (float)B * (float)w->D, grid, *h);
+    if (r != 0) {
+        delete h;
+        return r;
+    }
+    const dag::Table& T = h->tab;
+    static const char* kType[] = {"gemm", "prep", "sum", "adam"};
+    size_t o = 0;
+    auto put = [&](const char* fmt, auto... v) {
+        if (o < len) o += (size_t)snprintf(buf + o, len - o, fmt, v...);
+    };
+    put("grid %d nodes %d counters %d entries %d\n", T.grid, T.n_nodes, T.n_counters,
+        T.n_entries);
+    for (int i = 0; i < T.n_nodes; ++i) {
+        const dag::Node& nd = T.node[i];
+        put("%d %s %dx%d nk %d kgp %d band %d all %d deps", i, kType[nd.type], nd.tiles_m,
+            nd.tiles_n, nd.nk, nd.kgp, nd.out_band, nd.out_all);
+        for (int d = 0; d < nd.ndep; ++d)
+            put(" [%d%s>=%u]", nd.dep_ctr[d], nd.dep_band[d] ? "+band" : "", nd.dep_target[d]);
+        put("\n");
+    }
+    for (int q = 0; q < dag::kQueues; ++q) put("queue %d: %d jobs at %d\n", q, T.qlen[q], T.qoff[q]);
+    delete h;
+    return 0;
+}
+
+// Diagnostics only (not in include/ldm_sdf.h): skip the compute of DAG node types (bit t: type t
+// of train_dag.h NodeType; the jobs still wait and signal) and / or the fences (bit 4).
+extern "C" int ldm_dev_train_dag_flags(unsigned flags) {
+    train_cfg().dbg = flags;
+    return 0;
 }

@@ -27,6 +27,7 @@
 
 #include <mutex>
 #include "ddpm_common.h"
+#include "gemm_tile.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -35,87 +36,7 @@
 
 namespace ldm {
 namespace {
-
-constexpr int kBK = 64;                 // k per ring stage (128 B per operand row)
-
-// A wave-uniform value made opaque in an SGPR (v_readfirstlane): the compiler can neither
-// re-materialise it as a kernarg load nor move it to a VGPR.
-template <typename T>
-__device__ __forceinline__ T pin_s(T v) {
-    if constexpr (sizeof(T) == 4) {
-        return __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
-    } else {
-        static_assert(sizeof(T) == 8, "pin_s: 4- or 8-byte values");
-        const uint64_t u = __builtin_bit_cast(uint64_t, v);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
-        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
-    }
-}
-
-__device__ __forceinline__ unsigned pack2_bf16(float a, float b) {
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const f32x2 v = {a, b};
-    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
-}
-
-// Per-lane source pointers of one operand tile (ROWS x KB k): piece i (1 KiB) = tile rows
-// RP*i .. RP*i+RP-1 (RP = 1024 / (2 KB): 8 rows of 128 B at KB = 64, 4 rows of 256 B at
-// KB = 128); the NW waves of the workgroup issue pieces w, w + NW, ...  Lane L: row
-// RP*i + L/(KB/8), LDS chunk L%(KB/8) <- global chunk (L%(KB/8)) ^ swz(row).  Rows past the end
-// are clamped (valid bytes, never stored).
-// swz: KB = 64 -> (row >> 1) & 7 (two 128-B rows span the 64 banks); KB = 128 -> row & 15.
-// Either way the 16 rows one ds_read_b128 lane group reads hit 16 distinct 16-B bank quads.
-template <int KB>
-__device__ __forceinline__ int swz(int row) {
-    return KB == 64 ? (row >> 1) & 7 : row & 15;
-}
-template <int ROWS, int NW, int KB>
-struct TileSrc {
-    static constexpr int CPR = KB / 8;                   // 16-B chunks per row
-    static constexpr int RP = 64 / CPR;                  // rows per 1 KiB piece
-    static constexpr int NP = ROWS / (RP * NW);          // pieces per wave
-    static_assert(NP >= 1 && ROWS % (RP * NW) == 0, "tile rows vs issuing waves");
-    // Scalar base + 32-bit per-lane byte offsets: the DMA issues in the saddr form (one SGPR
-    // pair, no 64-bit vector address math per piece), and the k step is a scalar add.
-    const char* base;                                    // wave-uniform
-    uint32_t voff[NP];
-    __device__ __forceinline__ void init(const unsigned short* src, int64_t ld, int row0,
-                                         int nrows, int wave, int lane) {
-        const int rl = lane / CPR, cc = lane % CPR;
-        base = reinterpret_cast<const char*>(src);
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            const int rr = RP * (wave + NW * j) + rl;
-            const int row = min(row0 + rr, nrows - 1);
-            voff[j] = (uint32_t)(((int64_t)row * ld + 8 * (cc ^ swz<KB>(rr))) * 2);
-        }
-    }
-    // issue the next KB-deep stage into LDS `dst` and step on; `again`: re-issue the previous
-    // stage instead (a dummy that keeps every wave's vmcnt arithmetic uniform)
-    __device__ __forceinline__ void issue(unsigned short* dst, int wave, bool again) {
-        const char* b = again ? base - 2 * KB : base;
-#pragma unroll
-        for (int j = 0; j < NP; ++j)
-            __builtin_amdgcn_global_load_lds(
-                (const void*)(b + voff[j]),
-                (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 512), 16, 0, 0);
-        if (!again) base += 2 * KB;
-    }
-    // register staging (RS kernels): the same pieces through VGPRs, written to the same
-    // lane-linear LDS image by ds_write_b128 once the compute of the previous stage is done
-    __device__ __forceinline__ void load(u32x4* r) {
-#pragma unroll
-        for (int j = 0; j < NP; ++j) r[j] = *reinterpret_cast<const u32x4*>(base + voff[j]);
-        base += 2 * KB;
-    }
-    __device__ __forceinline__ void store(unsigned short* dst, const u32x4* r, int wave,
-                                          int lane) const {
-#pragma unroll
-        for (int j = 0; j < NP; ++j)
-            *reinterpret_cast<u32x4*>(dst + (wave + NW * j) * 512 + lane * 8) = r[j];
-    }
-};
+using namespace gtile;
 
 // The launch's argument block: the caller's problems plus the tile bookkeeping the host
 // resolves once (first tile and tile counts per problem, k-steps per tile, split-K slices), so
@@ -131,18 +52,10 @@ struct GemmKArgs {
 typedef const __attribute__((address_space(4))) GemmKArgs KArgs;
 typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
 
-template <int KB>
-__device__ __forceinline__ u32x4 read_frag(const unsigned short* tile, int row, int chunk) {
-    const int c = chunk ^ swz<KB>(row);
-    return *reinterpret_cast<const u32x4*>(tile + row * KB + 8 * c);
-}
 
 // Tile t of the launch -> (problem, output origin, split-K slice).  Tiles of a problem are
 // slice-major; inside a slice, groups of 4 tile-rows, column-major inside a group (L2 reuse of
 // both panels).
-struct TileLoc {
-    int p, m0, n0, slice;
-};
 template <int BM, int BN>
 __device__ __forceinline__ TileLoc locate(KArgs* ka, int t) {
     const int p = (t >= ka->first[1]) + (t >= ka->first[2]) + (t >= ka->first[3]);
@@ -333,182 +246,10 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
     constexpr int EPI_LDS_OFF = KG == 2 ? RM * 4 * RN * 16 * 64 * 4 : 0;   // past KG's `red`
     static_assert(PERSIST || EPI_LDS_OFF + NW * 4096 <= STAGES * STAGE_ELEMS * 2,
                   "epilogue scratch fits the ring");
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    // LDS-transposed epilogue of one 32 x 32 block (gemm_tile.h epi_lds_block)
     auto epi_lds = [&](const TileLoc& L, const f32x16& c, const int i, const int nb,
-                       const int mode, const int Mv, const int Mr, const int Nc, const int ksp,
-                       const int kt, const float scale, const float* bias_p, const float* Rp,
-                       const float* Pin, const unsigned short* Rbp, float* Cp, float* Pp,
-                       unsigned short* Cbp, unsigned short* CbTp, float* csp, float* lpp,
-                       float* wsp, const int64_t ldr, const int64_t ldpin, const int64_t ldrb,
-                       const int64_t ldc, const int64_t ldp, const int64_t ldcb,
-                       const int64_t ldct) __attribute__((always_inline)) {
-        const int rb = L.m0 + wr * (BM / 2) + i * 32;      // first row of this 32-row block
-        float* sc = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + EPI_LDS_OFF) +
-                    wave * 1024;
-        auto arow = [&](int v) { return (v & 3) + 8 * (v >> 2) + 4 * h; };   // block-local row
-        const int rl = lane >> 3, cq = 4 * (lane & 7);   // row layout: rows rl + 8p, 4 columns
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int v = 0; v < 16; ++v) sc[arow(v) * 32 + r32] = c[v];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        f32x4 cv[4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-            cv[p] = *reinterpret_cast<const f32x4*>(sc + (rl + 8 * p) * 32 + cq);
-        const int n4 = nb + cq;
-        if (ksp > 1) {                                       // split-K: raw partial slab
-            float* dst = wsp + (int64_t)L.slice * Mr * Nc;
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int b = rb + rl + 8 * p;
-                if (b < Mv) *reinterpret_cast<f32x4*>(dst + (int64_t)b * Nc + n4) = cv[p];
-            }
-            asm volatile("" ::: "memory");
-            return;
-        }
-        const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 bias4 = bias_p ? *reinterpret_cast<const f32x4*>(bias_p + n4) : zero4;
-        auto body = [&](auto mc) {
-            constexpr int MODE = decltype(mc)::value;
-            constexpr bool X1R = MODE == LDM_GEMM_RESID_SILU || MODE == LDM_GEMM_ADD_R ||
-                                 MODE == LDM_GEMM_DGRAD_SILU;
-            constexpr bool X1C = MODE == LDM_GEMM_ACCUM;
-            constexpr bool X2 = MODE == LDM_GEMM_DGRAD_SILU || MODE == LDM_GEMM_LOSS;
-            constexpr bool XB = MODE == LDM_GEMM_RELU_BWD;
-            constexpr bool LS = MODE == LDM_GEMM_LOSS;
-            f32x4 v1[4], v2[4];
-            u32x2 vb[4];
-            const bool has1 = X1C || (X1R && Rp != nullptr);
-            const float* x1 = X1C ? Cp : Rp;
-            const int64_t ld1 = X1C ? ldc : ldr;
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {    // padding rows read row 0 (valid) and drop it
-                const int b = rb + rl + 8 * p;
-                const int bb = b < Mv ? b : 0;
-                v1[p] = zero4;
-                v2[p] = zero4;
-                vb[p] = u32x2{0u, 0u};
-                if constexpr (X1R || X1C) {
-                    if (has1)
-                        v1[p] = *reinterpret_cast<const f32x4*>(x1 + (int64_t)bb * ld1 + n4);
-                }
-                if constexpr (X2)
-                    v2[p] = *reinterpret_cast<const f32x4*>(Pin + (int64_t)bb * ldpin + n4);
-                if constexpr (XB)
-                    vb[p] = *reinterpret_cast<const u32x2*>(Rbp + (int64_t)bb * ldrb + n4);
-            }
-            // one row at a time from the batched operand loads: only the values the write-back
-            // needs (keep) live across rows (the 128 x 128 kernels spilled with all of it live)
-            f32x4 keep[4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int b = rb + rl + 8 * p;
-                const bool live = b < Mv;
-                f32x4 out, pre_v, dh, dd;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {      // epi()'s expressions, element for element
-                    const float pre = cv[p][e] + bias4[e];
-                    pre_v[e] = pre;
-                    float o = pre;
-                    dh[e] = 0.f;
-                    dd[e] = 0.f;
-                    if constexpr (MODE == LDM_GEMM_SILU) o = silu(pre);
-                    if constexpr (MODE == LDM_GEMM_RESID_SILU) o = v1[p][e] + silu(pre);
-                    if constexpr (MODE == LDM_GEMM_RELU) o = fmaxf(pre, 0.f);
-                    if constexpr (MODE == LDM_GEMM_ACCUM || MODE == LDM_GEMM_ADD_R)
-                        o = v1[p][e] + pre;
-                    if constexpr (MODE == LDM_GEMM_DGRAD_SILU) {
-                        dh[e] = v1[p][e] + pre;
-                        o = dh[e] * silu_grad(v2[p][e]);
-                    }
-                    if constexpr (LS) {
-                        dd[e] = pre - v2[p][e];
-                        o = scale * dd[e];
-                    }
-                    if constexpr (MODE == LDM_GEMM_RELU_BWD) {
-                        const unsigned u = (vb[p][e >> 1] >> (16 * (e & 1))) & 0xffffu;
-                        o = (u != 0 && (u & 0x8000u) == 0) ? pre : 0.f;
-                    }
-                    out[e] = live ? o : 0.f;
-                }
-                if (Cp && live)
-                    *reinterpret_cast<f32x4*>(Cp + (int64_t)b * ldc + n4) =
-                        MODE == LDM_GEMM_DGRAD_SILU ? dh : out;
-                if constexpr (MODE == LDM_GEMM_SILU || MODE == LDM_GEMM_RESID_SILU) {
-                    if (Pp && live) *reinterpret_cast<f32x4*>(Pp + (int64_t)b * ldp + n4) = pre_v;
-                }
-                if (Cbp && b < Mr)
-                    *reinterpret_cast<u32x2*>(Cbp + (int64_t)b * ldcb + n4) =
-                        u32x2{pack2_bf16(out[0], out[1]), pack2_bf16(out[2], out[3])};
-                keep[p] = LS ? dd : out;
-            }
-            if (CbTp || csp || (LS && lpp)) {   // back to accumulator layout through the tile
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    *reinterpret_cast<f32x4*>(sc + (rl + 8 * p) * 32 + cq) = keep[p];
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                float oa[16];
-                float lsum = 0.f;
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    oa[v] = sc[arow(v) * 32 + r32];
-                    if constexpr (LS) {             // epi()'s loss expressions, in its order
-                        const float d = oa[v];
-                        const bool live = rb + arow(v) < Mv;
-                        lsum += live ? d * d : 0.f;
-                        oa[v] = live ? scale * d : 0.f;
-                    }
-                }
-                const int n = nb + r32;
-                if (CbTp) {                   // [n][b]: 4 consecutive rows per 8-byte store
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int b = rb + 8 * g + 4 * h;
-                        if (b < Mr) {
-                            const u32x2 w = {pack2_bf16(oa[4 * g], oa[4 * g + 1]),
-                                             pack2_bf16(oa[4 * g + 2], oa[4 * g + 3])};
-                            const int64_t at = kt ? ((int64_t)(b / kt) * Nc + n) * kt + b % kt
-                                                  : (int64_t)n * ldct + b;
-                            *reinterpret_cast<u32x2*>(CbTp + at) = w;
-                        }
-                    }
-                }
-                if (csp) {                    // one partial per 32-row block and column
-                    float cs = 0.f;
-#pragma unroll
-                    for (int v = 0; v < 16; ++v) cs += oa[v];
-                    cs += __shfl_xor(cs, 32);
-                    if (h == 0 && rb < Mr) csp[(int64_t)(rb / 32) * Nc + n] = cs;
-                }
-                if constexpr (LS) {
-                    if (lpp) {
-#pragma unroll
-                        for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
-                        if (lane == 0 && rb < Mr)      // the block lies inside N here
-                            lpp[(int64_t)(rb / 32) * ((Nc + 31) / 32) + nb / 32] = lsum;
-                    }
-                }
-            }
-            asm volatile("" ::: "memory");
-        };
-        switch (mode) {
-            case LDM_GEMM_SILU: body(std::integral_constant<int, LDM_GEMM_SILU>{}); break;
-            case LDM_GEMM_RESID_SILU:
-                body(std::integral_constant<int, LDM_GEMM_RESID_SILU>{});
-                break;
-            case LDM_GEMM_RELU: body(std::integral_constant<int, LDM_GEMM_RELU>{}); break;
-            case LDM_GEMM_ACCUM: body(std::integral_constant<int, LDM_GEMM_ACCUM>{}); break;
-            case LDM_GEMM_DGRAD_SILU:
-                body(std::integral_constant<int, LDM_GEMM_DGRAD_SILU>{});
-                break;
-            case LDM_GEMM_LOSS: body(std::integral_constant<int, LDM_GEMM_LOSS>{}); break;
-            case LDM_GEMM_ADD_R: body(std::integral_constant<int, LDM_GEMM_ADD_R>{}); break;
-            case LDM_GEMM_RELU_BWD:
-                body(std::integral_constant<int, LDM_GEMM_RELU_BWD>{});
-                break;
-            default: body(std::integral_constant<int, LDM_GEMM_STORE>{}); break;
-        }
+                       const EpiArgs& e) __attribute__((always_inline)) {
+        epi_lds_block<BM>(smem, EPI_LDS_OFF, wave, lane, wr, h, r32, L, c, i, nb, e);
     };
 
     // ---- epilogue ------------------------------------------------------------------------
@@ -559,8 +300,10 @@ __global__ __launch_bounds__(256 * KG) void gemm_bf16_kernel(GemmKArgs a) {
                      (!Rbp || (al(Rbp, 8) && (ldrb & 3) == 0)) && (!bias_p || al(bias_p, 16));
             }
             if (ok) {
-                epi_lds(L, c, i, nb, mode, Mv, Mr, Nc, ksp, kt, scale, bias_p, Rp, Pin, Rbp, Cp,
-                        Pp, Cbp, CbTp, csp, lpp, wsp, ldr, ldpin, ldrb, ldc, ldp, ldcb, ldct);
+                const EpiArgs ea = {mode, Mv, Mr, Nc, ksp, kt, scale, bias_p, Rp, Pin, Rbp, Cp,
+                                    Pp, Cbp, CbTp, csp, lpp, wsp, ldr, ldpin, ldrb, ldc, ldp,
+                                    ldcb, ldct};
+                epi_lds(L, c, i, nb, ea);
                 return;
             }
         }
@@ -969,6 +712,40 @@ int gemm_tiles(const ldm_gemm_args_t& a, int bm, int bn) {
 
 int env_int(const char* name) { return dev_knob(name, 0); }
 
+// The tile ldm_gemm_bf16 runs a launch on (a.tile, or the automatic rule below).  Exposed so the
+// persistent training step (train_dag.hip) can reproduce each launch's k-group split.
+int gemm_tile_choice(const ldm_gemm_args_t& a) {
+    const int forced = dev_knob("LDM_GEMM_TILE", 0);
+    int tile = a.tile;
+    if (tile == 0) {
+        bool k128 = true;
+        for (int p = 0; p < a.n_prob; ++p)
+            for (int g = 0; g < a.prob[p].n_seg; ++g) k128 = k128 && a.prob[p].seg[g].K % 128 == 0;
+        const int t64 = gemm_tiles(a, 64, 64);
+        // tuning knobs per launch size class (tile counts at 64 x 64): <= 256, <= 512, < 2048,
+        // >= 2048
+        const int by_size[4] = {env_int("LDM_GEMM_TILE_SMALL"),
+                                       env_int("LDM_GEMM_TILE_MID"), env_int("LDM_GEMM_TILE_BIG"),
+                                       env_int("LDM_GEMM_TILE_HUGE")};
+        const int cls = t64 <= 256 ? 0 : t64 <= 512 ? 1 : t64 < 2048 ? 2 : 3;
+        tile = forced ? forced : by_size[cls] ? by_size[cls] : t64 >= 2048 ? 15
+             : (k128 && t64 <= 256) ? 24 : 4;
+    }
+    return tile;
+}
+
+// 0 for a tile on one k-group; for the two-k-group tiles (KG = 2: 5, 6, 7, 11 with 64-deep
+// stages, 24 with 128-deep ones) the number of 64-deep k-steps a group takes in a row: group g
+// sums the k-steps q with (q / period) % 2 == g and the tile's result is group 0's sum + group
+// 1's (the reduction above) -- what train_dag.hip reproduces to stay bit-identical.
+int gemm_tile_kgroup_period(int tile) {
+    switch (tile) {
+        case 5: case 6: case 7: case 11: return 1;
+        case 24: return 2;
+        default: return 0;
+    }
+}
+
 int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     LDM_REQUIRE(a.n_prob >= 1 && a.n_prob <= LDM_GEMM_MAX_PROBS, LDM_EINVAL,
                 "ldm_gemm_bf16: n_prob %d", a.n_prob);
@@ -1027,22 +804,7 @@ int gemm_bf16(const ldm_gemm_args_t& a, hipStream_t s) {
     //    768-tile backward launches run in ONE wave of workgroups; the 128-deep 2-stage tile at
     //    2 per CU left half a wave: the step 0.348 -> 0.317-0.326 ms, scripts/rounds/train_tiles2.sh,
     //    profiles/r02h/train_tiles2.log).
-    const int forced = dev_knob("LDM_GEMM_TILE", 0);
-    int tile = a.tile;
-    if (tile == 0) {
-        bool k128 = true;
-        for (int p = 0; p < a.n_prob; ++p)
-            for (int g = 0; g < a.prob[p].n_seg; ++g) k128 = k128 && a.prob[p].seg[g].K % 128 == 0;
-        const int t64 = gemm_tiles(a, 64, 64);
-        // tuning knobs per launch size class (tile counts at 64 x 64): <= 256, <= 512, < 2048,
-        // >= 2048
-        const int by_size[4] = {env_int("LDM_GEMM_TILE_SMALL"),
-                                       env_int("LDM_GEMM_TILE_MID"), env_int("LDM_GEMM_TILE_BIG"),
-                                       env_int("LDM_GEMM_TILE_HUGE")};
-        const int cls = t64 <= 256 ? 0 : t64 <= 512 ? 1 : t64 < 2048 ? 2 : 3;
-        tile = forced ? forced : by_size[cls] ? by_size[cls] : t64 >= 2048 ? 15
-             : (k128 && t64 <= 256) ? 24 : 4;
-    }
+    const int tile = gemm_tile_choice(a);
     if (tile >= 20) {                          // 128-deep stages: every K a multiple of 128
         for (int p = 0; p < a.n_prob; ++p)
             for (int g = 0; g < a.prob[p].n_seg; ++g)

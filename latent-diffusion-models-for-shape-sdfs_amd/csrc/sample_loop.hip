@@ -528,6 +528,38 @@ __device__ __forceinline__ bool stage_tagged(float* xs, const u64* G, int n, uns
 
 constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per wave
 
+// Diagnostic build only (-DSL_STAMP=1, scripts/stamp_sampler.py): every wave of the replica loop
+// keeps per-phase sums of s_memrealtime ticks (100 MHz) in registers over all its layers --
+// 0 own granules landed, 1 the workgroup's staging barrier (the slowest wave's granules), 2 the
+// row dot products, 3 the reduce-scatter, 4 epilogue + publish -- and writes them at its end
+// (g_sl_stamp[workgroup][wave]); slot 5 counts the layers.
+#ifndef SL_STAMP
+#define SL_STAMP 0
+#endif
+#if SL_STAMP
+__device__ unsigned long long g_sl_stamp[256][kRepWaves][8];
+#endif
+struct SlStamp {
+    uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t t = 0;
+    __device__ __forceinline__ void start() {
+        if (SL_STAMP) t = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ void mark(int k) {
+        if (SL_STAMP) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            acc[k] += now - t;
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void flush(int wave) {
+#if SL_STAMP
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)
+            for (int i = 0; i < 6; ++i) g_sl_stamp[blockIdx.x][wave][i] = acc[i];
+#endif
+    }
+};
+
 template <int D_, int MBX>
 __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs a) {
     constexpr int H = 1024, NB = 4, NWV = kRepWaves, R = H / (32 * NWV), RO = D_ / (32 * NWV);
@@ -606,6 +638,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         return replica_sync(sync, xcc, nloc, phase, ok, a.spin_limit);
     };
     // stage this replica's [MBX][K] activations of the layer that published under tag `tg`
+    SlStamp stp;
     auto stage_act = [&](float* dst, const float* plain, const u64* gran, int K, unsigned tg) {
         if (!tagged || gran == nullptr) {
 #pragma unroll
@@ -618,10 +651,13 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         // only this replica's nsh shapes are published (rows of a missing second shape are
         // computed on whatever the LDS holds and never written)
         const bool good = stage_tagged<NT, 2>(dst, gran, nsh * K, tg, status, a.spin_limit);
+        stp.mark(0);
         if (!good) *ok = 0;
         __syncthreads();
+        stp.mark(1);
         return *ok != 0;
     };
+    stp.start();
 
     for (int s = 0; s < a.steps; ++s) {
         const int t = a.t_hi - s;
@@ -649,12 +685,16 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         {
             float v[NV];
             rows_partial<R, R, NJD, MBX>(v, get_in, xs, D, lane);
+            stp.mark(2);
             const float acc = reduce_scatter<NV>(v, lane);
+            stp.mark(3);
             ++phase;
             if (wr_h) {
                 if (tagged) publish_tagged(hgr + (size_t)qb * H + mh, acc + bi, phase);
                 else publish(hrep + (size_t)qb * H + mh, acc + bi);
             }
+            stp.mark(4);
+            if (SL_STAMP) stp.acc[5] += 1;
         }
         if (!boundary()) return;
         // the four blocks as four compile-time copies (a runtime block index into wb would
@@ -673,7 +713,9 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
             float v[NV];
             rows_partial<R, R, NJH, MBX>(v, [&](int r, int j) { return wb[k][r][j]; }, xs, H,
                                          lane);
+            stp.mark(2);
             const float acc = reduce_scatter<NV>(v, lane);
+            stp.mark(3);
             ++phase;
             if (wr_h) {
                 const float pre = acc + ep[k];
@@ -681,6 +723,8 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                 if (tagged) publish_tagged(hgr + (size_t)((k + 1) & 1) * MBX * H + (size_t)qb * H + mh, hv, phase);
                 else publish(hout + (size_t)qb * H + mh, hv);
             }
+            stp.mark(4);
+            if (SL_STAMP) stp.acc[5] += 1;
             alive = boundary();
         };
         static_assert(NB == 4, "four residual blocks");
@@ -696,7 +740,9 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
             float v[NV];
             // out-projection: RO rows, zero-padded to the R-row reduce-scatter
             rows_partial<R, RO, NJH, MBX>(v, get_out, xs, H, lane);
+            stp.mark(2);
             const float acc = reduce_scatter<NV>(v, lane);
+            stp.mark(3);
             ++phase;
             if (wr_o) {
                 const float pre = acc + bo;
@@ -707,9 +753,12 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                     publish_tagged(xgr + (size_t)((s & 1) ^ 1) * MBX * D + (size_t)qb * D + mo,
                                    xv, phase);
             }
+            stp.mark(4);
+            if (SL_STAMP) stp.acc[5] += 1;
         }
         if (!boundary()) return;
     }
+    stp.flush(wave);
 }
 
 // Residency: every workgroup of the grid must be resident at once (the grid barriers wait for
@@ -906,3 +955,13 @@ extern "C" int ldm_sample_loop_config(int form, unsigned spin_limit, int tagged)
 }
 
 extern "C" int ldm_sample_loop_last_form(void) { return g_last_form[cur_dev()].load(); }
+
+#if SL_STAMP
+// diagnostic build only: the replica loop's per-wave phase sums [256][8 waves][8]
+extern "C" int ldm_dev_sample_stamps(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(ldm::g_sl_stamp), sizeof(ldm::g_sl_stamp)) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#endif

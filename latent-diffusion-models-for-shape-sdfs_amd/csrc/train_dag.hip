@@ -1,0 +1,402 @@
+// The whole DDPM training step (config 2, SURVEY.md §8(a) A6/A7/A9 + AdamW) as ONE persistent
+// launch: train_dag_kernel walks the job DAG that denoiser_train.hip build_dag records from the
+// launch-per-GEMM step (train_dag.h).  Why: the launch-per-GEMM step spends two thirds of its
+// time in per-launch fixed cost -- argument issue, ring fill, the epilogue tail of the last
+// workgroups, the gap to the next launch -- and its AdamW (HBM-bound) starts only after the
+// last GEMM (DESIGN.md §5, round-4 stamps).  Here a workgroup that finishes a tile takes the
+// next job at once, dependent layers are handed off per 64-row band instead of per launch, and
+// the weight-gradient tiles, bias sums and AdamW tiles fill the CUs the residual chain leaves
+// idle.
+//
+// Every job computes its outputs with the same instructions as the launch path: the GEMM tile
+// runs gemm_bf16.hip's LDS-DMA ring and its LDS-transposed epilogue (gemm_tile.h), reproducing
+// the k-group split of the launch's tile choice (two accumulators, summed in the same order),
+// the sums are colsum_jobs_kernel's, the updates adamw_tile (adamw_tile.h).  So the step is
+// BIT-IDENTICAL to ldm_denoiser_train_step + ldm_adamw_multi (tests/test_gpu_train_dag.py).
+//
+// Hand-offs (MI355X guide, "Valid forms"): a job's producer drains its stores (every wave
+// s_waitcnt vmcnt(0)), joins a workgroup barrier, and ONE lane fences release at agent scope,
+// drains again (the guide's compiler-hazard fix) and adds to the node's band and all-jobs
+// counters; a consumer's lane polls the counters with relaxed agent loads, fences acquire,
+// drains, and the workgroup joins a barrier before any load of the handed-off bytes.  Every
+// spin is bounded: a timeout raises the status word, every later wait gives up at once, every
+// workgroup still drains its queue and exits, and the host reads the status back.
+#include "train_dag.h"
+#include "gemm_tile.h"
+#include "adamw_tile.h"
+#include "ddpm_common.h"
+
+#include <mutex>
+
+namespace ldm {
+namespace dag {
+namespace {
+using namespace gtile;
+
+typedef const __attribute__((address_space(4))) Table KTab;
+typedef const __attribute__((address_space(4))) Node KNode;
+typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
+
+constexpr int BM = 64, BN = 64, STAGES = 3, KB = 64, NW = 4;
+constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
+constexpr int kLdsBytes = STAGES * STAGE_ELEMS * 2;            // 48 KiB: 3 workgroups per CU
+typedef TileSrc<BM, NW, KB> Src;
+constexpr int G = 2 * Src::NP;                                // DMA pieces per wave per stage
+static_assert(NW * 4096 <= kLdsBytes, "epilogue scratch fits the ring");
+static_assert(64 * (64 + 8) * 2 <= kLdsBytes, "AdamW transpose tile fits the ring");
+
+__device__ __forceinline__ unsigned* ctr(unsigned* sync, int i) {
+    return sync + (kSyncCtr0 + i) * kCtrStride;
+}
+
+// Poll *w (relaxed agent-scope load) until >= target.  Run by a whole wave with wave-uniform
+// arguments: every lane loads the same word and the value is made uniform (readfirstlane), so
+// the loop is a scalar loop -- no lane of the wave leaves it before another, which a barrier
+// later in the kernel relies on (a one-lane spin let the compiler split the scheduler loop per
+// lane around the workgroup barrier: a hang).  Bounded in TIME (s_memrealtime, 100 MHz:
+// `limit_us` microseconds), not in polls -- a poll's latency grows with the number of pollers
+// -- and abandoned as soon as anyone raised the status word.  The sleep between polls backs off
+// (64 -> 512 clocks) so that hundreds of waiting workgroups do not crowd the counters' lines.
+__device__ __forceinline__ unsigned poll(const unsigned* w) {
+    return __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ bool spin(const unsigned* w, unsigned target, unsigned* status,
+                                     unsigned limit_us) {
+    if (poll(w) >= target) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t lim = (uint64_t)limit_us * 100u;
+    for (unsigned n = 1;; ++n) {
+        if (n <= 4) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(8);
+        if (poll(w) >= target) return true;
+        if ((n & 15) == 0) {
+            if (poll(status) != 0) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > lim) {
+                if ((threadIdx.x & 63) == 0)
+                    __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned short to_bf16(float x) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 v = {x, 0.f};
+    return (unsigned short)(__builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2)) &
+                            0xffffu);
+}
+
+// ---- GEMM tile job: 64 x 64 output tile (tm, tn) of node N's problem ------------------------
+// The launch path's ring (gemm_bf16_kernel<64, 64, 3, 1, false, false, 64>, non-persistent) and
+// epilogue.  kgp > 0 reproduces a launch that ran the problem on two k-groups (tile 24: 128-deep
+// stages, kgp = 2; 64-deep, kgp = 1): k-step i (64 deep) accumulates into acc[(i / kgp) & 1] and
+// the tile's result is acc[0] + acc[1], that launch's summation exactly.
+__device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
+                                         unsigned short* smem, int wave, int lane) {
+    KProb& P = N.P;
+    const int tn_n = N.tiles_n;
+    const int tm = job / tn_n, tn = job - tm * tn_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int wr = wave >> 1, wc = wave & 1, r32 = lane & 31, h = lane >> 5;
+    const int nk = N.nk, kgp = N.kgp;
+    Src srcA, srcB;
+    int seg = 0, seg_left = 0, qi = 0;
+    auto seat = [&](int sg) {
+        const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[sg];
+        srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
+        srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
+        seg_left = S.K / KB;
+    };
+    auto issue = [&]() {
+        if (seg_left == 0) seat(++seg);
+        unsigned short* st = smem + (qi % STAGES) * STAGE_ELEMS;
+        ++qi;
+        srcA.issue(st, wave, false);
+        srcB.issue(st + A_ELEMS, wave, false);
+        --seg_left;
+    };
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        acc0[v] = 0.f;
+        acc1[v] = 0.f;
+    }
+    auto compute = [&](const unsigned short* sa, f32x16& acc) __attribute__((always_inline)) {
+        const unsigned short* sb = sa + A_ELEMS;
+        u32x4 af[KB / 16], bfr[KB / 16];
+#pragma unroll
+        for (int s = 0; s < KB / 16; ++s) {
+            af[s] = read_frag<KB>(sa, wr * (BM / 2) + r32, 2 * s + h);
+            bfr[s] = read_frag<KB>(sb, wc * (BN / 2) + r32, 2 * s + h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < KB / 16; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[s]),
+                                                          __builtin_bit_cast(bf16x8, bfr[s]),
+                                                          acc, 0, 0, 0);
+    };
+    seat(0);
+    issue();
+    if (nk > 1) issue();
+    for (int it = 0; it < nk; ++it) {
+        // RAW: this wave's pieces of stage it landed (one younger stage may still fly); the
+        // barrier makes every wave's pieces visible and retires every read of stage it - 1,
+        // whose slot the issue below refills
+        if (it + 1 < nk)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (it + 2 < nk) issue();
+        const unsigned short* st = smem + (it % STAGES) * STAGE_ELEMS;
+        if (kgp > 0 && ((it / kgp) & 1)) compute(st, acc1);
+        else compute(st, acc0);
+    }
+    if (kgp > 0) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc0[v] += acc1[v];
+    }
+    __syncthreads();        // the epilogue's LDS tiles overwrite ring slots others may still read
+    EpiArgs e;
+    e.mode = P.mode; e.Mv = P.M_valid; e.Mr = P.M; e.Nc = P.N; e.ksp = 1; e.kt = P.ct_blk;
+    e.scale = P.scale;
+    e.bias_p = P.bias; e.Rp = P.R;
+    e.Pin = N.pin_eps ? eps : P.P_in;
+    e.Rbp = reinterpret_cast<const unsigned short*>(P.Rb);
+    e.Cp = P.C; e.Pp = P.P;
+    e.Cbp = reinterpret_cast<unsigned short*>(P.Cb);
+    e.CbTp = reinterpret_cast<unsigned short*>(P.CbT);
+    e.csp = P.colsum; e.lpp = P.loss_part; e.wsp = nullptr;
+    e.ldr = P.ldr; e.ldpin = P.ldp_in; e.ldrb = P.ldrb; e.ldc = P.ldc; e.ldp = P.ldp;
+    e.ldcb = P.ldcb; e.ldct = P.ldct;
+    const TileLoc L = {0, m0, n0, 0};
+    epi_lds_block<BM>(smem, 0, wave, lane, wr, h, r32, L, acc0, 0, n0 + wc * (BN / 2) + 0, e);
+}
+
+// ---- input preparation of one 64-row band (prep_inputs_kernel<true>'s arithmetic) -----------
+__device__ __forceinline__ void prep_job(KNode& N, int band, const float* x0, const float* eps,
+                                         const int32_t* t) {
+#pragma clang fp contract(off)
+    const int B = N.B, Bp = N.Bp, D = N.D, TE = N.TE, W = D + TE;
+    const float* sab = N.sab;
+    const float* s1mab = N.s1mab;
+    const float* emb = N.emb;
+    unsigned short* xt_b = N.xt_b;
+    unsigned short* xt_T = N.xt_T;
+    unsigned short* e_b = N.e_b;
+    unsigned short* e_T = N.e_T;
+    for (int i = threadIdx.x; i < 64 * W; i += 256) {
+        const int b = band * 64 + i / W, c = i - (i / W) * W;
+        const bool live = b < B;
+        const int tb = live ? t[b] : 0;
+        if (c < D) {
+            float v = 0.f;
+            if (live) {
+                const float a = sab[tb] * x0[(int64_t)b * D + c];
+                const float e = s1mab[tb] * eps[(int64_t)b * D + c];
+                v = a + e;
+            }
+            const unsigned short q = to_bf16(v);
+            xt_b[(int64_t)b * D + c] = q;
+            xt_T[(int64_t)c * Bp + b] = q;
+        } else {
+            const int cc = c - D;
+            const unsigned short q = to_bf16(live ? emb[(int64_t)tb * TE + cc] : 0.f);
+            e_b[(int64_t)b * TE + cc] = q;
+            e_T[(int64_t)cc * Bp + b] = q;
+        }
+    }
+}
+
+// ---- a bias gradient (or the loss) from the epilogues' partials, + that bias's AdamW --------
+// colsum_jobs_kernel's sum (8 loads in flight, summed in row order), then adamw_update on the
+// stored gradient, as adamw_multi_kernel does.
+__device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
+                                        const AdamHyper& hy) {
+    const int rows = N.rows, len = N.len;
+    const int64_t ld = N.ld;
+    const float scale = N.scale;
+    float* dst = N.dst ? N.dst : loss_out;
+    const int ti = N.adam;
+    for (int c = threadIdx.x; c < len; c += 256) {
+        const float* src = N.src + c;
+        float s = 0.f;
+        int r = 0;
+        for (; r + 8 <= rows; r += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(r + u) * ld];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; r < rows; ++r) s += src[(int64_t)r * ld];
+        const float g = scale * s;
+        dst[c] = g;
+        if (ti >= 0) {
+            const __attribute__((address_space(4))) ldm_adamw_tensor_t& T = tab->tensor[ti];
+            float p = T.p[c], m = T.m[c], v = T.v[c];
+            adamw_update(p, g, m, v, hy.decay, hy.omb1, hy.b2, hy.omb2, hy.eps, hy.step_size,
+                         hy.bc2_sqrt);
+            T.p[c] = p;
+            T.m[c] = m;
+            T.v[c] = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+    __shared__ int s_job;
+    __shared__ int s_last;
+    typedef const __attribute__((address_space(4))) LaunchArgs KLA;
+    KLA* ka = (KLA*)__builtin_amdgcn_kernarg_segment_ptr();
+    KTab* tab = (KTab*)ka->tab;
+    unsigned* sync = ka->sync;
+    unsigned* status = sync + kSyncStatus * kCtrStride;
+    const unsigned limit = ka->spin_limit;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int q = blockIdx.x & (kQueues - 1);
+    const float* dh = ka->d_hyper;
+    const AdamHyper hy = {dh ? dh[0] : ka->hy[0], dh ? dh[1] : ka->hy[1], dh ? dh[2] : ka->hy[2],
+                          dh ? dh[3] : ka->hy[3], dh ? dh[4] : ka->hy[4], dh ? dh[5] : ka->hy[5],
+                          dh ? dh[6] : ka->hy[6]};
+    const bool table_ok = tab->hash == ka->hash;
+    if (!table_ok && threadIdx.x == 0)
+        __hip_atomic_store(status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int qlen = tab->qlen[q], qoff = tab->qoff[q];
+    const uint32_t* entries = reinterpret_cast<const uint32_t*>(ka->tab + 1);
+    unsigned* head = sync + (kSyncHead + q) * kCtrStride;
+    // The scheduler's control flow is wave-uniform (wave 0 runs it with all its lanes; a lane-0
+    // region holds no loop), so every wave meets every workgroup barrier the same number of
+    // times.
+    for (;;) {
+        if (wave == 0) {
+            unsigned jl = 0;
+            if (lane == 0 && table_ok)
+                jl = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int j = table_ok ? (int)__builtin_amdgcn_readfirstlane(jl) : qlen;
+            int e = -1;
+            if (j < qlen) {
+                e = (int)__builtin_amdgcn_readfirstlane(entries[qoff + j]);
+                // wait for the job's inputs (the consumer side of the hand-off)
+                KNode& N = tab->node[e >> 16];
+                const int job = e & 0xffff;
+                const int band = N.type == N_GEMM ? job / N.tiles_n : job;
+                bool ok = true;
+                for (int d = 0; d < N.ndep && ok; ++d)
+                    ok = spin(ctr(sync, N.dep_ctr[d] + (N.dep_band[d] ? band : 0)),
+                              N.dep_target[d], status, limit);
+                if (!ok) e = -2 - e;     // skip the job (everything drains after a timeout)
+                if (!(ka->dbg & 16)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (lane == 0) s_job = e;
+        }
+        __syncthreads();
+        const int e = __builtin_amdgcn_readfirstlane(s_job);
+        if (e == -1) break;
+        if (e >= 0) {
+            KNode& N = tab->node[e >> 16];
+            const int job = e & 0xffff;
+            const int type = N.type;
+            if ((ka->dbg >> type) & 1) {
+                // diagnostics: this node type's compute skipped
+            } else if (type == N_GEMM) {
+                gemm_job(N, job, ka->eps, smem, wave, lane);
+            } else if (type == N_PREP) {
+                prep_job(N, job, ka->x0, ka->eps, ka->t);
+            } else if (type == N_SUM) {
+                sum_job(tab, N, ka->loss_out, hy);
+            } else {
+                const __attribute__((address_space(4))) ldm_adamw_tensor_t& T =
+                    tab->tensor[N.adam];
+                const int tr = job / N.tiles_n, tc = job - tr * N.tiles_n;
+                const int tl = tr * ((T.cols + 63) / 64) + N.col_off + tc;
+                adamw_tile(T, hy, *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem), tl);
+            }
+            // the producer side of the hand-off: every wave's stores drained, one wave releases
+            // and one lane counts the job
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (wave == 0) {
+                if (!(ka->dbg & 16)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) {
+                    if (N.out_band >= 0) {
+                        const int band = type == N_GEMM ? job / N.tiles_n : job;
+                        __hip_atomic_fetch_add(ctr(sync, N.out_band + band), 1u,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    __hip_atomic_fetch_add(ctr(sync, N.out_all), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        // (s_job is rewritten only after the barrier at the top of the next round, which every
+        // wave reaches after its read above)
+    }
+    // exit: the last workgroup out zeroes the heads, the exit counter and every job counter for
+    // the next launch (the status word stays for the host to read)
+    if (wave == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned nl = 0;
+        if (lane == 0)
+            nl = __hip_atomic_fetch_add(sync + kSyncExit * kCtrStride, 1u, __ATOMIC_ACQ_REL,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = __builtin_amdgcn_readfirstlane(nl) + 1 == gridDim.x;
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lane == 0) s_last = last;
+    }
+    __syncthreads();
+    // after a failure the words stay as they are for inspection; ldm_denoiser_train_status
+    // zeroes them when it reads a non-zero status
+    if (s_last && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        const int nc = tab->n_counters;
+        for (int i = threadIdx.x; i < kSyncCtr0 + nc; i += 256)
+            if (i != kSyncStatus)
+                __hip_atomic_store(sync + i * kCtrStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+}  // namespace
+
+int dag_grid(int* grid) {
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static int g[kMaxDev], err[kMaxDev];
+    int dev = 0;
+    LDM_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev, LDM_EINVAL,
+                "train dag: no current device");
+    std::call_once(once[dev], [&] {
+        const void* k = reinterpret_cast<const void*>(&train_dag_kernel);
+        hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           kLdsBytes);
+        int per_cu = 0, cus = 0;
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, kLdsBytes);
+        if (e == hipSuccess)
+            e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess && per_cu < 1) e = hipErrorInvalidConfiguration;
+        err[dev] = (int)e;
+        // every workgroup resident (the deadlock-freedom argument needs it): the occupancy
+        // answer x CUs, rounded down to whole queues
+        g[dev] = (per_cu * cus) / kQueues * kQueues;
+    });
+    LDM_REQUIRE(err[dev] == 0, err[dev], "train dag: occupancy query failed: %s",
+                hipGetErrorString((hipError_t)err[dev]));
+    *grid = g[dev];
+    return 0;
+}
+
+int dag_launch(const LaunchArgs& a, int grid, hipStream_t s) {
+    LDM_REQUIRE(grid >= kQueues && grid % kQueues == 0, LDM_EINVAL, "train dag: grid %d", grid);
+    hipLaunchKernelGGL(train_dag_kernel, dim3(grid), dim3(256), kLdsBytes, s, a);
+    return launch_status("ldm_denoiser_train_step (dag)");
+}
+
+}  // namespace dag
+}  // namespace ldm

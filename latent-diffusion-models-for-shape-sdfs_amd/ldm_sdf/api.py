@@ -430,6 +430,16 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
                     w.copy_(p)                   # an fp32 working copy that is not the master
         state.step += 1
         state.losses.append(loss)
+    if fused and ops.train_step_last_form() == "dag":
+        # the one-launch step's waits are bounded: a non-zero status means a step gave up and
+        # the weights are not to be trusted (one read-back per train() call, where the losses
+        # are read back anyway)
+        dev_ = denoiser.device_pack(dtype, device, with_tables=False)
+        st = ops.train_status(dev_["desc"], batch, denoiser.train_workspace(batch, device))
+        if st != 0:
+            raise capi.LdmError(f"train: the one-launch training step reported status {st} "
+                                "(1: a dependency wait timed out, 3: stale job table); the "
+                                "parameters are not valid")
     if state.optimizer is None and dtype == "bf16":
         # the built-in AdamW kept every working copy current (bf16 copies in both layouts; an
         # fp32 pack holds the masters themselves): only the E tables (sampling) are rebuilt

@@ -675,6 +675,34 @@ def denoiser_train_step_adamw(desc: capi.Denoiser, sched_desc: capi.Sched, x0: t
         "ldm_denoiser_train_step_adamw")
 
 
+TRAIN_FORMS = {"auto": 0, "launches": 1, "dag": 2}
+
+
+def train_step_config(form: str = "auto", spin_limit: int = 0) -> None:
+    """Form of ``denoiser_train_step_adamw`` on the current device (``ldm_train_step_config``):
+    "auto" (the one-launch DAG step whenever the configuration has one), "launches" (one launch
+    per GEMM group + AdamW), "dag" (required).  Same bits either way.  ``spin_limit``: polls
+    before a DAG wait gives up (0 = default; tiny values exercise the timeout path)."""
+    capi.check(capi.load().ldm_train_step_config(TRAIN_FORMS[form], int(spin_limit)),
+               "ldm_train_step_config")
+
+
+def train_step_last_form() -> str:
+    """The form the last ``denoiser_train_step_adamw`` on this device ran ("" before any)."""
+    f = capi.load().ldm_train_step_last_form()
+    return {0: "", 1: "launches", 2: "dag"}.get(f, str(f))
+
+
+def train_status(desc: capi.Denoiser, B: int, ws: torch.Tensor) -> int:
+    """The DAG step's status word in ``ws`` (read and cleared; one stream synchronisation):
+    0 ok, 1 a wait timed out (that step's results are garbage), 3 stale job table."""
+    st = C.c_uint(0)
+    capi.check(capi.load().ldm_denoiser_train_status(C.byref(desc), B, ws.data_ptr(),
+                                                     C.byref(st), capi.stream_handle(ws.device)),
+               "ldm_denoiser_train_status")
+    return int(st.value)
+
+
 def adamw_hyper(*, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                 step: int) -> List[float]:
     """The 7 AdamW scalars of one step exactly as the library derives them
