@@ -1122,9 +1122,7 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
     const dag::Table& T = h->tab;
     static const char* kType[] = {"gemm", "prep", "sum", "adam"};
     size_t o = 0;
-    auto put = [&](const char* fmt, auto... v) {
-        if (o < len) o += (size_t)snprintf(buf + o, len - o, fmt, v...);
-    };
+#define put(...) (o < len ? (void)(o += (size_t)snprintf(buf + o, len - o, __VA_ARGS__)) : (void)0)
     put("grid %d nodes %d counters %d entries %d\n", T.grid, T.n_nodes, T.n_counters,
         T.n_entries);
     for (int i = 0; i < T.n_nodes; ++i) {
@@ -1136,6 +1134,7 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
         put("\n");
     }
     for (int q = 0; q < dag::kQueues; ++q) put("queue %d: %d jobs at %d\n", q, T.qlen[q], T.qoff[q]);
+#undef put
     delete h;
     return 0;
 }

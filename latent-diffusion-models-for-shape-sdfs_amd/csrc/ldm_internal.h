@@ -47,6 +47,24 @@ int set_max_lds_once(int bytes, const char* what) {
 
 #define LDM_ALIGNED(p, a) ((((uintptr_t)(p)) & ((a) - 1)) == 0)
 
+// Device-side invariant checks: compiled in by `make DEBUG=1` (-DLDM_DEBUG), where a failed
+// check prints its location and traps the kernel (an error the host sees at the next
+// synchronisation); the product build compiles them out.
+#ifdef LDM_DEBUG
+#define LDM_DASSERT(cond)                                                                    \
+    do {                                                                                     \
+        if (!(cond)) {                                                                       \
+            printf("LDM_DASSERT %s:%d: %s (block %d thread %d)\n", __FILE__, __LINE__, #cond, \
+                   (int)blockIdx.x, (int)threadIdx.x);                                       \
+            __builtin_trap();                                                                \
+        }                                                                                    \
+    } while (0)
+#else
+#define LDM_DASSERT(cond) \
+    do {                  \
+    } while (0)
+#endif
+
 inline int launch_status(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

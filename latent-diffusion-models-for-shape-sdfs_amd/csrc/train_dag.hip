@@ -246,6 +246,17 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
     }
 }
 
+// Diagnostic build only (-DDAG_TRACE=1, scripts/trace_dag.py): per queue entry the workgroup that
+// ran it and the s_memrealtime stamps (100 MHz) of its dequeue, of its inputs being ready and of
+// its completion (counters raised); per workgroup its start and exit.
+#ifndef DAG_TRACE
+#define DAG_TRACE 0
+#endif
+#if DAG_TRACE
+__device__ unsigned long long g_dag_trace[kMaxEntries][4];
+__device__ unsigned long long g_dag_wg[4096][2];
+#endif
+
 __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     __shared__ int s_job;
@@ -268,6 +279,11 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
     const int qlen = tab->qlen[q], qoff = tab->qoff[q];
     const uint32_t* entries = reinterpret_cast<const uint32_t*>(ka->tab + 1);
     unsigned* head = sync + (kSyncHead + q) * kCtrStride;
+#if DAG_TRACE
+    uint64_t tr_deq = 0, tr_rdy = 0;
+    int tr_idx = 0;
+    if (threadIdx.x == 0) g_dag_wg[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+#endif
     // The scheduler's control flow is wave-uniform (wave 0 runs it with all its lanes; a lane-0
     // region holds no loop), so every wave meets every workgroup barrier the same number of
     // times.
@@ -279,18 +295,28 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
             const int j = table_ok ? (int)__builtin_amdgcn_readfirstlane(jl) : qlen;
             int e = -1;
             if (j < qlen) {
+#if DAG_TRACE
+                tr_deq = __builtin_amdgcn_s_memrealtime();
+                tr_idx = qoff + j;
+#endif
+                LDM_DASSERT(qoff + j < tab->n_entries);
                 e = (int)__builtin_amdgcn_readfirstlane(entries[qoff + j]);
+                LDM_DASSERT((e >> 16) < tab->n_nodes);
                 // wait for the job's inputs (the consumer side of the hand-off)
                 KNode& N = tab->node[e >> 16];
                 const int job = e & 0xffff;
                 const int band = N.type == N_GEMM ? job / N.tiles_n : job;
                 bool ok = true;
+                LDM_DASSERT(job < N.tiles_m * N.tiles_n && N.ndep <= kMaxDeps);
                 for (int d = 0; d < N.ndep && ok; ++d)
                     ok = spin(ctr(sync, N.dep_ctr[d] + (N.dep_band[d] ? band : 0)),
                               N.dep_target[d], status, limit);
                 if (!ok) e = -2 - e;     // skip the job (everything drains after a timeout)
                 if (!(ka->dbg & 16)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if DAG_TRACE
+                tr_rdy = __builtin_amdgcn_s_memrealtime();
+#endif
             }
             if (lane == 0) s_job = e;
         }
@@ -324,13 +350,21 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
                 if (!(ka->dbg & 16)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) {
+                    LDM_DASSERT(N.out_all < tab->n_counters);
                     if (N.out_band >= 0) {
                         const int band = type == N_GEMM ? job / N.tiles_n : job;
+                        LDM_DASSERT(N.out_band + band < tab->n_counters);
                         __hip_atomic_fetch_add(ctr(sync, N.out_band + band), 1u,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     __hip_atomic_fetch_add(ctr(sync, N.out_all), 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+#if DAG_TRACE
+                    g_dag_trace[tr_idx][0] = (uint64_t)(unsigned)e << 32 | blockIdx.x;
+                    g_dag_trace[tr_idx][1] = tr_deq;
+                    g_dag_trace[tr_idx][2] = tr_rdy;
+                    g_dag_trace[tr_idx][3] = __builtin_amdgcn_s_memrealtime();
+#endif
                 }
             }
         }
@@ -351,6 +385,9 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
         if (lane == 0) s_last = last;
     }
     __syncthreads();
+#if DAG_TRACE
+    if (threadIdx.x == 0) g_dag_wg[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
     // after a failure the words stay as they are for inspection; ldm_denoiser_train_status
     // zeroes them when it reads a non-zero status
     if (s_last && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -392,6 +429,14 @@ int dag_grid(int* grid) {
     return 0;
 }
 
+#if DAG_TRACE
+int dag_trace(void* entries, void* wgs) {
+    if (hipMemcpyFromSymbol(entries, HIP_SYMBOL(g_dag_trace), sizeof(g_dag_trace)) != hipSuccess)
+        return 1;
+    return hipMemcpyFromSymbol(wgs, HIP_SYMBOL(g_dag_wg), sizeof(g_dag_wg)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 int dag_launch(const LaunchArgs& a, int grid, hipStream_t s) {
     LDM_REQUIRE(grid >= kQueues && grid % kQueues == 0, LDM_EINVAL, "train dag: grid %d", grid);
     hipLaunchKernelGGL(train_dag_kernel, dim3(grid), dim3(256), kLdsBytes, s, a);
@@ -400,3 +445,11 @@ int dag_launch(const LaunchArgs& a, int grid, hipStream_t s) {
 
 }  // namespace dag
 }  // namespace ldm
+
+#if DAG_TRACE
+// diagnostic build: the last launch's trace (entries: kMaxEntries x {workgroup, dequeue, inputs
+// ready, done}; workgroups: 4096 x {start, exit}), s_memrealtime ticks
+extern "C" int ldm_dev_train_dag_trace(void* entries, void* wgs) {
+    return ldm::dag::dag_trace(entries, wgs);
+}
+#endif

@@ -274,6 +274,73 @@ class TrainState:
     adam_pack: Optional[Dict[str, object]] = None    # the device pack the table points into
     graphs: Optional[Dict[str, object]] = None       # captured steps (train(graph=True))
 
+    # ---- checkpoint / resume ({denoiser, optimizer, step, rng}) --------------
+    FORMAT = "ldm_sdf.TrainState/1"
+
+    def save(self, path: str, generator: Optional[torch.Generator] = None) -> None:
+        """Write the training state: the fp32 masters (the denoiser's parameters), the built-in
+        AdamW moments or a torch optimizer's state dict, the step count, the losses, the
+        hyper-parameters and -- when given -- the random generator's state, so that
+        ``TrainState.load`` + ``train(..., state=)`` continues the run bit for bit (resume at a
+        multiple of train()'s 32-step draw block).  Derived data (bf16 working copies, E tables,
+        AdamW descriptor tables, graphs) is rebuilt after a load, never saved."""
+        if self.masters is None:
+            raise ValueError("TrainState.save: nothing trained yet")
+        ck = {"format": self.FORMAT, "step": int(self.step),
+              "losses": [float(l) for l in self.losses], "hparams": dict(self.hparams),
+              "masters": {n: v.detach().cpu() for n, v in self.masters.items()}}
+        if self.adam is not None:
+            ck["adam"] = {n: (m.detach().cpu(), v.detach().cpu())
+                          for n, (m, v) in self.adam.items()}
+        if self.optimizer is not None:
+            ck["optimizer"] = self.optimizer.state_dict()
+        if generator is not None:
+            ck["rng"] = generator.get_state().cpu()
+            ck["rng_device"] = str(generator.device)
+        torch.save(ck, path)
+
+    @classmethod
+    def load(cls, path: str, denoiser: MLPDenoiser, device=None,
+             generator: Optional[torch.Generator] = None,
+             optimizer: Optional[torch.optim.Optimizer] = None) -> "TrainState":
+        """Restore a state written by ``save`` into ``denoiser`` (its parameters become the
+        saved masters, on ``device``) and, when given, ``generator`` (its state) and
+        ``optimizer`` (its state dict).  Loaded with ``torch.load(weights_only=True)``: nothing
+        in the file is executed."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        if ck.get("format") != cls.FORMAT:
+            raise ValueError(f"{path}: not a {cls.FORMAT} checkpoint")
+        device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
+        names = denoiser.names()
+        if sorted(ck["masters"]) != sorted(names):
+            raise ValueError(f"{path}: parameters {sorted(ck['masters'])} do not match the "
+                             f"denoiser's {sorted(names)}")
+        for n in names:
+            if tuple(ck["masters"][n].shape) != tuple(denoiser.params[n].shape):
+                raise ValueError(f"{path}: {n} has shape {tuple(ck['masters'][n].shape)}")
+        denoiser.params = {n: ck["masters"][n].to(torch.float32) for n in names}
+        denoiser.to_device(device)               # also drops packs, tables, workspaces
+        denoiser.invalidate()
+        st = cls()
+        st.step = int(ck["step"])
+        st.losses = list(ck["losses"])
+        st.hparams = dict(ck["hparams"])
+        st.masters = {n: denoiser.params[n] for n in names}
+        for v in st.masters.values():
+            v.requires_grad_(False)
+        if "adam" in ck:
+            st.adam = {n: (m.to(device), v.to(device)) for n, (m, v) in ck["adam"].items()}
+        if optimizer is not None:
+            if "optimizer" not in ck:
+                raise ValueError(f"{path}: no optimizer state saved")
+            optimizer.load_state_dict(ck["optimizer"])
+            st.optimizer = optimizer
+        if generator is not None:
+            if "rng" not in ck:
+                raise ValueError(f"{path}: no generator state saved")
+            generator.set_state(ck["rng"])
+        return st
+
 
 def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
                t: torch.Tensor, eps: torch.Tensor, *, dtype: str = "bf16",

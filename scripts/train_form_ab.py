@@ -19,18 +19,20 @@ dev = torch.device("cuda", 0)
 lat = torch.randn(1000, 256, device=dev) * 0.5
 sch = ldm_sdf.DDPMSchedule()
 forms = os.environ.get("AB_FORMS", "dag,launches").split(",")
-states, models = {}, {}
-for f in forms:
+states, models, gens = {}, {}, {}
+for f in forms:     # same weights, same t / eps draws per form: the params must end bit-identical
     ops.train_step_config(f)
     models[f] = ldm_sdf.MLPDenoiser(seed=4321)
-    states[f] = ldm_sdf.train(models[f], sch, lat, steps=3, batch=1000)
+    gens[f] = torch.Generator(device=dev).manual_seed(7)
+    states[f] = ldm_sdf.train(models[f], sch, lat, steps=3, batch=1000, generator=gens[f])
 res = {f: [] for f in forms}
 for r in range(R):
     for f in forms:
         ops.train_step_config(f)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        states[f] = ldm_sdf.train(models[f], sch, lat, steps=S, batch=1000, state=states[f])
+        states[f] = ldm_sdf.train(models[f], sch, lat, steps=S, batch=1000, state=states[f],
+                                  generator=gens[f])
         torch.cuda.synchronize()
         res[f].append(S / (time.perf_counter() - t0))
         assert ops.train_step_last_form() == f

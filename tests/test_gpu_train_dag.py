@@ -126,3 +126,49 @@ def test_dag_required_form_fails_loudly_with_side_stream(dev, form):
     ldm_sdf.train(model, ldm_sdf.DDPMSchedule(), lat, steps=1, batch=64, dtype="bf16",
                   overlap=True)
     assert ops.train_step_last_form() == "launches"
+
+
+def test_trainstate_save_resume_bitwise(dev, tmp_path):
+    """SURVEY §5 checkpoint / resume: 64 uninterrupted steps == 32 steps, TrainState.save
+    (masters, AdamW moments, step, losses, generator state), a FRESH denoiser object loading it
+    (TrainState.load), 32 more steps -- bit for bit: losses, masters, moments."""
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser
+    from ldm_sdf.api import TrainState
+    sch = ldm_sdf.DDPMSchedule()
+    lat = torch.randn(256, 256, generator=torch.Generator().manual_seed(5)).to(dev) * 0.5
+
+    def fresh(seed):
+        m = MLPDenoiser(seed=seed)
+        m.to_device(dev)
+        return m
+
+    ref = fresh(11)
+    g = torch.Generator(device=dev).manual_seed(3)
+    st = ldm_sdf.train(ref, sch, lat, steps=64, batch=256, lr=1e-3, weight_decay=0.01,
+                       dtype="bf16", generator=g)
+    a = fresh(11)
+    g2 = torch.Generator(device=dev).manual_seed(3)
+    st_a = ldm_sdf.train(a, sch, lat, steps=32, batch=256, lr=1e-3, weight_decay=0.01,
+                         dtype="bf16", generator=g2)
+    path = str(tmp_path / "train_state.pt")
+    st_a.save(path, generator=g2)
+    b = fresh(999)                               # other weights: all must come from the file
+    g3 = torch.Generator(device=dev).manual_seed(12345)
+    st_b = TrainState.load(path, b, device=dev, generator=g3)
+    assert st_b.step == 32 and st_b.hparams == {"lr": 1e-3, "weight_decay": 0.01}
+    st_b = ldm_sdf.train(b, sch, lat, steps=32, batch=256, dtype="bf16", generator=g3,
+                         state=st_b)
+    torch.cuda.synchronize()
+    assert st_b.step == 64
+    assert st_b.losses == st.losses
+    for n in ref.params:
+        assert torch.equal(b.params[n], ref.params[n]), n
+        assert torch.equal(st_b.adam[n][0], st.adam[n][0]) and \
+            torch.equal(st_b.adam[n][1], st.adam[n][1]), n
+    # and the resumed model samples like the uninterrupted one
+    xT = torch.randn(4, 256, generator=torch.Generator().manual_seed(1)).to(dev)
+    nz = torch.randn(1000, 4, 256, generator=torch.Generator().manual_seed(2)).to(dev)
+    s_ref = ldm_sdf.sample(ref, sch, 4, steps=20, x_T=xT, noise=nz, device=dev)
+    s_b = ldm_sdf.sample(b, sch, 4, steps=20, x_T=xT, noise=nz, device=dev)
+    assert torch.equal(s_ref, s_b)
