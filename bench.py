@@ -331,10 +331,11 @@ class SlabTimer:
 
 def run_decode_steps(slab, B: int, N: int, *, steps: int, warmup: int, world: int, group,
                      device: torch.device, out: torch.Tensor, sync=None,
-                     shapes_per_group=None, on_timed=None) -> float:
+                     shapes_per_group=None, on_timed=None, local=None) -> float:
     """The bench's per-rank step loop (shared with the gloo test, tests/test_bench_gloo.py):
     ``warmup`` untimed steps, then barrier + sync, ``steps`` timed steps, sync + barrier, and
-    the MAX of the per-rank elapsed times (all-reduce).  One step = the (sharded) decode of B
+    the MAX of the per-rank elapsed times (all-reduce; ``local``, a list, receives this rank's
+    own).  One step = the (sharded) decode of B
     shapes on an N^3 grid into ``out``; ``slab(k0, k1, dst, b0, b1)`` computes a slab."""
     from ldm_sdf.dist import decode_sharded
     sync = sync or (lambda: None)
@@ -360,11 +361,26 @@ def run_decode_steps(slab, B: int, N: int, *, steps: int, warmup: int, world: in
     if world > 1:
         dist.barrier(group)
     elapsed = time.perf_counter() - t0
+    if local is not None:
+        local.append(elapsed)           # this rank's own time (before the max over ranks)
     if world > 1:
         tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
         elapsed = float(tt)
     return elapsed
+
+
+def rank_breakdown(step_ms: float, kernel_ms: float, group, device) -> dict:
+    """Every rank's step time, its slab kernels' time per step (HIP events) and the difference
+    -- the part of the all-gathers the kernels did not hide -- gathered from all ranks, with the
+    world size and backend the process group reports (tests/test_bench_gloo.py)."""
+    loc = torch.tensor([step_ms, kernel_ms], device=device, dtype=torch.float64)
+    n = dist.get_world_size(group)
+    allv = [torch.zeros_like(loc) for _ in range(n)]
+    dist.all_gather(allv, loc, group=group)
+    return {"world_seen": n, "backend": dist.get_backend(group),
+            "per_rank": [{"rank": r, "step_ms": float(v[0]), "kernel_ms": float(v[1]),
+                          "gather_exposed_ms": float(v[0] - v[1])} for r, v in enumerate(allv)]}
 
 
 def decoder_traffic(queries_per_launch: float):
@@ -593,12 +609,19 @@ def main():
     stream = torch.cuda.current_stream(dev)
     slab = SlabTimer(desc, lambda: ops.decoder_fold(desc, latents), N, stream)
     spg = args.shapes_per_group or None
+    local = []
     elapsed = run_decode_steps(slab, B, N, steps=args.steps, warmup=args.warmup, world=world,
                                group=group, device=dev, out=out, sync=torch.cuda.synchronize,
                                shapes_per_group=spg,
-                               on_timed=lambda: setattr(slab, "timed", True))
+                               on_timed=lambda: setattr(slab, "timed", True), local=local)
     slab.timed = False
     kms, qpl = slab.kernel_stats()
+    multi = None
+    if world > 1:
+        # per rank: its step time, its slab kernels' time per step (HIP events) and the rest --
+        # the part of the all-gathers the kernels did not hide -- plus the world the group saw
+        multi = rank_breakdown(local[0] / args.steps * 1e3,
+                               kms * len(slab.events) / max(1, args.steps), group, dev)
     total_q = B * N ** 3 * args.steps
     value = total_q / elapsed
     ach = FLOPS_PER_QUERY * qpl / (kms * 1e-3) / 1e12
@@ -634,6 +657,8 @@ def main():
                          "launches_per_step": len(slab.events) // max(1, args.steps)},
             "decode_b1": b1,
         }
+        if multi is not None:
+            res["multi_gpu"] = multi
     if not args.no_ddpm:
         r = bench_ddpm(args, rank, world, dev, group, gen, decoder)
         if rank == 0:

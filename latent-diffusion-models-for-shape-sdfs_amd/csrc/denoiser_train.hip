@@ -713,7 +713,8 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     };
     auto dep = [&](int c, int p, bool band) {
         Node& C = T.node[c];
-        const Node& Pn = T.node[p];
+        Node& Pn = T.node[p];
+        Pn.signal = 1;
         C.dep_ctr[C.ndep] = band ? Pn.out_band : Pn.out_all;
         C.dep_band[C.ndep] = band ? 1 : 0;
         C.dep_target[C.ndep] = band ? (unsigned)Pn.tiles_n : (unsigned)(Pn.tiles_m * Pn.tiles_n);
@@ -780,7 +781,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     memset(&pr, 0, sizeof(pr));
     pr.type = N_PREP;
     pr.tiles_m = L.Bp / 64;
-    pr.tiles_n = 1;
+    pr.tiles_n = (L.D + 63) / 64 + (L.TE + 63) / 64;     // 64-column chunks of [xt | e]
     pr.adam = -1;
     pr.sab = sc->sqrt_ab; pr.s1mab = sc->sqrt_1mab; pr.emb = w->emb_table;
     pr.B = L.B; pr.Bp = L.Bp; pr.D = L.D; pr.TE = L.TE;
@@ -1127,8 +1128,8 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
         T.n_entries);
     for (int i = 0; i < T.n_nodes; ++i) {
         const dag::Node& nd = T.node[i];
-        put("%d %s %dx%d nk %d kgp %d band %d all %d deps", i, kType[nd.type], nd.tiles_m,
-            nd.tiles_n, nd.nk, nd.kgp, nd.out_band, nd.out_all);
+        put("%d %s %dx%d nk %d kgp %d band %d all %d sig %d deps", i, kType[nd.type],
+            nd.tiles_m, nd.tiles_n, nd.nk, nd.kgp, nd.out_band, nd.out_all, nd.signal);
         for (int d = 0; d < nd.ndep; ++d)
             put(" [%d%s>=%u]", nd.dep_ctr[d], nd.dep_band[d] ? "+band" : "", nd.dep_target[d]);
         put("\n");
@@ -1140,7 +1141,8 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
 }
 
 // Diagnostics only (not in include/ldm_sdf.h): skip the compute of DAG node types (bit t: type t
-// of train_dag.h NodeType; the jobs still wait and signal) and / or the fences (bit 4).
+// of train_dag.h NodeType; the jobs still wait and signal) and / or the fences (bit 4: both,
+// bit 5: release, bit 6: acquire -- timing experiments only, results may be stale).
 extern "C" int ldm_dev_train_dag_flags(unsigned flags) {
     train_cfg().dbg = flags;
     return 0;

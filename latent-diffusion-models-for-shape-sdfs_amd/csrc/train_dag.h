@@ -39,14 +39,16 @@ enum NodeType : int { N_GEMM = 0, N_PREP = 1, N_SUM = 2, N_ADAM = 3 };
 struct Node {
     int type;
     int tiles_m, tiles_n, nk;       // GEMM: 64 x 64 tile grid, k-steps (64 deep); PREP: tiles_m
-                                    // row bands (tiles_n 1); SUM: 1 x 1; ADAM: the node's
-                                    // 64 x 64 parameter tiles
+                                    // row bands x tiles_n 64-column chunks of [xt | e]; SUM:
+                                    // 1 x 1; ADAM: the node's 64 x 64 parameter tiles
     int ndep;
     int dep_ctr[kMaxDeps];          // counter index (band dependency: + the consumer's band)
     int dep_band[kMaxDeps];
     unsigned dep_target[kMaxDeps];
     int out_band;                   // first of tiles_m band counters (-1: none)
     int out_all;                    // the all-jobs counter
+    int signal;                     // 1: a later node waits on this node's counters (release +
+                                    // count after every job); 0: nobody does, the job just ends
     int pin_eps;                    // GEMM: P_in is the launch's eps (the LOSS target)
     int kgp;                        // GEMM: 0, or the k-group period of the launch path's tile
                                     // (two accumulators alternating every kgp 64-deep k-steps)
@@ -97,7 +99,8 @@ struct LaunchArgs {
     float hy[7];
     unsigned spin_limit;    // microseconds a dependency wait may take before it gives up
     unsigned dbg;           // diagnostics (ldm_dev_train_dag_flags): bit t skips the compute of
-                            // node type t (jobs still wait and signal); bit 4: no fences
+                            // node type t (jobs still wait and signal); bit 4: no fences; bit 5: no release
+                            // fences; bit 6: no acquire fences (timing only: results may be stale)
 };
 
 // device side (train_dag.hip)

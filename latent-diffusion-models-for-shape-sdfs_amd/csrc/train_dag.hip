@@ -175,38 +175,47 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
     epi_lds_block<BM>(smem, 0, wave, lane, wr, h, r32, L, acc0, 0, n0 + wc * (BN / 2) + 0, e);
 }
 
-// ---- input preparation of one 64-row band (prep_inputs_kernel<true>'s arithmetic) -----------
-__device__ __forceinline__ void prep_job(KNode& N, int band, const float* x0, const float* eps,
-                                         const int32_t* t) {
+// ---- input preparation of one 64-row x 64-column chunk (prep_inputs_kernel<true>'s arithmetic)
+// Chunk ch of a band: columns 64 ch .. of xt (ch < ceil(D / 64)) or of e (the rest).  The rows
+// go out as they are computed (64 lanes per row: 128-B stores); the transposed copy ([c][Bp]) is
+// staged in LDS and goes out column by column, so its stores are 128-B runs too.
+__device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, const float* eps,
+                                         const int32_t* t, unsigned short* smem) {
 #pragma clang fp contract(off)
-    const int B = N.B, Bp = N.Bp, D = N.D, TE = N.TE, W = D + TE;
+    const int B = N.B, Bp = N.Bp, D = N.D, TE = N.TE;
+    const int band = job / N.tiles_n, ch = job - band * N.tiles_n;
+    const int nd = (D + 63) / 64;
+    const bool is_x = ch < nd;
+    const int c0 = (is_x ? ch : ch - nd) * 64, width = is_x ? D : TE;
     const float* sab = N.sab;
     const float* s1mab = N.s1mab;
     const float* emb = N.emb;
-    unsigned short* xt_b = N.xt_b;
-    unsigned short* xt_T = N.xt_T;
-    unsigned short* e_b = N.e_b;
-    unsigned short* e_T = N.e_T;
-    for (int i = threadIdx.x; i < 64 * W; i += 256) {
-        const int b = band * 64 + i / W, c = i - (i / W) * W;
+    unsigned short* rows_out = is_x ? N.xt_b : N.e_b;
+    unsigned short* cols_out = is_x ? N.xt_T : N.e_T;
+    unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(smem);
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int r = i >> 6, c = c0 + (i & 63), b = band * 64 + r;
+        if (c >= width) continue;
         const bool live = b < B;
         const int tb = live ? t[b] : 0;
-        if (c < D) {
-            float v = 0.f;
-            if (live) {
+        float v = 0.f;
+        if (live) {
+            if (is_x) {
                 const float a = sab[tb] * x0[(int64_t)b * D + c];
                 const float e = s1mab[tb] * eps[(int64_t)b * D + c];
                 v = a + e;
+            } else {
+                v = emb[(int64_t)tb * TE + c];
             }
-            const unsigned short q = to_bf16(v);
-            xt_b[(int64_t)b * D + c] = q;
-            xt_T[(int64_t)c * Bp + b] = q;
-        } else {
-            const int cc = c - D;
-            const unsigned short q = to_bf16(live ? emb[(int64_t)tb * TE + cc] : 0.f);
-            e_b[(int64_t)b * TE + cc] = q;
-            e_T[(int64_t)cc * Bp + b] = q;
         }
+        const unsigned short q = to_bf16(v);
+        rows_out[(int64_t)b * width + c] = q;
+        tile[r][i & 63] = q;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int cc = i >> 6, r = i & 63;
+        if (c0 + cc < width) cols_out[(int64_t)(c0 + cc) * Bp + band * 64 + r] = tile[r][cc];
     }
 }
 
@@ -305,14 +314,14 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
                 // wait for the job's inputs (the consumer side of the hand-off)
                 KNode& N = tab->node[e >> 16];
                 const int job = e & 0xffff;
-                const int band = N.type == N_GEMM ? job / N.tiles_n : job;
+                const int band = job / N.tiles_n;      // (GEMM and PREP; others have no band)
                 bool ok = true;
                 LDM_DASSERT(job < N.tiles_m * N.tiles_n && N.ndep <= kMaxDeps);
                 for (int d = 0; d < N.ndep && ok; ++d)
                     ok = spin(ctr(sync, N.dep_ctr[d] + (N.dep_band[d] ? band : 0)),
                               N.dep_target[d], status, limit);
                 if (!ok) e = -2 - e;     // skip the job (everything drains after a timeout)
-                if (!(ka->dbg & 16)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (!(ka->dbg & (16 | 64))) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if DAG_TRACE
                 tr_rdy = __builtin_amdgcn_s_memrealtime();
@@ -332,7 +341,7 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
             } else if (type == N_GEMM) {
                 gemm_job(N, job, ka->eps, smem, wave, lane);
             } else if (type == N_PREP) {
-                prep_job(N, job, ka->x0, ka->eps, ka->t);
+                prep_job(N, job, ka->x0, ka->eps, ka->t, smem);
             } else if (type == N_SUM) {
                 sum_job(tab, N, ka->loss_out, hy);
             } else {
@@ -343,30 +352,33 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
                 adamw_tile(T, hy, *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem), tl);
             }
             // the producer side of the hand-off: every wave's stores drained, one wave releases
-            // and one lane counts the job
+            // and one lane counts the job (a node no later job waits on skips both: the launch's
+            // end publishes its stores)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (wave == 0) {
-                if (!(ka->dbg & 16)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (wave == 0 && N.signal) {
+                if (!(ka->dbg & (16 | 32))) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) {
                     LDM_DASSERT(N.out_all < tab->n_counters);
                     if (N.out_band >= 0) {
-                        const int band = type == N_GEMM ? job / N.tiles_n : job;
+                        const int band = job / N.tiles_n;
                         LDM_DASSERT(N.out_band + band < tab->n_counters);
                         __hip_atomic_fetch_add(ctr(sync, N.out_band + band), 1u,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     __hip_atomic_fetch_add(ctr(sync, N.out_all), 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-#if DAG_TRACE
-                    g_dag_trace[tr_idx][0] = (uint64_t)(unsigned)e << 32 | blockIdx.x;
-                    g_dag_trace[tr_idx][1] = tr_deq;
-                    g_dag_trace[tr_idx][2] = tr_rdy;
-                    g_dag_trace[tr_idx][3] = __builtin_amdgcn_s_memrealtime();
-#endif
                 }
             }
+#if DAG_TRACE
+            if (threadIdx.x == 0) {
+                g_dag_trace[tr_idx][0] = (uint64_t)(unsigned)e << 32 | blockIdx.x;
+                g_dag_trace[tr_idx][1] = tr_deq;
+                g_dag_trace[tr_idx][2] = tr_rdy;
+                g_dag_trace[tr_idx][3] = __builtin_amdgcn_s_memrealtime();
+            }
+#endif
         }
         // (s_job is rewritten only after the barrier at the top of the next round, which every
         // wave reaches after its read above)

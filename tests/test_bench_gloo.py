@@ -46,8 +46,11 @@ def _bench_steps(rank, world):
         calls = []
         slab = _oracle_slab(N, calls) if name == "oracle" else _exact_slab(N)
         vol = torch.empty(B, N, N, N)
+        loc = []
         el = bench.run_decode_steps(slab, B, N, steps=2, warmup=1, world=world, group=None,
-                                    device=torch.device("cpu"), out=vol, shapes_per_group=spg)
+                                    device=torch.device("cpu"), out=vol, shapes_per_group=spg,
+                                    local=loc)
+        assert len(loc) == 1 and 0 < loc[0] <= el
         # the same on this rank alone (world 1): the reference volume
         ref = torch.empty(B, N, N, N)
         bench.run_decode_steps(slab, B, N, steps=1, warmup=0, world=1, group=None,
@@ -57,6 +60,12 @@ def _bench_steps(rank, world):
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         out[name] = (bool(torch.equal(vol, ref)), float(t) == float(mx), el > 0)
+    # the per-rank breakdown the bench reports at world > 1
+    br = bench.rank_breakdown(10.0 + rank, 4.0, None, torch.device("cpu"))
+    ok = (br["world_seen"] == world and br["backend"] == "gloo" and
+          [p["rank"] for p in br["per_rank"]] == list(range(world)) and
+          all(p["gather_exposed_ms"] == 6.0 + p["rank"] for p in br["per_rank"]))
+    out["breakdown"] = (ok, True, True)
     return out
 
 
