@@ -272,9 +272,10 @@ int ldm_denoiser_train_step_adamw(const ldm_denoiser_t* w, const ldm_sched_t* sc
  * bounded: ldm_denoiser_train_status reads (and clears) the status word of `saved`: 0 ok, 1 a
  * wait timed out (the step's results are garbage), 3 the table in `saved` was built for other
  * inputs (nothing computed).  ldm_train_step_config selects the form per device:
- * LDM_TRAIN_AUTO (default: the DAG whenever the configuration has one), LDM_TRAIN_LAUNCHES (the
- * launch path), LDM_TRAIN_DAG (required: LDM_ENOSYS otherwise); spin_limit: microseconds one dependency wait
- * may take before the launch gives up (0 = default, 2 s). */
+ * LDM_TRAIN_AUTO (default: the form measured faster for the configuration, DESIGN.md §5 --
+ * ldm_train_step_last_form tells which ran), LDM_TRAIN_LAUNCHES (the launch path), LDM_TRAIN_DAG
+ * (required: LDM_ENOSYS otherwise); spin_limit: microseconds one dependency wait may take before
+ * the launch gives up (0 = default, 2 s). */
 #define LDM_TRAIN_AUTO 0
 #define LDM_TRAIN_LAUNCHES 1
 #define LDM_TRAIN_DAG 2

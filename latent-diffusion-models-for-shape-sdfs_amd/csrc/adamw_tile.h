@@ -6,6 +6,7 @@
 #pragma once
 #include "ldm_internal.h"
 #include "ddpm_common.h"
+#include "wt_store.h"
 
 namespace ldm {
 
@@ -16,7 +17,8 @@ struct AdamHyper {
 
 // Tile `tl` (row-major over the tensor's 64 x 64 tiles; a 1-D tensor is one row) of tensor T:
 // each thread 4 rows x 4 consecutive columns.  TT: ldm_adamw_tensor_t in any address space.
-template <typename TT>
+// WT: write-through stores (wt_store.h).
+template <bool WT = false, typename TT>
 __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
                                            unsigned short (&sT)[64][64 + 8], int tl) {
     const int rows = T.rows, cols = T.cols;
@@ -68,21 +70,23 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         }
         if (!rin) continue;
         if (vec) {
-            *reinterpret_cast<f32x4*>(P + off[i]) = p4[i];
-            *reinterpret_cast<f32x4*>(M + off[i]) = m4[i];
-            *reinterpret_cast<f32x4*>(V + off[i]) = v4[i];
+            vst_at<WT>(P, off[i], p4[i]);
+            vst_at<WT>(M, off[i], m4[i]);
+            vst_at<WT>(V, off[i], v4[i]);
             if (T.p_bf16) {
                 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 w = {(unsigned)q[0] | ((unsigned)q[1] << 16),
                                  (unsigned)q[2] | ((unsigned)q[3] << 16)};
-                *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(T.p_bf16) + off[i]) = w;
+                vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), off[i], w);
             }
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (c0 + cq + e >= cols) continue;
-                P[off[i] + e] = p4[i][e]; M[off[i] + e] = m4[i][e]; V[off[i] + e] = v4[i][e];
-                if (T.p_bf16) reinterpret_cast<unsigned short*>(T.p_bf16)[off[i] + e] = q[e];
+                vst_at<WT>(P, off[i] + e, p4[i][e]);
+                vst_at<WT>(M, off[i] + e, m4[i][e]);
+                vst_at<WT>(V, off[i] + e, v4[i][e]);
+                if (T.p_bf16) vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), off[i] + e, q[e]);
             }
         }
     }
@@ -92,7 +96,8 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
     const int cl = tid >> 2, rb = (tid & 3) * 16;
     const int c = c0 + cl;
     if (c >= cols) return;
-    unsigned short* dst = reinterpret_cast<unsigned short*>(T.p_bf16_t) + (int64_t)c * rows;
+    unsigned short* dst = reinterpret_cast<unsigned short*>(T.p_bf16_t);   // (uniform base)
+    const int64_t cr = (int64_t)c * rows;
     if ((rows & 7) == 0 && r0 + rb + 16 <= rows) {
         u32x4 w0, w1;
 #pragma unroll
@@ -100,13 +105,13 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
             w0[e] = (unsigned)sT[cl][rb + 2 * e] | ((unsigned)sT[cl][rb + 2 * e + 1] << 16);
             w1[e] = (unsigned)sT[cl][rb + 8 + 2 * e] | ((unsigned)sT[cl][rb + 9 + 2 * e] << 16);
         }
-        *reinterpret_cast<u32x4*>(dst + r0 + rb) = w0;
-        *reinterpret_cast<u32x4*>(dst + r0 + rb + 8) = w1;
+        vst_at<WT>(dst, cr + r0 + rb, w0);
+        vst_at<WT>(dst, cr + r0 + rb + 8, w1);
     } else {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int r = r0 + rb + e;
-            if (r < rows) dst[r] = sT[cl][rb + e];
+            if (r < rows) vst_at<WT>(dst, cr + r, sT[cl][rb + e]);
         }
     }
 }

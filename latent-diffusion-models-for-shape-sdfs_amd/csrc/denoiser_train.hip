@@ -715,6 +715,10 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         Node& C = T.node[c];
         Node& Pn = T.node[p];
         Pn.signal = 1;
+        // a band hand-off pairs the same 64-row bands: both nodes are row nodes
+        if (band)
+            ok = ok && (Pn.type == N_PREP || Pn.tile == kBand) &&
+                 (C.type == N_PREP || C.tile == kBand);
         C.dep_ctr[C.ndep] = band ? Pn.out_band : Pn.out_all;
         C.dep_band[C.ndep] = band ? 1 : 0;
         C.dep_target[C.ndep] = band ? (unsigned)Pn.tiles_n : (unsigned)(Pn.tiles_m * Pn.tiles_n);
@@ -727,8 +731,11 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         memset(&nd, 0, sizeof(nd));
         nd.type = N_GEMM;
         nd.P = P;
-        nd.tiles_m = (P.M + 63) / 64;
-        nd.tiles_n = P.N / 64;
+        // row nodes (the batch rows: the chain, band hand-offs) on 64 x 64 tiles, the weight-
+        // gradient products on 128 x 128 (train_dag.hip)
+        nd.tile = P.M == L.Bp ? kBand : 128;
+        nd.tiles_m = (P.M + nd.tile - 1) / nd.tile;
+        nd.tiles_n = (P.N + nd.tile - 1) / nd.tile;
         for (int g = 0; g < P.n_seg; ++g) nd.nk += P.seg[g].K / 64;
         nd.kgp = gemm_tile_kgroup_period(gemm_tile_choice(a));
         nd.adam = -1;
@@ -771,7 +778,8 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         nd.adam = ti;
         nd.col_off = col_off;
         nd.tiles_m = (t.rows + 63) / 64;
-        nd.tiles_n = col_tiles ? col_tiles : (t.cols + 63) / 64;
+        nd.nk = col_tiles ? col_tiles : (t.cols + 63) / 64;      // the node's 64-column tiles
+        nd.tiles_n = (nd.nk + kAdamGroup - 1) / kAdamGroup;       // jobs: kAdamGroup of them
         used[ti] = true;
         return add(nd);
     };
@@ -780,12 +788,13 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     Node pr;
     memset(&pr, 0, sizeof(pr));
     pr.type = N_PREP;
-    pr.tiles_m = L.Bp / 64;
+    pr.tiles_m = (L.Bp + kBand - 1) / kBand;
     pr.tiles_n = (L.D + 63) / 64 + (L.TE + 63) / 64;     // 64-column chunks of [xt | e]
     pr.adam = -1;
     pr.sab = sc->sqrt_ab; pr.s1mab = sc->sqrt_1mab; pr.emb = w->emb_table;
     pr.B = L.B; pr.Bp = L.Bp; pr.D = L.D; pr.TE = L.TE;
     pr.xt_b = L.xt_b; pr.xt_T = L.xt_T; pr.e_b = L.e_b; pr.e_T = L.e_T;
+    ok = ok && L.D % 4 == 0 && L.TE % 4 == 0;        // prep_job's 4-column stores
     const int prep = add(pr);
     const int f1 = gemm(0, 0), f3 = gemm(0, 1);
     dep(f1, prep, true);
@@ -909,6 +918,13 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     return 0;
 }
 
+// LDM_TRAIN_AUTO's choice: the one-launch step where it measured faster than the launch path
+// (not yet at config 2's batch -- profiles/r05*/train_ab.log).
+bool dag_auto(int B) {
+    (void)B;
+    return false;
+}
+
 // The step as one launch.  Returns 1 when the configuration has no DAG form (nothing done).
 int dag_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, const float* eps,
              const int32_t* t, int B, void* saved, const ldm_denoiser_grads_t* grads,
@@ -1010,7 +1026,8 @@ extern "C" int ldm_denoiser_train_step_adamw(
     LDM_REQUIRE(cfg.form != LDM_TRAIN_DAG || side == nullptr || side == s, LDM_ENOSYS,
                 "ldm_denoiser_train_step_adamw: the one-launch step (LDM_TRAIN_DAG, required) "
                 "has no side-stream form");
-    if ((side == nullptr || side == s) && cfg.form != LDM_TRAIN_LAUNCHES) {
+    if ((side == nullptr || side == s) &&
+        (cfg.form == LDM_TRAIN_DAG || (cfg.form == LDM_TRAIN_AUTO && dag_auto(B)))) {
         float h7[7];
         adamw_hyper(lr, beta1, beta2, eps_adam, weight_decay, step, h7);
         const int r = dag_step(w, sc, x0, eps, t, B, saved, grads, loss_out, tensors, n, h7,

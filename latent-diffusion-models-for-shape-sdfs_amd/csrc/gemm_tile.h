@@ -5,6 +5,7 @@
 #pragma once
 #include "ldm_internal.h"
 #include "ddpm_common.h"
+#include "wt_store.h"
 
 #include <type_traits>
 
@@ -137,7 +138,7 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // accumulator layout, in that epilogue's order (bit-identical too).  The caller checks
 // eligibility (the block lies inside N; pointers / strides allow the vectors).
 // Block: rows rb = L.m0 + wr * (BM / 2) + i * 32 .. +32, columns nb .. nb + 32.
-template <int BM>
+template <int BM, bool WT = false>
 __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off, int wave,
                                               int lane, int wr, int h, int r32, const TileLoc& L,
                                               const f32x16& c, const int i, const int nb,
@@ -177,7 +178,7 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int b = rb + rl + 8 * p;
-            if (b < Mv) *reinterpret_cast<f32x4*>(dst + (int64_t)b * Nc + n4) = cv[p];
+            if (b < Mv) vst_at<WT>(dst, (int64_t)b * Nc + n4, cv[p]);
         }
         asm volatile("" ::: "memory");
         return;
@@ -248,14 +249,13 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
                 out[e] = live ? o : 0.f;
             }
             if (Cp && live)
-                *reinterpret_cast<f32x4*>(Cp + (int64_t)b * ldc + n4) =
-                    MODE == LDM_GEMM_DGRAD_SILU ? dh : out;
+                vst_at<WT>(Cp, (int64_t)b * ldc + n4, MODE == LDM_GEMM_DGRAD_SILU ? dh : out);
             if constexpr (MODE == LDM_GEMM_SILU || MODE == LDM_GEMM_RESID_SILU) {
-                if (Pp && live) *reinterpret_cast<f32x4*>(Pp + (int64_t)b * ldp + n4) = pre_v;
+                if (Pp && live) vst_at<WT>(Pp, (int64_t)b * ldp + n4, pre_v);
             }
             if (Cbp && b < Mr)
-                *reinterpret_cast<u32x2*>(Cbp + (int64_t)b * ldcb + n4) =
-                    u32x2{pack2_bf16(out[0], out[1]), pack2_bf16(out[2], out[3])};
+                vst_at<WT>(Cbp, (int64_t)b * ldcb + n4,
+                        u32x2{pack2_bf16(out[0], out[1]), pack2_bf16(out[2], out[3])});
             keep[p] = LS ? dd : out;
         }
         if (CbTp || csp || (LS && lpp)) {   // back to accumulator layout through the tile
@@ -286,7 +286,7 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
                                          pack2_bf16(oa[4 * g + 2], oa[4 * g + 3])};
                         const int64_t at = kt ? ((int64_t)(b / kt) * Nc + n) * kt + b % kt
                                               : (int64_t)n * ldct + b;
-                        *reinterpret_cast<u32x2*>(CbTp + at) = w;
+                        vst_at<WT>(CbTp, at, w);
                     }
                 }
             }
@@ -295,14 +295,14 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
 #pragma unroll
                 for (int v = 0; v < 16; ++v) cs += oa[v];
                 cs += __shfl_xor(cs, 32);
-                if (h == 0 && rb < Mr) csp[(int64_t)(rb / 32) * Nc + n] = cs;
+                if (h == 0 && rb < Mr) vst_at<WT>(csp, (int64_t)(rb / 32) * Nc + n, cs);
             }
             if constexpr (LS) {
                 if (lpp) {
 #pragma unroll
                     for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
                     if (lane == 0 && rb < Mr)      // the block lies inside N here
-                        lpp[(int64_t)(rb / 32) * ((Nc + 31) / 32) + nb / 32] = lsum;
+                        vst_at<WT>(lpp, (int64_t)(rb / 32) * ((Nc + 31) / 32) + nb / 32, lsum);
                 }
             }
         }

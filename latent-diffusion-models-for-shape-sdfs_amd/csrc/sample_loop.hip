@@ -536,24 +536,32 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 #ifndef SL_STAMP
 #define SL_STAMP 0
 #endif
-#if SL_STAMP
+// SL_MARKS (A/B builds only): a bit mask of the marks to keep without the rest of the stamps
+#ifndef SL_MARKS
+#define SL_MARKS 0
+#endif
+#define SL_ANY (SL_STAMP || SL_MARKS)
+#ifndef SL_PRIO
+#define SL_PRIO 0
+#endif
+#if SL_ANY
 __device__ unsigned long long g_sl_stamp[256][kRepWaves][8];
 #endif
 struct SlStamp {
     uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
     uint64_t t = 0;
     __device__ __forceinline__ void start() {
-        if (SL_STAMP) t = __builtin_amdgcn_s_memrealtime();
+        if (SL_ANY) t = __builtin_amdgcn_s_memrealtime();
     }
     __device__ __forceinline__ void mark(int k) {
-        if (SL_STAMP) {
+        if (SL_STAMP || ((SL_MARKS >> k) & 1)) {
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
             acc[k] += now - t;
             t = now;
         }
     }
     __device__ __forceinline__ void flush(int wave) {
-#if SL_STAMP
+#if SL_ANY
         if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)
             for (int i = 0; i < 6; ++i) g_sl_stamp[blockIdx.x][wave][i] = acc[i];
 #endif
@@ -650,7 +658,13 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         __syncthreads();
         // only this replica's nsh shapes are published (rows of a missing second shape are
         // computed on whatever the LDS holds and never written)
+#if SL_PRIO
+        __builtin_amdgcn_s_setprio(0);           // (A/B) polling waves yield issue to computing ones
+#endif
         const bool good = stage_tagged<NT, 2>(dst, gran, nsh * K, tg, status, a.spin_limit);
+#if SL_PRIO
+        __builtin_amdgcn_s_setprio(SL_PRIO);
+#endif
         stp.mark(0);
         if (!good) *ok = 0;
         __syncthreads();

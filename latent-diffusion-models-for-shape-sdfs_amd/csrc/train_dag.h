@@ -5,9 +5,9 @@
 // AdamW) is a DAG of NODES: the 15 grouped-GEMM problems of the launch-per-GEMM step
 // (denoiser_train.hip forward / backward, recorded, not re-derived), the input preparation, the
 // bias-gradient / loss sums (each fused with its bias's AdamW update) and the AdamW tiles of
-// every weight.  A node is a set of JOBS (64 x 64 output tiles, row bands, 64 x 64 parameter
-// tiles); a job waits on counters its producers raise:
-//   * band dependency: the producer's 64-row band counter of the consumer's own band reaches
+// every weight.  A node is a set of JOBS (kBand x kBand output tiles, kBand-row x 64-column
+// input chunks, groups of 64 x 64 parameter tiles); a job waits on counters its producers raise:
+//   * band dependency: the producer's kBand-row band counter of the consumer's own band reaches
 //     the producer's tiles per band (a layer of the residual chain needs only its band of the
 //     layer below -- no grid-wide barrier between dependent GEMMs);
 //   * all dependency: the producer's all-jobs counter reaches its job count (weight gradients
@@ -24,8 +24,10 @@ namespace ldm {
 namespace dag {
 
 constexpr int kQueues = 8;
+constexpr int kBand = 64;               // rows of a band (= a row node's GEMM tile)
 constexpr int kMaxDeps = 4;
 constexpr int kMaxNodes = 96;
+constexpr int kAdamGroup = 4;           // AdamW 64 x 64 tiles per job (one acquire for 4)
 constexpr int kCtrStride = 32;          // counters 128 bytes apart (one line each)
 // sync region (unsigned words, each on its own 128-byte line): queue heads, exit counter,
 // status, then the counters
@@ -38,9 +40,10 @@ enum NodeType : int { N_GEMM = 0, N_PREP = 1, N_SUM = 2, N_ADAM = 3 };
 
 struct Node {
     int type;
-    int tiles_m, tiles_n, nk;       // GEMM: 64 x 64 tile grid, k-steps (64 deep); PREP: tiles_m
+    int tiles_m, tiles_n, nk;       // GEMM: tile x tile grid, k-steps (64 deep); PREP: tiles_m
                                     // row bands x tiles_n 64-column chunks of [xt | e]; SUM:
-                                    // 1 x 1; ADAM: the node's 64 x 64 parameter tiles
+                                    // 1 x 1; ADAM: tiles_m 64-row tiles x tiles_n jobs of
+                                    // kAdamGroup of the node's nk 64-column tiles
     int ndep;
     int dep_ctr[kMaxDeps];          // counter index (band dependency: + the consumer's band)
     int dep_band[kMaxDeps];
@@ -50,6 +53,7 @@ struct Node {
     int signal;                     // 1: a later node waits on this node's counters (release +
                                     // count after every job); 0: nobody does, the job just ends
     int pin_eps;                    // GEMM: P_in is the launch's eps (the LOSS target)
+    int tile;                       // GEMM: 64 (row nodes: 64 x 64) or 128 (128 x 128)
     int kgp;                        // GEMM: 0, or the k-group period of the launch path's tile
                                     // (two accumulators alternating every kgp 64-deep k-steps)
     int adam;                       // SUM / ADAM: tensor index (-1: no update)
@@ -66,7 +70,7 @@ struct Node {
     const float* emb;
     int B, Bp, D, TE;
     unsigned short *xt_b, *xt_T, *e_b, *e_T;
-    ldm_gemm_prob_t P;              // GEMM (64 x 64 tiles, KB 64, LDS-transposed epilogue)
+    ldm_gemm_prob_t P;              // GEMM (KB 64, LDS-transposed epilogue)
 };
 
 struct Table {

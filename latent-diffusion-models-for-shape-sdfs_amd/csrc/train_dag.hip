@@ -4,7 +4,7 @@
 // time in per-launch fixed cost -- argument issue, ring fill, the epilogue tail of the last
 // workgroups, the gap to the next launch -- and its AdamW (HBM-bound) starts only after the
 // last GEMM (DESIGN.md §5, round-4 stamps).  Here a workgroup that finishes a tile takes the
-// next job at once, dependent layers are handed off per 64-row band instead of per launch, and
+// next job at once, dependent layers are handed off per 128-row band instead of per launch, and
 // the weight-gradient tiles, bias sums and AdamW tiles fill the CUs the residual chain leaves
 // idle.
 //
@@ -14,11 +14,13 @@
 // the sums are colsum_jobs_kernel's, the updates adamw_tile (adamw_tile.h).  So the step is
 // BIT-IDENTICAL to ldm_denoiser_train_step + ldm_adamw_multi (tests/test_gpu_train_dag.py).
 //
-// Hand-offs (MI355X guide, "Valid forms"): a job's producer drains its stores (every wave
-// s_waitcnt vmcnt(0)), joins a workgroup barrier, and ONE lane fences release at agent scope,
-// drains again (the guide's compiler-hazard fix) and adds to the node's band and all-jobs
-// counters; a consumer's lane polls the counters with relaxed agent loads, fences acquire,
-// drains, and the workgroup joins a barrier before any load of the handed-off bytes.  Every
+// Hand-offs (MI355X guide, "Valid forms"): every store of the kernel is write-through (sc1,
+// wt_store.h: no XCD L2 holds a dirty line, so a release has nothing to write back); a job's
+// producer drains its stores (every wave s_waitcnt vmcnt(0)), joins a workgroup barrier, and ONE
+// lane fences release at agent scope, drains again (the guide's compiler-hazard fix) and adds
+// to the node's band and all-jobs counters; a consumer's lane polls the counters with relaxed
+// agent loads, fences acquire, drains, and the workgroup joins a barrier before any load of the
+// handed-off bytes.  Every
 // spin is bounded: a timeout raises the status word, every later wait gives up at once, every
 // workgroup still drains its queue and exits, and the host reads the status back.
 #include "train_dag.h"
@@ -37,13 +39,46 @@ typedef const __attribute__((address_space(4))) Table KTab;
 typedef const __attribute__((address_space(4))) Node KNode;
 typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
 
-constexpr int BM = 64, BN = 64, STAGES = 3, KB = 64, NW = 4;
-constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
-constexpr int kLdsBytes = STAGES * STAGE_ELEMS * 2;            // 48 KiB: 3 workgroups per CU
-typedef TileSrc<BM, NW, KB> Src;
-constexpr int G = 2 * Src::NP;                                // DMA pieces per wave per stage
+// GEMM jobs come in two tile shapes (Node::tile), both on one workgroup per CU (4 waves, 128 KiB
+// of LDS):
+//   * 64 x 64 for the row nodes (M = the batch: the forward / backward chain and its band
+//     hand-offs): a chain layer then spreads over up to 256 CUs, as the launch path's does --
+//     the chain's latency is the step's critical path (profiles/r05l: at 128 x 128 a chain
+//     layer ran on 64 CUs at one job time each, 52 % of the workgroup-time waited for inputs);
+//     an 8-deep ring of 64-deep stages (16 KiB each) keeps 7 in flight;
+//   * 128 x 128 for the weight-gradient products (off the chain): half the operand bytes per
+//     output of a 64 x 64 tile (the operand stream is what bounds a GEMM job: ~30 GB/s per CU
+//     measured), a 4-deep ring of 32 KiB stages; each wave owns a 64 x 64 quarter.
+constexpr int KB = 64, NW = 4, kWgPerCu = 1;
+constexpr int kLdsBytes = 128 * 1024;
+template <int T>
+struct TileCfg {
+    static constexpr int BM = T, BN = T, STAGES = T == 128 ? 4 : 8;
+    static constexpr int RM = BM / 64, RN = BN / 64;           // 32 x 32 blocks per wave
+    static constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
+    typedef TileSrc<BM, NW, KB> Src;
+    static constexpr int G = 2 * Src::NP;                      // DMA pieces per wave per stage
+    static_assert(STAGES * STAGE_ELEMS * 2 <= kLdsBytes, "ring fits");
+    static_assert((STAGES - 1) * G <= 63, "vmcnt immediate");
+};
 static_assert(NW * 4096 <= kLdsBytes, "epilogue scratch fits the ring");
 static_assert(64 * (64 + 8) * 2 <= kLdsBytes, "AdamW transpose tile fits the ring");
+static_assert(kBand * 66 * 2 <= kLdsBytes, "prep transpose tile fits the ring");
+static_assert(kBand == 64, "row-node tiles are kBand x kBand");
+
+// s_waitcnt vmcnt(y * G) lgkmcnt(0) + s_barrier for a runtime y in 0..7 (vmcnt is an immediate)
+template <int G>
+__device__ __forceinline__ void wait_younger(int y) {
+    switch (y) {
+#define LDM_WY(n)                                                                              \
+    case n:                                                                                    \
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(n * G) : "memory"); \
+        break;
+        LDM_WY(7) LDM_WY(6) LDM_WY(5) LDM_WY(4) LDM_WY(3) LDM_WY(2) LDM_WY(1)
+#undef LDM_WY
+        default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+}
 
 __device__ __forceinline__ unsigned* ctr(unsigned* sync, int i) {
     return sync + (kSyncCtr0 + i) * kCtrStride;
@@ -88,13 +123,20 @@ __device__ __forceinline__ unsigned short to_bf16(float x) {
                             0xffffu);
 }
 
-// ---- GEMM tile job: 64 x 64 output tile (tm, tn) of node N's problem ------------------------
-// The launch path's ring (gemm_bf16_kernel<64, 64, 3, 1, false, false, 64>, non-persistent) and
-// epilogue.  kgp > 0 reproduces a launch that ran the problem on two k-groups (tile 24: 128-deep
-// stages, kgp = 2; 64-deep, kgp = 1): k-step i (64 deep) accumulates into acc[(i / kgp) & 1] and
-// the tile's result is acc[0] + acc[1], that launch's summation exactly.
+// ---- GEMM tile job: T x T output tile (tm, tn) of node N's problem -------------------------
+// The launch path's LDS-DMA ring and LDS-transposed epilogue (gemm_tile.h).
+// Every output element gets the launch path's arithmetic: per 64-deep k-step the same four
+// 32x32x16 MFMAs in order, so the tile shape does not change a bit; kgp > 0 reproduces a launch
+// that ran the problem on two k-groups (tile 24: 128-deep stages, kgp = 2; 64-deep, kgp = 1):
+// k-step i accumulates into acc[(i / kgp) & 1] and the result is acc[0] + acc[1], that launch's
+// summation exactly.
+template <int T>
 __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
                                          unsigned short* smem, int wave, int lane) {
+    typedef TileCfg<T> C;
+    constexpr int BM = C::BM, BN = C::BN, STAGES = C::STAGES, RM = C::RM, RN = C::RN;
+    constexpr int A_ELEMS = C::A_ELEMS, STAGE_ELEMS = C::STAGE_ELEMS, G = C::G;
+    typedef typename C::Src Src;
     KProb& P = N.P;
     const int tn_n = N.tiles_n;
     const int tm = job / tn_n, tn = job - tm * tn_n;
@@ -117,46 +159,97 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
         srcB.issue(st + A_ELEMS, wave, false);
         --seg_left;
     };
-    f32x16 acc0, acc1;
+    f32x16 acc0[RM][RN], acc1[RM][RN];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        acc0[v] = 0.f;
-        acc1[v] = 0.f;
-    }
-    auto compute = [&](const unsigned short* sa, f32x16& acc) __attribute__((always_inline)) {
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                acc0[i][j][v] = 0.f;
+                acc1[i][j][v] = 0.f;
+            }
+    // Software-pipelined k-loop: the fragments of stage j + 1 are read from LDS (into the other
+    // register set) while the MFMAs of stage j run, so the LDS reads and the matrix pipe overlap
+    // inside one wave (one wave per SIMD at 128-row bands: nothing else hides the read
+    // latency; profiles/r05k: 1.2 us per 128 x 128 k-step with reads and MFMAs serialised).
+    struct Frags {
+        u32x4 a[KB / 16][RM], b[KB / 16][RN];
+    };
+    auto read_frags = [&](int slot, Frags& f) __attribute__((always_inline)) {
+        const unsigned short* sa = smem + slot * STAGE_ELEMS;
         const unsigned short* sb = sa + A_ELEMS;
-        u32x4 af[KB / 16], bfr[KB / 16];
 #pragma unroll
         for (int s = 0; s < KB / 16; ++s) {
-            af[s] = read_frag<KB>(sa, wr * (BM / 2) + r32, 2 * s + h);
-            bfr[s] = read_frag<KB>(sb, wc * (BN / 2) + r32, 2 * s + h);
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+                f.a[s][i] = read_frag<KB>(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+                f.b[s][j] = read_frag<KB>(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
         }
-        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma = [&](const Frags& f, f32x16 (&acc)[RM][RN]) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < KB / 16; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[s]),
-                                                          __builtin_bit_cast(bf16x8, bfr[s]),
-                                                          acc, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        __builtin_bit_cast(bf16x8, f.a[s][i]), __builtin_bit_cast(bf16x8, f.b[s][j]),
+                        acc[i][j], 0, 0, 0);
+    };
+    // wait until this wave's pieces of a stage landed with `younger` later stages still in
+    // flight, and every wave's LDS reads so far completed; then the workgroup barrier
+    auto wait_stage = [&](int younger) __attribute__((always_inline)) {
+        wait_younger<G>(younger);
+    };
+    // k-step j: MFMAs of stage j from `cur`; meanwhile stage j + 1 -> `nxt`.  Before the reads:
+    // stage j + 1 landed for every wave, and every wave's reads of stage j are done (they went
+    // to registers one step earlier), so stage j + STAGES can refill stage j's slot.
+    auto kstep = [&](int j, const Frags& cur, Frags& nxt, f32x16 (&acc)[RM][RN])
+                     __attribute__((always_inline)) {
+        if (j + 1 < nk) {
+            wait_stage(min(STAGES - 2, nk - j - 2));
+            if (j + STAGES < nk) issue();
+            read_frags((j + 1) % STAGES, nxt);
+        }
+        mfma(cur, acc);
     };
     seat(0);
-    issue();
-    if (nk > 1) issue();
-    for (int it = 0; it < nk; ++it) {
-        // RAW: this wave's pieces of stage it landed (one younger stage may still fly); the
-        // barrier makes every wave's pieces visible and retires every read of stage it - 1,
-        // whose slot the issue below refills
-        if (it + 1 < nk)
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (it + 2 < nk) issue();
-        const unsigned short* st = smem + (it % STAGES) * STAGE_ELEMS;
-        if (kgp > 0 && ((it / kgp) & 1)) compute(st, acc1);
-        else compute(st, acc0);
+    for (int p = 0; p < STAGES && p < nk; ++p) issue();
+    Frags F0, F1;
+    wait_stage(min(STAGES - 1, nk - 1));
+    read_frags(0, F0);
+    // Each k-step's accumulator set and fragment set are fixed at its code position (a runtime
+    // choice between the k-group sets made the compiler copy a set between VGPRs and AGPRs every
+    // step); groups of 4 k-steps cover both k-group periods (1 and 2)
+    if (kgp == 0) {
+        for (int j = 0; j < nk; j += 2) {
+            kstep(j, F0, F1, acc0);
+            if (j + 1 < nk) kstep(j + 1, F1, F0, acc0);
+        }
+    } else if (kgp == 1) {
+        for (int j = 0; j < nk; j += 2) {
+            kstep(j, F0, F1, acc0);
+            if (j + 1 < nk) kstep(j + 1, F1, F0, acc1);
+        }
+    } else {
+        for (int j = 0; j < nk; j += 4) {
+            kstep(j, F0, F1, acc0);
+            if (j + 1 < nk) kstep(j + 1, F1, F0, acc0);
+            if (j + 2 < nk) kstep(j + 2, F0, F1, acc1);
+            if (j + 3 < nk) kstep(j + 3, F1, F0, acc1);
+        }
     }
     if (kgp > 0) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc0[v] += acc1[v];
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) acc0[i][j][v] += acc1[i][j][v];
     }
     __syncthreads();        // the epilogue's LDS tiles overwrite ring slots others may still read
     EpiArgs e;
@@ -172,13 +265,26 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
     e.ldr = P.ldr; e.ldpin = P.ldp_in; e.ldrb = P.ldrb; e.ldc = P.ldc; e.ldp = P.ldp;
     e.ldcb = P.ldcb; e.ldct = P.ldct;
     const TileLoc L = {0, m0, n0, 0};
-    epi_lds_block<BM>(smem, 0, wave, lane, wr, h, r32, L, acc0, 0, n0 + wc * (BN / 2) + 0, e);
+    // one inlined epilogue, looped over the wave's blocks (four inlined copies spilled: the
+    // launch path's note on its 128 x 128 tiles); a block past N (N a multiple of 64) is skipped
+#pragma unroll 1
+    for (int b = 0; b < RM * RN; ++b) {
+        const int i = b / RN, j = b - (b / RN) * RN;
+        const int nb = n0 + wc * (BN / 2) + j * 32;
+        if (nb >= P.N) continue;
+        f32x16 c = acc0[0][0];
+#pragma unroll
+        for (int bb = 1; bb < RM * RN; ++bb)
+            if (b == bb) c = acc0[bb / RN][bb % RN];
+        epi_lds_block<BM, true>(smem, 0, wave, lane, wr, h, r32, L, c, i, nb, e);
+    }
 }
 
-// ---- input preparation of one 64-row x 64-column chunk (prep_inputs_kernel<true>'s arithmetic)
-// Chunk ch of a band: columns 64 ch .. of xt (ch < ceil(D / 64)) or of e (the rest).  The rows
-// go out as they are computed (64 lanes per row: 128-B stores); the transposed copy ([c][Bp]) is
-// staged in LDS and goes out column by column, so its stores are 128-B runs too.
+// ---- input preparation of one kBand-row x 64-column chunk (prep_inputs_kernel<true>'s arithmetic)
+// Chunk ch of a band: columns 64 ch .. of xt (ch < ceil(D / 64)) or of e (the rest); a thread
+// takes 4 consecutive columns.  The rows go out as they are computed (8-byte write-through
+// stores, 128-B runs per 16 lanes); the transposed copy ([c][Bp]) is staged in LDS and goes out
+// 4 rows per store, 128-B runs too.  (D and TE are multiples of 4: build_dag.)
 __device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, const float* eps,
                                          const int32_t* t, unsigned short* smem) {
 #pragma clang fp contract(off)
@@ -193,29 +299,37 @@ __device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, con
     unsigned short* rows_out = is_x ? N.xt_b : N.e_b;
     unsigned short* cols_out = is_x ? N.xt_T : N.e_T;
     unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(smem);
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int r = i >> 6, c = c0 + (i & 63), b = band * 64 + r;
-        if (c >= width) continue;
+    for (int i = threadIdx.x; i < kBand * 16; i += 256) {
+        const int r = i >> 4, cl = 4 * (i & 15), c = c0 + cl, b = band * kBand + r;
+        if (c >= width || b >= Bp) continue;
         const bool live = b < B;
         const int tb = live ? t[b] : 0;
-        float v = 0.f;
-        if (live) {
-            if (is_x) {
-                const float a = sab[tb] * x0[(int64_t)b * D + c];
-                const float e = s1mab[tb] * eps[(int64_t)b * D + c];
-                v = a + e;
-            } else {
-                v = emb[(int64_t)tb * TE + c];
+        unsigned short q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float v = 0.f;
+            if (live) {
+                if (is_x) {
+                    const float a = sab[tb] * x0[(int64_t)b * D + c + u];
+                    const float e = s1mab[tb] * eps[(int64_t)b * D + c + u];
+                    v = a + e;
+                } else {
+                    v = emb[(int64_t)tb * TE + c + u];
+                }
             }
+            q[u] = to_bf16(v);
+            tile[r][cl + u] = q[u];
         }
-        const unsigned short q = to_bf16(v);
-        rows_out[(int64_t)b * width + c] = q;
-        tile[r][i & 63] = q;
+        vst_at<true>(rows_out, (int64_t)b * width + c,
+                  u32x2{(unsigned)q[0] | (unsigned)q[1] << 16, (unsigned)q[2] | (unsigned)q[3] << 16});
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int cc = i >> 6, r = i & 63;
-        if (c0 + cc < width) cols_out[(int64_t)(c0 + cc) * Bp + band * 64 + r] = tile[r][cc];
+    for (int i = threadIdx.x; i < 64 * (kBand / 4); i += 256) {
+        const int cc = i / (kBand / 4), r = 4 * (i % (kBand / 4));
+        if (c0 + cc >= width || band * kBand + r >= Bp) continue;
+        vst_at<true>(cols_out, (int64_t)(c0 + cc) * Bp + band * kBand + r,
+                  u32x2{(unsigned)tile[r][cc] | (unsigned)tile[r + 1][cc] << 16,
+                        (unsigned)tile[r + 2][cc] | (unsigned)tile[r + 3][cc] << 16});
     }
 }
 
@@ -242,15 +356,15 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
         }
         for (; r < rows; ++r) s += src[(int64_t)r * ld];
         const float g = scale * s;
-        dst[c] = g;
+        vst_at<true>(dst, c, g);
         if (ti >= 0) {
             const __attribute__((address_space(4))) ldm_adamw_tensor_t& T = tab->tensor[ti];
             float p = T.p[c], m = T.m[c], v = T.v[c];
             adamw_update(p, g, m, v, hy.decay, hy.omb1, hy.b2, hy.omb2, hy.eps, hy.step_size,
                          hy.bc2_sqrt);
-            T.p[c] = p;
-            T.m[c] = m;
-            T.v[c] = v;
+            vst_at<true>(T.p, c, p);
+            vst_at<true>(T.m, c, m);
+            vst_at<true>(T.v, c, v);
         }
     }
 }
@@ -266,7 +380,7 @@ __device__ unsigned long long g_dag_trace[kMaxEntries][4];
 __device__ unsigned long long g_dag_wg[4096][2];
 #endif
 
-__global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     __shared__ int s_job;
     __shared__ int s_last;
@@ -339,7 +453,8 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
             if ((ka->dbg >> type) & 1) {
                 // diagnostics: this node type's compute skipped
             } else if (type == N_GEMM) {
-                gemm_job(N, job, ka->eps, smem, wave, lane);
+                if (N.tile == 128) gemm_job<128>(N, job, ka->eps, smem, wave, lane);
+                else gemm_job<64>(N, job, ka->eps, smem, wave, lane);
             } else if (type == N_PREP) {
                 prep_job(N, job, ka->x0, ka->eps, ka->t, smem);
             } else if (type == N_SUM) {
@@ -347,9 +462,16 @@ __global__ __launch_bounds__(256, 3) void train_dag_kernel(LaunchArgs a) {
             } else {
                 const __attribute__((address_space(4))) ldm_adamw_tensor_t& T =
                     tab->tensor[N.adam];
-                const int tr = job / N.tiles_n, tc = job - tr * N.tiles_n;
-                const int tl = tr * ((T.cols + 63) / 64) + N.col_off + tc;
-                adamw_tile(T, hy, *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem), tl);
+                const int tr = job / N.tiles_n, tg = job - tr * N.tiles_n;
+                const int tl0 = tr * ((T.cols + 63) / 64) + N.col_off;
+                for (int k = 0; k < kAdamGroup; ++k) {
+                    const int tc = tg * kAdamGroup + k;
+                    if (tc >= N.nk) break;
+                    if (k) __syncthreads();      // the transpose tile is rewritten
+                    adamw_tile<true>(T, hy,
+                                     *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem),
+                                     tl0 + tc);
+                }
             }
             // the producer side of the hand-off: every wave's stores drained, one wave releases
             // and one lane counts the job (a node no later job waits on skips both: the launch's
