@@ -17,7 +17,7 @@ struct AdamHyper {
 
 // Tile `tl` (row-major over the tensor's 64 x 64 tiles; a 1-D tensor is one row) of tensor T:
 // each thread 4 rows x 4 consecutive columns.  TT: ldm_adamw_tensor_t in any address space.
-// WT: write-through stores (wt_store.h).
+// WT: write-through stores and an sc1 load of the gradient (wt_store.h).
 template <bool WT = false, typename TT>
 __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
                                            unsigned short (&sT)[64][64 + 8], int tl) {
@@ -43,14 +43,15 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         off[i] = (int64_t)r * cols + c0 + cq;
         if (vec) {
             p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
-            g4[i] = *reinterpret_cast<const f32x4*>(Gp + off[i]);
+            g4[i] = vld_at<WT, f32x4>(Gp, off[i]);     // (WT: the handed-off gradient, sc1)
             m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
             v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int64_t x = c0 + cq + e < cols ? off[i] + e : off[i];
-                p4[i][e] = P[x]; g4[i][e] = Gp[x]; m4[i][e] = M[x]; v4[i][e] = V[x];
+                p4[i][e] = P[x]; g4[i][e] = vld_at<WT, float>(Gp, x); m4[i][e] = M[x];
+                v4[i][e] = V[x];
             }
         }
     }

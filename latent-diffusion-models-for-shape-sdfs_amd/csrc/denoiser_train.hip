@@ -724,7 +724,9 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         C.dep_target[C.ndep] = band ? (unsigned)Pn.tiles_n : (unsigned)(Pn.tiles_m * Pn.tiles_n);
         ++C.ndep;
     };
-    auto gemm = [&](int li, int pi) -> int {
+    // row: the product's rows are the batch's (the forward / backward chain: band hand-offs,
+    // 64 x 64 tiles); otherwise a weight-gradient product (rows = features, 128 x 128 tiles)
+    auto gemm = [&](int li, int pi, bool row) -> int {
         const ldm_gemm_args_t& a = rec.launches[li];
         const ldm_gemm_prob_t& P = a.prob[pi];
         Node nd;
@@ -733,7 +735,8 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         nd.P = P;
         // row nodes (the batch rows: the chain, band hand-offs) on 64 x 64 tiles, the weight-
         // gradient products on 128 x 128 (train_dag.hip)
-        nd.tile = P.M == L.Bp ? kBand : 128;
+        nd.tile = row ? kBand : 128;
+        ok = ok && (!row || P.M == L.Bp);
         nd.tiles_m = (P.M + nd.tile - 1) / nd.tile;
         nd.tiles_n = (P.N + nd.tile - 1) / nd.tile;
         for (int g = 0; g < P.n_seg; ++g) nd.nk += P.seg[g].K / 64;
@@ -796,25 +799,25 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     pr.xt_b = L.xt_b; pr.xt_T = L.xt_T; pr.e_b = L.e_b; pr.e_T = L.e_T;
     ok = ok && L.D % 4 == 0 && L.TE % 4 == 0;        // prep_job's 4-column stores
     const int prep = add(pr);
-    const int f1 = gemm(0, 0), f3 = gemm(0, 1);
+    const int f1 = gemm(0, 0, true), f3 = gemm(0, 1, true);
     dep(f1, prep, true);
     dep(f3, prep, true);
-    const int f2 = gemm(1, 0);
+    const int f2 = gemm(1, 0, true);
     dep(f2, f1, true);
     std::vector<int> fb(nb);
     for (int k = 0; k < nb; ++k) {
-        fb[k] = gemm(2 + k, 0);
+        fb[k] = gemm(2 + k, 0, true);
         dep(fb[k], k == 0 ? f3 : fb[k - 1], true);
         dep(fb[k], f2, true);
     }
-    const int fo = gemm(2 + nb, 0);
+    const int fo = gemm(2 + nb, 0, true);
     dep(fo, fb[nb - 1], true);
-    const int dhout = gemm(base, 1);
+    const int dhout = gemm(base, 1, true);
     dep(dhout, fo, true);
     dep(sum(L.p_bout, gr->b_out, L.Bp / 32, L.D, L.D, 1.f, gr->b_out), fo, false);
     dep(sum(L.loss_part, nullptr, (L.Bp / 32) * (L.D / 32), 1, 1, 1.f / nf, nullptr), fo,
         false);
-    const int dwo = gemm(base, 0);
+    const int dwo = gemm(base, 0, false);
     dep(dwo, fo, false);
     std::vector<int> Dk(nb), dwk(nb), duk(nb);
     std::vector<bool> wdone(nb, false);
@@ -838,11 +841,11 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     for (int i = 0; i < nb; ++i) {
         const int k = nb - 1 - i;
         const int gprod = k == nb - 1 ? dhout : Dk[k + 1];      // produced g_k and p_bblk[k]
-        Dk[k] = gemm(base + 1 + i, 2);
+        Dk[k] = gemm(base + 1 + i, 2, true);
         dep(Dk[k], gprod, true);
-        dwk[k] = gemm(base + 1 + i, 0);
+        dwk[k] = gemm(base + 1 + i, 0, false);
         dep(dwk[k], gprod, false);
-        duk[k] = gemm(base + 1 + i, 1);
+        duk[k] = gemm(base + 1 + i, 1, false);
         dep(duk[k], gprod, false);
         dep(sum(L.p_bblk[k], gr->b_blk[k], L.Bp / 32, H_, H_, 1.f, gr->b_blk[k]), gprod, false);
         if (k + 1 < nb) adam_w(k + 1);
@@ -850,14 +853,14 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     }
     if (!wout_done) adam_wout();
     dep(sum(L.p_bin, gr->b_in, L.Bp / 32, H_, H_, 1.f, gr->b_in), Dk[0], false);
-    const int dt = gemm(base + 1 + nb, 0);
+    const int dt = gemm(base + 1 + nb, 0, true);
     dep(dt, nb >= 2 ? Dk[1] : dhout, true);      // the producer of g_0 (the chain covers g_k>0)
     adam_w(0);
-    const int gt = gemm(base + 2 + nb, 1);
+    const int gt = gemm(base + 2 + nb, 1, true);
     dep(gt, dt, true);
-    const int dwi = gemm(base + 3 + nb, 1);
+    const int dwi = gemm(base + 3 + nb, 1, false);
     dep(dwi, Dk[0], false);
-    const int dw2 = gemm(base + 2 + nb, 0);
+    const int dw2 = gemm(base + 2 + nb, 0, false);
     dep(dw2, dt, false);
     dep(sum(L.p_bt2, gr->b_t2, L.Bp / 32, H_, H_, 1.f, gr->b_t2), dt, false);
     for (int k = nb - 1; k >= 0; --k) {      // U_k's update: its gradient and dtemb (reads U_k^T)
@@ -867,7 +870,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
             dep(a, dt, false);
         }
     }
-    const int dw1 = gemm(base + 3 + nb, 0);
+    const int dw1 = gemm(base + 3 + nb, 0, false);
     dep(dw1, gt, false);
     dep(sum(L.p_bt1, gr->b_t1, L.Bp / 32, H_, H_, 1.f, gr->b_t1), gt, false);
     int a = adam(gr->w_in, 0, 0);
@@ -895,7 +898,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     for (int i = 0; i < T.n_nodes; ++i) {
         const Node& nd = T.node[i];
         const int jobs = nd.tiles_m * nd.tiles_n;
-        const bool rows = nd.type == N_PREP || (nd.type == N_GEMM && nd.P.M == L.Bp);
+        const bool rows = nd.type == N_PREP || (nd.type == N_GEMM && nd.tile == kBand);
         for (int j = 0; j < jobs; ++j) {
             int qq;
             if (jobs == 1) qq = rr++ % kQueues;
@@ -1158,8 +1161,8 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
 }
 
 // Diagnostics only (not in include/ldm_sdf.h): skip the compute of DAG node types (bit t: type t
-// of train_dag.h NodeType; the jobs still wait and signal) and / or the fences (bit 4: both,
-// bit 5: release, bit 6: acquire -- timing experiments only, results may be stale).
+// of train_dag.h NodeType; the jobs still wait and signal) and / or add the release / acquire
+// fences to every hand-off (bit 7, dag::kDbgFences).
 extern "C" int ldm_dev_train_dag_flags(unsigned flags) {
     train_cfg().dbg = flags;
     return 0;

@@ -69,13 +69,15 @@ struct TileSrc {
     }
     // issue the next KB-deep stage into LDS `dst` and step on; `again`: re-issue the previous
     // stage instead (a dummy that keeps every wave's vmcnt arithmetic uniform)
+    // CP: the load's cache policy (0; 16 = sc1, the DAG kernel's hand-off loads: wt_store.h)
+    template <int CP = 0>
     __device__ __forceinline__ void issue(unsigned short* dst, int wave, bool again) {
         const char* b = again ? base - 2 * KB : base;
 #pragma unroll
         for (int j = 0; j < NP; ++j)
             __builtin_amdgcn_global_load_lds(
                 (const void*)(b + voff[j]),
-                (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 512), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(dst + (wave + NW * j) * 512), 16, 0, CP);
         if (!again) base += 2 * KB;
     }
     // register staging (RS kernels): the same pieces through VGPRs, written to the same
@@ -207,12 +209,12 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
             vb[p] = u32x2{0u, 0u};
             if constexpr (X1R || X1C) {
                 if (has1)
-                    v1[p] = *reinterpret_cast<const f32x4*>(x1 + (int64_t)bb * ld1 + n4);
+                    v1[p] = vld_at<WT, f32x4>(x1, (int64_t)bb * ld1 + n4);
             }
             if constexpr (X2)
-                v2[p] = *reinterpret_cast<const f32x4*>(Pin + (int64_t)bb * ldpin + n4);
+                v2[p] = vld_at<WT, f32x4>(Pin, (int64_t)bb * ldpin + n4);
             if constexpr (XB)
-                vb[p] = *reinterpret_cast<const u32x2*>(Rbp + (int64_t)bb * ldrb + n4);
+                vb[p] = vld_at<WT, u32x2>(Rbp, (int64_t)bb * ldrb + n4);
         }
         // one row at a time from the batched operand loads: only the values the write-back
         // needs (keep) live across rows (the 128 x 128 kernels spilled with all of it live)

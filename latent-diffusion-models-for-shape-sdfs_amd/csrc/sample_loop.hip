@@ -544,6 +544,9 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 #ifndef SL_PRIO
 #define SL_PRIO 0
 #endif
+#ifndef SL_NAPS
+#define SL_NAPS 0
+#endif
 #if SL_ANY
 __device__ unsigned long long g_sl_stamp[256][kRepWaves][8];
 #endif
@@ -554,6 +557,7 @@ struct SlStamp {
         if (SL_ANY) t = __builtin_amdgcn_s_memrealtime();
     }
     __device__ __forceinline__ void mark(int k) {
+        if ((SL_NAPS >> k) & 1) __builtin_amdgcn_s_sleep(1);
         if (SL_STAMP || ((SL_MARKS >> k) & 1)) {
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
             acc[k] += now - t;

@@ -83,6 +83,7 @@ struct Table {
 };
 
 constexpr int kMaxEntries = 16384;
+constexpr unsigned kDbgFences = 128;
 inline size_t table_bytes() { return sizeof(Table) + sizeof(uint32_t) * kMaxEntries; }
 inline size_t sync_bytes(int n_counters) {
     return (size_t)(kSyncCtr0 + n_counters) * kCtrStride * sizeof(unsigned);
@@ -103,8 +104,8 @@ struct LaunchArgs {
     float hy[7];
     unsigned spin_limit;    // microseconds a dependency wait may take before it gives up
     unsigned dbg;           // diagnostics (ldm_dev_train_dag_flags): bit t skips the compute of
-                            // node type t (jobs still wait and signal); bit 4: no fences; bit 5: no release
-                            // fences; bit 6: no acquire fences (timing only: results may be stale)
+                            // node type t (jobs still wait and signal); kDbgFences: add the
+                            // agent release / acquire fences to every hand-off (A/B)
 };
 
 // device side (train_dag.hip)

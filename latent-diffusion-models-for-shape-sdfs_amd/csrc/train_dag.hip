@@ -14,14 +14,16 @@
 // the sums are colsum_jobs_kernel's, the updates adamw_tile (adamw_tile.h).  So the step is
 // BIT-IDENTICAL to ldm_denoiser_train_step + ldm_adamw_multi (tests/test_gpu_train_dag.py).
 //
-// Hand-offs (MI355X guide, "Valid forms"): every store of the kernel is write-through (sc1,
-// wt_store.h: no XCD L2 holds a dirty line, so a release has nothing to write back); a job's
-// producer drains its stores (every wave s_waitcnt vmcnt(0)), joins a workgroup barrier, and ONE
-// lane fences release at agent scope, drains again (the guide's compiler-hazard fix) and adds
-// to the node's band and all-jobs counters; a consumer's lane polls the counters with relaxed
-// agent loads, fences acquire, drains, and the workgroup joins a barrier before any load of the
-// handed-off bytes.  Every
-// spin is bounded: a timeout raises the status word, every later wait gives up at once, every
+// Hand-offs (MI355X guide, inter-workgroup visibility, "Valid forms" table row 1: one workgroup
+// per CU, hipMalloc memory): EVERY store of a handed-off byte is write-through (sc1, wt_store.h)
+// and EVERY load of one is an sc1 load -- the GEMM operands' LDS-DMA, the epilogue operands, the
+// bias sums' partials, AdamW's gradients -- so no release or acquire fence is needed.  A job's
+// storing waves drain (s_waitcnt vmcnt(0)) and join a workgroup barrier; then ONE lane adds to
+// the node's band and all-jobs counters (agent-scope atomics).  A consumer's wave 0 polls the
+// counters (relaxed agent loads), drains, and the workgroup joins a barrier before any load of
+// the handed-off bytes.  (The release/acquire form stays selectable for A/B:
+// ldm_dev_train_dag_flags bit 7; it cost ~95 us per step, profiles/r05m.)  Every spin is
+// bounded: a timeout raises the status word, every later wait gives up at once, every
 // workgroup still drains its queue and exits, and the host reads the status back.
 #include "train_dag.h"
 #include "gemm_tile.h"
@@ -155,8 +157,8 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
         if (seg_left == 0) seat(++seg);
         unsigned short* st = smem + (qi % STAGES) * STAGE_ELEMS;
         ++qi;
-        srcA.issue(st, wave, false);
-        srcB.issue(st + A_ELEMS, wave, false);
+        srcA.template issue<16>(st, wave, false);           // sc1 operand loads (hand-offs)
+        srcB.template issue<16>(st + A_ELEMS, wave, false);
         --seg_left;
     };
     f32x16 acc0[RM][RN], acc1[RM][RN];
@@ -344,17 +346,17 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
     float* dst = N.dst ? N.dst : loss_out;
     const int ti = N.adam;
     for (int c = threadIdx.x; c < len; c += 256) {
-        const float* src = N.src + c;
+        const float* src = N.src;                // (uniform base for the sc1 loads)
         float s = 0.f;
         int r = 0;
         for (; r + 8 <= rows; r += 8) {
             float v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(r + u) * ld];
+            for (int u = 0; u < 8; ++u) v[u] = vld_at<true, float>(src, (int64_t)(r + u) * ld + c);
 #pragma unroll
             for (int u = 0; u < 8; ++u) s += v[u];
         }
-        for (; r < rows; ++r) s += src[(int64_t)r * ld];
+        for (; r < rows; ++r) s += vld_at<true, float>(src, (int64_t)r * ld + c);
         const float g = scale * s;
         vst_at<true>(dst, c, g);
         if (ti >= 0) {
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) 
                     ok = spin(ctr(sync, N.dep_ctr[d] + (N.dep_band[d] ? band : 0)),
                               N.dep_target[d], status, limit);
                 if (!ok) e = -2 - e;     // skip the job (everything drains after a timeout)
-                if (!(ka->dbg & (16 | 64))) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (ka->dbg & kDbgFences) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if DAG_TRACE
                 tr_rdy = __builtin_amdgcn_s_memrealtime();
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (wave == 0 && N.signal) {
-                if (!(ka->dbg & (16 | 32))) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (ka->dbg & kDbgFences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) {
                     LDM_DASSERT(N.out_all < tab->n_counters);
