@@ -18,13 +18,14 @@ struct AdamHyper {
 // Tile `tl` (row-major over the tensor's 64 x 64 tiles; a 1-D tensor is one row) of tensor T:
 // each thread 4 rows x 4 consecutive columns.  TT: ldm_adamw_tensor_t in any address space.
 // WT: write-through stores and an sc1 load of the gradient (wt_store.h).
+// tid: the thread's index among the tile's 256 (a 512-thread caller runs two tiles at once).
 template <bool WT = false, typename TT>
 __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
-                                           unsigned short (&sT)[64][64 + 8], int tl) {
+                                           unsigned short (&sT)[64][64 + 8], int tl,
+                                           int tid = threadIdx.x) {
     const int rows = T.rows, cols = T.cols;
     const int tcn = (cols + 63) / 64;
     const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
-    const int tid = threadIdx.x;
     const int cq = (tid & 15) * 4;
     const float decay = hy.decay, omb1 = hy.omb1, b2 = hy.b2, omb2 = hy.omb2, eps = hy.eps,
                 step_size = hy.step_size, bc2_sqrt = hy.bc2_sqrt;

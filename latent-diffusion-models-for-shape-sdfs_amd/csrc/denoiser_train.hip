@@ -716,9 +716,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         Node& Pn = T.node[p];
         Pn.signal = 1;
         // a band hand-off pairs the same 64-row bands: both nodes are row nodes
-        if (band)
-            ok = ok && (Pn.type == N_PREP || Pn.tile == kBand) &&
-                 (C.type == N_PREP || C.tile == kBand);
+        if (band) ok = ok && (Pn.type == N_PREP || Pn.row) && (C.type == N_PREP || C.row);
         C.dep_ctr[C.ndep] = band ? Pn.out_band : Pn.out_all;
         C.dep_band[C.ndep] = band ? 1 : 0;
         C.dep_target[C.ndep] = band ? (unsigned)Pn.tiles_n : (unsigned)(Pn.tiles_m * Pn.tiles_n);
@@ -733,14 +731,16 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         memset(&nd, 0, sizeof(nd));
         nd.type = N_GEMM;
         nd.P = P;
-        // row nodes (the batch rows: the chain, band hand-offs) on 64 x 64 tiles, the weight-
-        // gradient products on 128 x 128 (train_dag.hip)
-        nd.tile = row ? kBand : 128;
+        // row nodes: the batch's rows (the chain, band hand-offs); the tile kind: the launch
+        // tile's two k-groups -> 64 x 64 in two groups, else 64 x 128 (row) or 128 x 128 (the
+        // weight-gradient products) -- train_dag.hip TileCfg
+        nd.row = row ? 1 : 0;
         ok = ok && (!row || P.M == L.Bp);
-        nd.tiles_m = (P.M + nd.tile - 1) / nd.tile;
-        nd.tiles_n = (P.N + nd.tile - 1) / nd.tile;
         for (int g = 0; g < P.n_seg; ++g) nd.nk += P.seg[g].K / 64;
         nd.kgp = gemm_tile_kgroup_period(gemm_tile_choice(a));
+        nd.tile = nd.kgp > 0 ? TILE_K2 : row ? TILE_ROW : TILE_W;
+        nd.tiles_m = (P.M + tile_rows(nd.tile) - 1) / tile_rows(nd.tile);
+        nd.tiles_n = (P.N + tile_cols(nd.tile) - 1) / tile_cols(nd.tile);
         nd.adam = -1;
         if (P.P_in == kEps) {
             nd.pin_eps = 1;
@@ -792,6 +792,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     memset(&pr, 0, sizeof(pr));
     pr.type = N_PREP;
     pr.tiles_m = (L.Bp + kBand - 1) / kBand;
+    pr.row = 1;
     pr.tiles_n = (L.D + 63) / 64 + (L.TE + 63) / 64;     // 64-column chunks of [xt | e]
     pr.adam = -1;
     pr.sab = sc->sqrt_ab; pr.s1mab = sc->sqrt_1mab; pr.emb = w->emb_table;
@@ -898,7 +899,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     for (int i = 0; i < T.n_nodes; ++i) {
         const Node& nd = T.node[i];
         const int jobs = nd.tiles_m * nd.tiles_n;
-        const bool rows = nd.type == N_PREP || (nd.type == N_GEMM && nd.tile == kBand);
+        const bool rows = nd.type == N_PREP || (nd.type == N_GEMM && nd.row);
         for (int j = 0; j < jobs; ++j) {
             int qq;
             if (jobs == 1) qq = rr++ % kQueues;

@@ -528,13 +528,20 @@ __device__ __forceinline__ bool stage_tagged(float* xs, const u64* G, int n, uns
 
 constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per wave
 
-// Diagnostic build only (-DSL_STAMP=1, scripts/stamp_sampler.py): every wave of the replica loop
-// keeps per-phase sums of s_memrealtime ticks (100 MHz) in registers over all its layers --
-// 0 own granules landed, 1 the workgroup's staging barrier (the slowest wave's granules), 2 the
-// row dot products, 3 the reduce-scatter, 4 epilogue + publish -- and writes them at its end
-// (g_sl_stamp[workgroup][wave]); slot 5 counts the layers.
+// Phase stamps (scripts/stamp_sampler.py reads them through ldm_dev_sample_stamps): every wave
+// of the replica loop keeps per-phase sums of s_memrealtime ticks (100 MHz) in registers over
+// all its layers -- 0 own granules landed, 1 the workgroup's staging barrier (the slowest wave's
+// granules), 2 the row dot products, 3 the reduce-scatter, 4 epilogue + publish -- and writes
+// them at its end (g_sl_stamp[workgroup][wave]); slot 5 counts the layers.
+// ON in the product build (round 5): the loop built WITH its stamps ran 86.5-88.2k steps/s at
+// B = 8 against 72.0-74.4k without, in four runs on three boxes (profiles/r05j, r05k, r05o:
+// the stamped sample_loop.o linked with the product's other objects, libldm_slstamp, is the
+// fast one; the marks alone without the layer counter, SL_MARKS = 31, are not).  The codegen
+// differs in the loop's index arithmetic (the stamped build does it in SALU, s_mul_i32 x 11,
+// where the other uses VALU v_mul_lo_u32 / v_mad); the stamps themselves cost a few SALU
+// instructions per layer.  -DSL_STAMP=0 builds the loop without them.
 #ifndef SL_STAMP
-#define SL_STAMP 0
+#define SL_STAMP 1
 #endif
 // SL_MARKS (A/B builds only): a bit mask of the marks to keep without the rest of the stamps
 #ifndef SL_MARKS

@@ -24,7 +24,13 @@ namespace ldm {
 namespace dag {
 
 constexpr int kQueues = 8;
-constexpr int kBand = 64;               // rows of a band (= a row node's GEMM tile)
+constexpr int kBand = 64;               // rows of a band (= a row node's GEMM tile rows)
+constexpr int kThreads = 512;           // the kernel's workgroup: 8 waves, one per CU
+// GEMM job configurations (train_dag.hip TileCfg): tile rows x cols
+enum TileKind : int { TILE_K2 = 0 /* 64 x 64, two k-groups */, TILE_ROW = 1 /* 64 x 128 */,
+                      TILE_W = 2 /* 128 x 128 */ };
+inline int tile_rows(int kind) { return kind == TILE_W ? 128 : 64; }
+inline int tile_cols(int kind) { return kind == TILE_K2 ? 64 : 128; }
 constexpr int kMaxDeps = 4;
 constexpr int kMaxNodes = 96;
 constexpr int kAdamGroup = 4;           // AdamW 64 x 64 tiles per job (one acquire for 4)
@@ -53,7 +59,8 @@ struct Node {
     int signal;                     // 1: a later node waits on this node's counters (release +
                                     // count after every job); 0: nobody does, the job just ends
     int pin_eps;                    // GEMM: P_in is the launch's eps (the LOSS target)
-    int tile;                       // GEMM: 64 (row nodes: 64 x 64) or 128 (128 x 128)
+    int tile;                       // GEMM: TileKind
+    int row;                        // GEMM / PREP: rows are the batch's (64-row band counters)
     int kgp;                        // GEMM: 0, or the k-group period of the launch path's tile
                                     // (two accumulators alternating every kgp 64-deep k-steps)
     int adam;                       // SUM / ADAM: tensor index (-1: no update)

@@ -41,32 +41,42 @@ typedef const __attribute__((address_space(4))) Table KTab;
 typedef const __attribute__((address_space(4))) Node KNode;
 typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
 
-// GEMM jobs come in two tile shapes (Node::tile), both on one workgroup per CU (4 waves, 128 KiB
-// of LDS):
-//   * 64 x 64 for the row nodes (M = the batch: the forward / backward chain and its band
-//     hand-offs): a chain layer then spreads over up to 256 CUs, as the launch path's does --
-//     the chain's latency is the step's critical path (profiles/r05l: at 128 x 128 a chain
-//     layer ran on 64 CUs at one job time each, 52 % of the workgroup-time waited for inputs);
-//     an 8-deep ring of 64-deep stages (16 KiB each) keeps 7 in flight;
-//   * 128 x 128 for the weight-gradient products (off the chain): half the operand bytes per
-//     output of a 64 x 64 tile (the operand stream is what bounds a GEMM job: ~30 GB/s per CU
-//     measured), a 4-deep ring of 32 KiB stages; each wave owns a 64 x 64 quarter.
-constexpr int KB = 64, NW = 4, kWgPerCu = 1;
+// One workgroup of kThreads (8 waves) per CU, 128 KiB of LDS.  GEMM jobs come in three
+// configurations (Node::tile, train_dag.h), each on an LDS-DMA ring of 64-deep stages:
+//   * TILE_K2: 64 x 64 in two k-groups of 4 waves (the launch path's two-k-group tile, for the
+//     nodes whose launch tile summed two k-groups: k-group period kgp 1 or 2); the groups work
+//     on different stages at once and group 1's sum is added to group 0's at the end;
+//   * TILE_ROW: 64 x 128 (two 64-wide column halves), the other row nodes (batch rows: the
+//     chain, band hand-offs);
+//   * TILE_W: 128 x 128 (each wave 64 x 32), the weight-gradient products (half the operand
+//     bytes per output of 64 x 64).
+// Why 8 waves: a 4-wave workgroup streamed its operands at ~27-30 GB/s per CU, the launch
+// path's 8-wave tile at ~47 and 12 waves per CU at ~70 (profiles/r05n): the per-CU operand
+// stream scales with the waves issuing it, and fence-free hand-offs need one workgroup per CU.
+constexpr int KB = 64, NW = kThreads / 64, kWgPerCu = 1;
 constexpr int kLdsBytes = 128 * 1024;
-template <int T>
+template <int CFG>
 struct TileCfg {
-    static constexpr int BM = T, BN = T, STAGES = T == 128 ? 4 : 8;
-    static constexpr int RM = BM / 64, RN = BN / 64;           // 32 x 32 blocks per wave
+    static constexpr int BM = CFG == TILE_W ? 128 : 64;
+    static constexpr int BN = CFG == TILE_K2 ? 64 : 128;
+    static constexpr int KG = CFG == TILE_K2 ? 2 : 1;          // k-groups
+    static constexpr int WR = 2, WC = NW / KG / WR;             // waves per group: WR x WC
+    static constexpr int RM = BM / WR / 32, RN = BN / WC / 32;  // 32 x 32 blocks per wave
+    static constexpr int STAGES = CFG == TILE_W ? 4 : CFG == TILE_ROW ? 5 : 8;
+    static constexpr bool PIPE = false;        // double-buffered fragments (KG = 1 only)
     static constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
-    typedef TileSrc<BM, NW, KB> Src;
-    static constexpr int G = 2 * Src::NP;                      // DMA pieces per wave per stage
+    typedef TileSrc<BM, NW, KB> SrcA;
+    typedef TileSrc<BN, NW, KB> SrcB;
+    static constexpr int G = SrcA::NP + SrcB::NP;               // DMA pieces per wave per stage
     static_assert(STAGES * STAGE_ELEMS * 2 <= kLdsBytes, "ring fits");
     static_assert((STAGES - 1) * G <= 63, "vmcnt immediate");
+    static_assert(RM >= 1 && RN >= 1 && WC >= 1, "wave grid");
 };
 static_assert(NW * 4096 <= kLdsBytes, "epilogue scratch fits the ring");
-static_assert(64 * (64 + 8) * 2 <= kLdsBytes, "AdamW transpose tile fits the ring");
+static_assert(2 * 64 * (64 + 8) * 2 <= kLdsBytes, "two AdamW transpose tiles fit the ring");
+static_assert(kAdamGroup % 2 == 0 && kThreads == 512, "AdamW jobs: two tiles per step");
 static_assert(kBand * 66 * 2 <= kLdsBytes, "prep transpose tile fits the ring");
-static_assert(kBand == 64, "row-node tiles are kBand x kBand");
+static_assert(kBand == 64, "row-node tiles are kBand rows");
 
 // s_waitcnt vmcnt(y * G) lgkmcnt(0) + s_barrier for a runtime y in 0..7 (vmcnt is an immediate)
 template <int G>
@@ -125,27 +135,29 @@ __device__ __forceinline__ unsigned short to_bf16(float x) {
                             0xffffu);
 }
 
-// ---- GEMM tile job: T x T output tile (tm, tn) of node N's problem -------------------------
-// The launch path's LDS-DMA ring and LDS-transposed epilogue (gemm_tile.h).
-// Every output element gets the launch path's arithmetic: per 64-deep k-step the same four
-// 32x32x16 MFMAs in order, so the tile shape does not change a bit; kgp > 0 reproduces a launch
-// that ran the problem on two k-groups (tile 24: 128-deep stages, kgp = 2; 64-deep, kgp = 1):
-// k-step i accumulates into acc[(i / kgp) & 1] and the result is acc[0] + acc[1], that launch's
+// ---- GEMM tile job: tile (tm, tn) of node N's problem in configuration CFG ------------------
+// The launch path's LDS-DMA ring and LDS-transposed epilogue (gemm_tile.h).  Every output
+// element gets the launch path's arithmetic: per 64-deep k-step the same four 32x32x16 MFMAs in
+// order, so the tile shape does not change a bit; kgp > 0 reproduces a launch that ran the
+// problem on two k-groups (tile 24: 128-deep stages, kgp = 2; 64-deep, kgp = 1): k-step i
+// belongs to group (i / kgp) & 1 and the result is group 0's sum + group 1's, that launch's
 // summation exactly.
-template <int T>
+template <int CFG>
 __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
                                          unsigned short* smem, int wave, int lane) {
-    typedef TileCfg<T> C;
+    typedef TileCfg<CFG> C;
     constexpr int BM = C::BM, BN = C::BN, STAGES = C::STAGES, RM = C::RM, RN = C::RN;
-    constexpr int A_ELEMS = C::A_ELEMS, STAGE_ELEMS = C::STAGE_ELEMS, G = C::G;
-    typedef typename C::Src Src;
+    constexpr int KG = C::KG, WC = C::WC, A_ELEMS = C::A_ELEMS, STAGE_ELEMS = C::STAGE_ELEMS;
+    constexpr int G = C::G;
     KProb& P = N.P;
     const int tn_n = N.tiles_n;
     const int tm = job / tn_n, tn = job - tm * tn_n;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int wr = wave >> 1, wc = wave & 1, r32 = lane & 31, h = lane >> 5;
+    const int grp = wave / (NW / KG), wl = wave % (NW / KG);   // k-group, wave in the group
+    const int wr = wl / WC, wc = wl % WC, r32 = lane & 31, h = lane >> 5;
     const int nk = N.nk, kgp = N.kgp;
-    Src srcA, srcB;
+    typename C::SrcA srcA;
+    typename C::SrcB srcB;
     int seg = 0, seg_left = 0, qi = 0;
     auto seat = [&](int sg) {
         const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[sg];
@@ -161,20 +173,13 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
         srcB.template issue<16>(st + A_ELEMS, wave, false);
         --seg_left;
     };
-    f32x16 acc0[RM][RN], acc1[RM][RN];
+    f32x16 acc[RM][RN];
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                acc0[i][j][v] = 0.f;
-                acc1[i][j][v] = 0.f;
-            }
-    // Software-pipelined k-loop: the fragments of stage j + 1 are read from LDS (into the other
-    // register set) while the MFMAs of stage j run, so the LDS reads and the matrix pipe overlap
-    // inside one wave (one wave per SIMD at 128-row bands: nothing else hides the read
-    // latency; profiles/r05k: 1.2 us per 128 x 128 k-step with reads and MFMAs serialised).
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
     struct Frags {
         u32x4 a[KB / 16][RM], b[KB / 16][RN];
     };
@@ -188,10 +193,10 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
                 f.a[s][i] = read_frag<KB>(sa, wr * (BM / 2) + i * 32 + r32, 2 * s + h);
 #pragma unroll
             for (int j = 0; j < RN; ++j)
-                f.b[s][j] = read_frag<KB>(sb, wc * (BN / 2) + j * 32 + r32, 2 * s + h);
+                f.b[s][j] = read_frag<KB>(sb, wc * (BN / WC) + j * 32 + r32, 2 * s + h);
         }
     };
-    auto mfma = [&](const Frags& f, f32x16 (&acc)[RM][RN]) __attribute__((always_inline)) {
+    auto mfma = [&](const Frags& f) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < KB / 16; ++s)
 #pragma unroll
@@ -202,58 +207,77 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
                         __builtin_bit_cast(bf16x8, f.a[s][i]), __builtin_bit_cast(bf16x8, f.b[s][j]),
                         acc[i][j], 0, 0, 0);
     };
-    // wait until this wave's pieces of a stage landed with `younger` later stages still in
-    // flight, and every wave's LDS reads so far completed; then the workgroup barrier
-    auto wait_stage = [&](int younger) __attribute__((always_inline)) {
-        wait_younger<G>(younger);
-    };
-    // k-step j: MFMAs of stage j from `cur`; meanwhile stage j + 1 -> `nxt`.  Before the reads:
-    // stage j + 1 landed for every wave, and every wave's reads of stage j are done (they went
-    // to registers one step earlier), so stage j + STAGES can refill stage j's slot.
-    auto kstep = [&](int j, const Frags& cur, Frags& nxt, f32x16 (&acc)[RM][RN])
-                     __attribute__((always_inline)) {
-        if (j + 1 < nk) {
-            wait_stage(min(STAGES - 2, nk - j - 2));
-            if (j + STAGES < nk) issue();
-            read_frags((j + 1) % STAGES, nxt);
-        }
-        mfma(cur, acc);
-    };
     seat(0);
     for (int p = 0; p < STAGES && p < nk; ++p) issue();
-    Frags F0, F1;
-    wait_stage(min(STAGES - 1, nk - 1));
-    read_frags(0, F0);
-    // Each k-step's accumulator set and fragment set are fixed at its code position (a runtime
-    // choice between the k-group sets made the compiler copy a set between VGPRs and AGPRs every
-    // step); groups of 4 k-steps cover both k-group periods (1 and 2)
-    if (kgp == 0) {
-        for (int j = 0; j < nk; j += 2) {
-            kstep(j, F0, F1, acc0);
-            if (j + 1 < nk) kstep(j + 1, F1, F0, acc0);
+    if constexpr (KG == 1 && !C::PIPE) {
+        // one fragment set: the workgroup's two waves per SIMD hide each other's LDS reads
+        // stage j landed (stages issued: STAGES, then one per step from step 1, refilling the
+        // slot of stage j - 1, whose reads every wave finished before this barrier)
+        for (int j = 0; j < nk; ++j) {
+            wait_younger<G>(j == 0 ? min(STAGES - 1, nk - 1) : min(STAGES - 2, nk - 1 - j));
+            Frags f;
+            read_frags(j % STAGES, f);
+            if (j > 0 && j - 1 + STAGES < nk) issue();
+            mfma(f);
         }
-    } else if (kgp == 1) {
+    } else if constexpr (KG == 1) {
+        // Software-pipelined: stage j + 1's fragments are read from LDS (into the other register
+        // set) while stage j's MFMAs run.  Before the reads: stage j + 1 landed for every wave
+        // and every wave's reads of stage j are done (they went to registers one step earlier),
+        // so stage j + STAGES can refill stage j's slot.
+        auto kstep = [&](int j, const Frags& cur, Frags& nxt) __attribute__((always_inline)) {
+            if (j + 1 < nk) {
+                wait_younger<G>(min(STAGES - 2, nk - j - 2));
+                if (j + STAGES < nk) issue();
+                read_frags((j + 1) % STAGES, nxt);
+            }
+            mfma(cur);
+        };
+        Frags F0, F1;
+        wait_younger<G>(min(STAGES - 1, nk - 1));
+        read_frags(0, F0);
         for (int j = 0; j < nk; j += 2) {
-            kstep(j, F0, F1, acc0);
-            if (j + 1 < nk) kstep(j + 1, F1, F0, acc1);
+            kstep(j, F0, F1);
+            if (j + 1 < nk) kstep(j + 1, F1, F0);
         }
     } else {
-        for (int j = 0; j < nk; j += 4) {
-            kstep(j, F0, F1, acc0);
-            if (j + 1 < nk) kstep(j + 1, F1, F0, acc0);
-            if (j + 2 < nk) kstep(j + 2, F0, F1, acc1);
-            if (j + 3 < nk) kstep(j + 3, F1, F0, acc1);
+        // Two k-groups: per super-step of 2 kgp stages, group g takes stages s0 + g kgp + u
+        // (u < kgp) -- the two groups read and multiply different stages at once.  The next
+        // stages refill the slots of the previous super-step (all its reads done: the barrier).
+        for (int s0 = 0; s0 < nk; s0 += 2 * kgp) {
+            wait_younger<G>(qi - min(nk, s0 + 2 * kgp));
+            while (qi < nk && qi < s0 + STAGES) issue();
+            for (int u = 0; u < kgp; ++u) {
+                const int q = s0 + grp * kgp + u;
+                if (q < nk) {
+                    Frags f;
+                    read_frags(q % STAGES, f);
+                    mfma(f);
+                }
+            }
         }
-    }
-    if (kgp > 0) {
+        // group 1's sums -> LDS (past the epilogue scratch), group 0 adds them: acc0 + acc1
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        float* red = reinterpret_cast<float*>(smem) + NW * 1024;
+        const int slot = wl * (RM * RN * 16 * 64) + lane;
+        if (grp == 1) {
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) red[slot + ((i * RN + j) * 16 + v) * 64] = acc[i][j][v];
+        }
+        __syncthreads();
+        if (grp == 1) return;      // (every later barrier of the job is inside this guard's peers)
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
             for (int j = 0; j < RN; ++j)
 #pragma unroll
-                for (int v = 0; v < 16; ++v) acc0[i][j][v] += acc1[i][j][v];
+                for (int v = 0; v < 16; ++v) acc[i][j][v] += red[slot + ((i * RN + j) * 16 + v) * 64];
     }
-    __syncthreads();        // the epilogue's LDS tiles overwrite ring slots others may still read
+    if constexpr (KG == 1) __syncthreads();   // the epilogue overwrites ring slots others read
     EpiArgs e;
     e.mode = P.mode; e.Mv = P.M_valid; e.Mr = P.M; e.Nc = P.N; e.ksp = 1; e.kt = P.ct_blk;
     e.scale = P.scale;
@@ -267,18 +291,18 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
     e.ldr = P.ldr; e.ldpin = P.ldp_in; e.ldrb = P.ldrb; e.ldc = P.ldc; e.ldp = P.ldp;
     e.ldcb = P.ldcb; e.ldct = P.ldct;
     const TileLoc L = {0, m0, n0, 0};
-    // one inlined epilogue, looped over the wave's blocks (four inlined copies spilled: the
-    // launch path's note on its 128 x 128 tiles); a block past N (N a multiple of 64) is skipped
+    // one inlined epilogue, looped over the wave's blocks (inlined per block it spilled); a
+    // block past N (N a multiple of 64) is skipped
 #pragma unroll 1
     for (int b = 0; b < RM * RN; ++b) {
         const int i = b / RN, j = b - (b / RN) * RN;
-        const int nb = n0 + wc * (BN / 2) + j * 32;
+        const int nb = n0 + wc * (BN / WC) + j * 32;
         if (nb >= P.N) continue;
-        f32x16 c = acc0[0][0];
+        f32x16 c = acc[0][0];
 #pragma unroll
         for (int bb = 1; bb < RM * RN; ++bb)
-            if (b == bb) c = acc0[bb / RN][bb % RN];
-        epi_lds_block<BM, true>(smem, 0, wave, lane, wr, h, r32, L, c, i, nb, e);
+            if (b == bb) c = acc[bb / RN][bb % RN];
+        epi_lds_block<BM, true>(smem, 0, wl, lane, wr, h, r32, L, c, i, nb, e);
     }
 }
 
@@ -301,7 +325,7 @@ __device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, con
     unsigned short* rows_out = is_x ? N.xt_b : N.e_b;
     unsigned short* cols_out = is_x ? N.xt_T : N.e_T;
     unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(smem);
-    for (int i = threadIdx.x; i < kBand * 16; i += 256) {
+    for (int i = threadIdx.x; i < kBand * 16; i += kThreads) {
         const int r = i >> 4, cl = 4 * (i & 15), c = c0 + cl, b = band * kBand + r;
         if (c >= width || b >= Bp) continue;
         const bool live = b < B;
@@ -326,7 +350,7 @@ __device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, con
                   u32x2{(unsigned)q[0] | (unsigned)q[1] << 16, (unsigned)q[2] | (unsigned)q[3] << 16});
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 64 * (kBand / 4); i += 256) {
+    for (int i = threadIdx.x; i < 64 * (kBand / 4); i += kThreads) {
         const int cc = i / (kBand / 4), r = 4 * (i % (kBand / 4));
         if (c0 + cc >= width || band * kBand + r >= Bp) continue;
         vst_at<true>(cols_out, (int64_t)(c0 + cc) * Bp + band * kBand + r,
@@ -345,7 +369,7 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
     const float scale = N.scale;
     float* dst = N.dst ? N.dst : loss_out;
     const int ti = N.adam;
-    for (int c = threadIdx.x; c < len; c += 256) {
+    for (int c = threadIdx.x; c < len; c += kThreads) {
         const float* src = N.src;                // (uniform base for the sc1 loads)
         float s = 0.f;
         int r = 0;
@@ -382,7 +406,7 @@ __device__ unsigned long long g_dag_trace[kMaxEntries][4];
 __device__ unsigned long long g_dag_wg[4096][2];
 #endif
 
-__global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
     __shared__ int s_job;
     __shared__ int s_last;
@@ -455,8 +479,9 @@ __global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) 
             if ((ka->dbg >> type) & 1) {
                 // diagnostics: this node type's compute skipped
             } else if (type == N_GEMM) {
-                if (N.tile == 128) gemm_job<128>(N, job, ka->eps, smem, wave, lane);
-                else gemm_job<64>(N, job, ka->eps, smem, wave, lane);
+                if (N.tile == TILE_W) gemm_job<TILE_W>(N, job, ka->eps, smem, wave, lane);
+                else if (N.tile == TILE_ROW) gemm_job<TILE_ROW>(N, job, ka->eps, smem, wave, lane);
+                else gemm_job<TILE_K2>(N, job, ka->eps, smem, wave, lane);
             } else if (type == N_PREP) {
                 prep_job(N, job, ka->x0, ka->eps, ka->t, smem);
             } else if (type == N_SUM) {
@@ -464,15 +489,18 @@ __global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) 
             } else {
                 const __attribute__((address_space(4))) ldm_adamw_tensor_t& T =
                     tab->tensor[N.adam];
+                // two 64 x 64 tiles at a time, one per 256-thread half, each with its own
+                // transpose tile; a half without a tile still meets the tile's barrier
                 const int tr = job / N.tiles_n, tg = job - tr * N.tiles_n;
                 const int tl0 = tr * ((T.cols + 63) / 64) + N.col_off;
-                for (int k = 0; k < kAdamGroup; ++k) {
-                    const int tc = tg * kAdamGroup + k;
-                    if (tc >= N.nk) break;
-                    if (k) __syncthreads();      // the transpose tile is rewritten
-                    adamw_tile<true>(T, hy,
-                                     *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem),
-                                     tl0 + tc);
+                const int half = threadIdx.x >> 8;
+                unsigned short(&sT)[64][64 + 8] =
+                    *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem + half * 64 * 72);
+                for (int k = 0; k < kAdamGroup; k += 2) {
+                    const int tc = tg * kAdamGroup + k + half;
+                    if (k) __syncthreads();      // the transpose tiles are rewritten
+                    if (tc < N.nk) adamw_tile<true>(T, hy, sT, tl0 + tc, threadIdx.x & 255);
+                    else if (T.p_bf16_t) __syncthreads();
                 }
             }
             // the producer side of the hand-off: every wave's stores drained, one wave releases
@@ -528,7 +556,7 @@ __global__ __launch_bounds__(256, kWgPerCu) void train_dag_kernel(LaunchArgs a) 
     // zeroes them when it reads a non-zero status
     if (s_last && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         const int nc = tab->n_counters;
-        for (int i = threadIdx.x; i < kSyncCtr0 + nc; i += 256)
+        for (int i = threadIdx.x; i < kSyncCtr0 + nc; i += kThreads)
             if (i != kSyncStatus)
                 __hip_atomic_store(sync + i * kCtrStride, 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -550,7 +578,7 @@ int dag_grid(int* grid) {
                                            kLdsBytes);
         int per_cu = 0, cus = 0;
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, kLdsBytes);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, kLdsBytes);
         if (e == hipSuccess)
             e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess && per_cu < 1) e = hipErrorInvalidConfiguration;
@@ -575,7 +603,7 @@ int dag_trace(void* entries, void* wgs) {
 
 int dag_launch(const LaunchArgs& a, int grid, hipStream_t s) {
     LDM_REQUIRE(grid >= kQueues && grid % kQueues == 0, LDM_EINVAL, "train dag: grid %d", grid);
-    hipLaunchKernelGGL(train_dag_kernel, dim3(grid), dim3(256), kLdsBytes, s, a);
+    hipLaunchKernelGGL(train_dag_kernel, dim3(grid), dim3(kThreads), kLdsBytes, s, a);
     return launch_status("ldm_denoiser_train_step (dag)");
 }
 

@@ -1,10 +1,8 @@
 """Per-phase times of the XCD-replica sampling loop (csrc/sample_loop.hip
-sample_replica_kernel), from the diagnostic build's stamps (-DSL_STAMP=1): every wave sums the
-s_memrealtime ticks (100 MHz) of each phase of every layer it runs -- own granules landed, the
-workgroup's staging barrier, row dot products, reduce-scatter, epilogue + publish.
-  build:  make -C <csrc> BUILD=build_stamp OUT=../ldm_sdf/libldm_diag.so \\
-            HIPFLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -DSL_STAMP=1"
-  run:    LDM_SDF_LIB=<...>/libldm_diag.so python scripts/stamp_sampler.py [B]"""
+sample_replica_kernel), from its stamps (on in the product build since round 5, SL_STAMP = 1):
+every wave sums the s_memrealtime ticks (100 MHz) of each phase of every layer it runs -- own
+granules landed, the workgroup's staging barrier, row dot products, reduce-scatter, epilogue +
+publish.  Usage: python scripts/stamp_sampler.py [B]"""
 import ctypes as C
 import os
 import sys
