@@ -19,10 +19,13 @@ struct AdamHyper {
 // each thread 4 rows x 4 consecutive columns.  TT: ldm_adamw_tensor_t in any address space.
 // WT: write-through stores and an sc1 load of the gradient (wt_store.h).
 // tid: the thread's index among the tile's 256 (a 512-thread caller runs two tiles at once).
+// mode (the one-launch step's split update, train_dag.hip): 0 the whole update; 1 p, m, v only
+// (no bf16 copies, no barrier); 2 the bf16 copies only, from the p a mode-1 tile stored (read
+// sc1 when WT).  Modes 1 then 2 store exactly what mode 0 stores.
 template <bool WT = false, typename TT>
 __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
                                            unsigned short (&sT)[64][64 + 8], int tl,
-                                           int tid = threadIdx.x) {
+                                           int tid = threadIdx.x, int mode = 0) {
     const int rows = T.rows, cols = T.cols;
     const int tcn = (cols + 63) / 64;
     const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
@@ -42,7 +45,15 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
     for (int i = 0; i < 4; ++i) {
         const int r = min(r0 + (tid >> 4) + 16 * i, rows - 1);
         off[i] = (int64_t)r * cols + c0 + cq;
-        if (vec) {
+        if (mode == 2) {                          // the copies: the stored p only
+            if (vec) {
+                p4[i] = vld_at<WT, f32x4>(P, off[i]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    p4[i][e] = vld_at<WT, float>(P, c0 + cq + e < cols ? off[i] + e : off[i]);
+            }
+        } else if (vec) {
             p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
             g4[i] = vld_at<WT, f32x4>(Gp, off[i]);     // (WT: the handed-off gradient, sc1)
             m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
@@ -64,7 +75,9 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             float pi = p4[i][e], mi = m4[i][e], vi = v4[i][e];
-            adamw_update(pi, g4[i][e], mi, vi, decay, omb1, b2, omb2, eps, step_size, bc2_sqrt);
+            if (mode != 2)
+                adamw_update(pi, g4[i][e], mi, vi, decay, omb1, b2, omb2, eps, step_size,
+                             bc2_sqrt);
             p4[i][e] = pi; m4[i][e] = mi; v4[i][e] = vi;
             const unsigned u = __builtin_bit_cast(unsigned, pi);
             q[e] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
@@ -72,10 +85,12 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         }
         if (!rin) continue;
         if (vec) {
-            vst_at<WT>(P, off[i], p4[i]);
-            vst_at<WT>(M, off[i], m4[i]);
-            vst_at<WT>(V, off[i], v4[i]);
-            if (T.p_bf16) {
+            if (mode != 2) {
+                vst_at<WT>(P, off[i], p4[i]);
+                vst_at<WT>(M, off[i], m4[i]);
+                vst_at<WT>(V, off[i], v4[i]);
+            }
+            if (T.p_bf16 && mode != 1) {
                 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 w = {(unsigned)q[0] | ((unsigned)q[1] << 16),
                                  (unsigned)q[2] | ((unsigned)q[3] << 16)};
@@ -85,14 +100,17 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (c0 + cq + e >= cols) continue;
-                vst_at<WT>(P, off[i] + e, p4[i][e]);
-                vst_at<WT>(M, off[i] + e, m4[i][e]);
-                vst_at<WT>(V, off[i] + e, v4[i][e]);
-                if (T.p_bf16) vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), off[i] + e, q[e]);
+                if (mode != 2) {
+                    vst_at<WT>(P, off[i] + e, p4[i][e]);
+                    vst_at<WT>(M, off[i] + e, m4[i][e]);
+                    vst_at<WT>(V, off[i] + e, v4[i][e]);
+                }
+                if (T.p_bf16 && mode != 1)
+                    vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), off[i] + e, q[e]);
             }
         }
     }
-    if (!T.p_bf16_t) return;
+    if (!T.p_bf16_t || mode == 1) return;
     __syncthreads();
     // transposed: [c][r], 16 consecutive rows per thread (4 threads per column)
     const int cl = tid >> 2, rb = (tid & 3) * 16;

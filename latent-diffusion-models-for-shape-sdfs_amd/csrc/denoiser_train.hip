@@ -738,7 +738,9 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         ok = ok && (!row || P.M == L.Bp);
         for (int g = 0; g < P.n_seg; ++g) nd.nk += P.seg[g].K / 64;
         nd.kgp = gemm_tile_kgroup_period(gemm_tile_choice(a));
-        nd.tile = nd.kgp > 0 ? TILE_K2 : row ? TILE_ROW : TILE_W;
+        bool k128 = true;                 // every segment's K a multiple of 128 (128-deep stages)
+        for (int g = 0; g < P.n_seg; ++g) k128 = k128 && P.seg[g].K % 128 == 0;
+        nd.tile = nd.kgp == 2 && k128 ? TILE_K2L : nd.kgp > 0 ? TILE_K2 : row ? TILE_ROW : TILE_W;
         nd.tiles_m = (P.M + tile_rows(nd.tile) - 1) / tile_rows(nd.tile);
         nd.tiles_n = (P.N + tile_cols(nd.tile) - 1) / tile_cols(nd.tile);
         nd.adam = -1;
@@ -771,7 +773,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         }
         return add(nd);
     };
-    auto adam = [&](const float* g, int col_off, int col_tiles) -> int {
+    auto adam = [&](const float* g, int col_off, int col_tiles, int amode = 0) -> int {
         const int ti = tens(g);
         if (ti < 0) return -1;
         const ldm_adamw_tensor_t& t = tensors[ti];
@@ -779,6 +781,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         memset(&nd, 0, sizeof(nd));
         nd.type = N_ADAM;
         nd.adam = ti;
+        nd.amode = amode;
         nd.col_off = col_off;
         nd.tiles_m = (t.rows + 63) / 64;
         nd.nk = col_tiles ? col_tiles : (t.cols + 63) / 64;      // the node's 64-column tiles
@@ -820,7 +823,7 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         false);
     const int dwo = gemm(base, 0, false);
     dep(dwo, fo, false);
-    std::vector<int> Dk(nb), dwk(nb), duk(nb);
+    std::vector<int> Dk(nb), dwk(nb), duk(nb), uupd(nb, -1);
     std::vector<bool> wdone(nb, false);
     bool wout_done = false;
     auto adam_w = [&](int k) {            // W_k's update: its gradient and dh_k (reads W_k^T)
@@ -849,6 +852,10 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         duk[k] = gemm(base + 1 + i, 1, false);
         dep(duk[k], gprod, false);
         dep(sum(L.p_bblk[k], gr->b_blk[k], L.Bp / 32, H_, H_, 1.f, gr->b_blk[k]), gprod, false);
+        // U_k's fp32 update as soon as its gradient is final; its bf16 copies wait for dtemb,
+        // which reads U_k^T (the tail below): most of its bytes move off the step's tail
+        uupd[k] = adam(gr->w_blk[k], H_ / 64, H_ / 64, 1);
+        if (uupd[k] >= 0) dep(uupd[k], duk[k], false);
         if (k + 1 < nb) adam_w(k + 1);
         if (k == nb - 2) adam_wout();
     }
@@ -864,25 +871,27 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     const int dw2 = gemm(base + 2 + nb, 0, false);
     dep(dw2, dt, false);
     dep(sum(L.p_bt2, gr->b_t2, L.Bp / 32, H_, H_, 1.f, gr->b_t2), dt, false);
-    for (int k = nb - 1; k >= 0; --k) {      // U_k's update: its gradient and dtemb (reads U_k^T)
-        const int a = adam(gr->w_blk[k], H_ / 64, H_ / 64);
-        if (a >= 0) {
-            dep(a, duk[k], false);
-            dep(a, dt, false);
-        }
-    }
+    // the critical tail first (dtemb -> g_t -> dW_t1 -> w_t1's update), then the updates that
+    // only wait for dtemb (the U_k halves) and the in-projection's
     const int dw1 = gemm(base + 3 + nb, 0, false);
     dep(dw1, gt, false);
     dep(sum(L.p_bt1, gr->b_t1, L.Bp / 32, H_, H_, 1.f, gr->b_t1), gt, false);
-    int a = adam(gr->w_in, 0, 0);
-    if (a >= 0) dep(a, dwi, false);
+    int a = adam(gr->w_t1, 0, 0);
+    if (a >= 0) dep(a, dw1, false);
     a = adam(gr->w_t2, 0, 0);
     if (a >= 0) {
         dep(a, dw2, false);
         dep(a, gt, false);
     }
-    a = adam(gr->w_t1, 0, 0);
-    if (a >= 0) dep(a, dw1, false);
+    for (int k = nb - 1; k >= 0; --k) {      // U_k's bf16 copies: its update and dtemb (WAR)
+        a = adam(gr->w_blk[k], H_ / 64, H_ / 64, 2);
+        if (a >= 0) {
+            dep(a, uupd[k], false);
+            dep(a, dt, false);
+        }
+    }
+    a = adam(gr->w_in, 0, 0);
+    if (a >= 0) dep(a, dwi, false);
     for (int i = 0; i < n; ++i) ok = ok && used[i];         // every tensor is one of ours
     for (int i = 0; i < n; ++i) T.tensor[i] = tensors[i];
     if (!ok || nctr > kMaxCounters) return 1;

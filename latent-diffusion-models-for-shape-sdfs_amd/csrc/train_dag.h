@@ -28,9 +28,10 @@ constexpr int kBand = 64;               // rows of a band (= a row node's GEMM t
 constexpr int kThreads = 512;           // the kernel's workgroup: 8 waves, one per CU
 // GEMM job configurations (train_dag.hip TileCfg): tile rows x cols
 enum TileKind : int { TILE_K2 = 0 /* 64 x 64, two k-groups */, TILE_ROW = 1 /* 64 x 128 */,
-                      TILE_W = 2 /* 128 x 128 */ };
+                      TILE_W = 2 /* 128 x 128 */,
+                      TILE_K2L = 3 /* 64 x 64, two k-groups, 128-deep stages (kgp 2) */ };
 inline int tile_rows(int kind) { return kind == TILE_W ? 128 : 64; }
-inline int tile_cols(int kind) { return kind == TILE_K2 ? 64 : 128; }
+inline int tile_cols(int kind) { return kind == TILE_K2 || kind == TILE_K2L ? 64 : 128; }
 constexpr int kMaxDeps = 4;
 constexpr int kMaxNodes = 96;
 constexpr int kAdamGroup = 4;           // AdamW 64 x 64 tiles per job (one acquire for 4)
@@ -64,6 +65,7 @@ struct Node {
     int kgp;                        // GEMM: 0, or the k-group period of the launch path's tile
                                     // (two accumulators alternating every kgp 64-deep k-steps)
     int adam;                       // SUM / ADAM: tensor index (-1: no update)
+    int amode;                      // ADAM: adamw_tile mode (0 all; 1 p, m, v; 2 bf16 copies)
     int col_off;                    // ADAM: first 64-column tile of this node in the tensor
     // SUM: dst[c] = scale * sum_{r < rows} src[r ld + c], c < len; dst NULL: the launch's
     // loss_out

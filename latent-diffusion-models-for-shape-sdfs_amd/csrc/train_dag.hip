@@ -53,17 +53,17 @@ typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
 // Why 8 waves: a 4-wave workgroup streamed its operands at ~27-30 GB/s per CU, the launch
 // path's 8-wave tile at ~47 and 12 waves per CU at ~70 (profiles/r05n): the per-CU operand
 // stream scales with the waves issuing it, and fence-free hand-offs need one workgroup per CU.
-constexpr int KB = 64, NW = kThreads / 64, kWgPerCu = 1;
+constexpr int NW = kThreads / 64, kWgPerCu = 1;
 constexpr int kLdsBytes = 128 * 1024;
 template <int CFG>
 struct TileCfg {
     static constexpr int BM = CFG == TILE_W ? 128 : 64;
-    static constexpr int BN = CFG == TILE_K2 ? 64 : 128;
-    static constexpr int KG = CFG == TILE_K2 ? 2 : 1;          // k-groups
+    static constexpr int BN = CFG == TILE_K2 || CFG == TILE_K2L ? 64 : 128;
+    static constexpr int KG = CFG == TILE_K2 || CFG == TILE_K2L ? 2 : 1;   // k-groups
+    static constexpr int KB = CFG == TILE_K2L ? 128 : 64;      // k per ring stage
     static constexpr int WR = 2, WC = NW / KG / WR;             // waves per group: WR x WC
     static constexpr int RM = BM / WR / 32, RN = BN / WC / 32;  // 32 x 32 blocks per wave
-    static constexpr int STAGES = CFG == TILE_W ? 4 : CFG == TILE_ROW ? 5 : 8;
-    static constexpr bool PIPE = false;        // double-buffered fragments (KG = 1 only)
+    static constexpr int STAGES = CFG == TILE_W || CFG == TILE_K2L ? 4 : CFG == TILE_ROW ? 5 : 8;
     static constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
     typedef TileSrc<BM, NW, KB> SrcA;
     typedef TileSrc<BN, NW, KB> SrcB;
@@ -148,14 +148,14 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
     typedef TileCfg<CFG> C;
     constexpr int BM = C::BM, BN = C::BN, STAGES = C::STAGES, RM = C::RM, RN = C::RN;
     constexpr int KG = C::KG, WC = C::WC, A_ELEMS = C::A_ELEMS, STAGE_ELEMS = C::STAGE_ELEMS;
-    constexpr int G = C::G;
+    constexpr int G = C::G, KB = C::KB, KS = KB / 64;        // KS 64-deep k-steps per stage
     KProb& P = N.P;
     const int tn_n = N.tiles_n;
     const int tm = job / tn_n, tn = job - tm * tn_n;
     const int m0 = tm * BM, n0 = tn * BN;
     const int grp = wave / (NW / KG), wl = wave % (NW / KG);   // k-group, wave in the group
     const int wr = wl / WC, wc = wl % WC, r32 = lane & 31, h = lane >> 5;
-    const int nk = N.nk, kgp = N.kgp;
+    const int nk = N.nk / KS, kgp = N.kgp / KS;     // in ring stages (TILE_K2L: kgp 2 -> 1)
     typename C::SrcA srcA;
     typename C::SrcB srcB;
     int seg = 0, seg_left = 0, qi = 0;
@@ -207,53 +207,38 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
                         __builtin_bit_cast(bf16x8, f.a[s][i]), __builtin_bit_cast(bf16x8, f.b[s][j]),
                         acc[i][j], 0, 0, 0);
     };
+    // The fragment reads of a stage go BEFORE the next DMA issue, and the prologue issues only
+    // the first stage(s) a step reads: an LDS read after an LDS-DMA issue makes the compiler
+    // wait for every DMA in flight (vmcnt(0): it cannot tell the ring slots apart), so the
+    // first read would otherwise wait for the whole prefetched ring.
     seat(0);
-    for (int p = 0; p < STAGES && p < nk; ++p) issue();
-    if constexpr (KG == 1 && !C::PIPE) {
-        // one fragment set: the workgroup's two waves per SIMD hide each other's LDS reads
-        // stage j landed (stages issued: STAGES, then one per step from step 1, refilling the
-        // slot of stage j - 1, whose reads every wave finished before this barrier)
+    if constexpr (KG == 1) {
+        // stage j landed (issued so far: min(nk, j + STAGES - 1) -- the issue after step j's
+        // reads refills the slot of stage j - 1, whose reads every wave finished before the
+        // barrier); the workgroup's two waves per SIMD hide each other's LDS reads
+        issue();
         for (int j = 0; j < nk; ++j) {
-            wait_younger<G>(j == 0 ? min(STAGES - 1, nk - 1) : min(STAGES - 2, nk - 1 - j));
+            wait_younger<G>(j == 0 ? 0 : min(STAGES - 2, nk - 1 - j));
             Frags f;
             read_frags(j % STAGES, f);
-            if (j > 0 && j - 1 + STAGES < nk) issue();
+            while (qi < nk && qi < j + STAGES) issue();
             mfma(f);
-        }
-    } else if constexpr (KG == 1) {
-        // Software-pipelined: stage j + 1's fragments are read from LDS (into the other register
-        // set) while stage j's MFMAs run.  Before the reads: stage j + 1 landed for every wave
-        // and every wave's reads of stage j are done (they went to registers one step earlier),
-        // so stage j + STAGES can refill stage j's slot.
-        auto kstep = [&](int j, const Frags& cur, Frags& nxt) __attribute__((always_inline)) {
-            if (j + 1 < nk) {
-                wait_younger<G>(min(STAGES - 2, nk - j - 2));
-                if (j + STAGES < nk) issue();
-                read_frags((j + 1) % STAGES, nxt);
-            }
-            mfma(cur);
-        };
-        Frags F0, F1;
-        wait_younger<G>(min(STAGES - 1, nk - 1));
-        read_frags(0, F0);
-        for (int j = 0; j < nk; j += 2) {
-            kstep(j, F0, F1);
-            if (j + 1 < nk) kstep(j + 1, F1, F0);
         }
     } else {
         // Two k-groups: per super-step of 2 kgp stages, group g takes stages s0 + g kgp + u
-        // (u < kgp) -- the two groups read and multiply different stages at once.  The next
-        // stages refill the slots of the previous super-step (all its reads done: the barrier).
+        // (u < kgp) -- the two groups read and multiply different stages at once.  The issue
+        // after the first reads refills the slots of the previous super-step (all its reads
+        // done: the barrier).
+        while (qi < nk && qi < 2 * kgp) issue();
         for (int s0 = 0; s0 < nk; s0 += 2 * kgp) {
             wait_younger<G>(qi - min(nk, s0 + 2 * kgp));
-            while (qi < nk && qi < s0 + STAGES) issue();
             for (int u = 0; u < kgp; ++u) {
                 const int q = s0 + grp * kgp + u;
-                if (q < nk) {
-                    Frags f;
-                    read_frags(q % STAGES, f);
-                    mfma(f);
-                }
+                Frags f;
+                if (q < nk) read_frags(q % STAGES, f);
+                if (u == 0)
+                    while (qi < nk && qi < s0 + STAGES) issue();
+                if (q < nk) mfma(f);
             }
         }
         // group 1's sums -> LDS (past the epilogue scratch), group 0 adds them: acc0 + acc1
@@ -436,11 +421,17 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
     // The scheduler's control flow is wave-uniform (wave 0 runs it with all its lanes; a lane-0
     // region holds no loop), so every wave meets every workgroup barrier the same number of
     // times.
+    // The next queue index is fetched as a job ends (its atomic's latency overlaps the job's
+    // store drain) and taken at the top of the next round: every fetched index is this
+    // workgroup's, and a job is bound to it only as it becomes free.
+    unsigned jl_next = 0;
+    bool have_next = false;
     for (;;) {
         if (wave == 0) {
-            unsigned jl = 0;
-            if (lane == 0 && table_ok)
+            unsigned jl = jl_next;
+            if (lane == 0 && table_ok && !have_next)
                 jl = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            have_next = false;
             const int j = table_ok ? (int)__builtin_amdgcn_readfirstlane(jl) : qlen;
             int e = -1;
             if (j < qlen) {
@@ -480,6 +471,7 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
                 // diagnostics: this node type's compute skipped
             } else if (type == N_GEMM) {
                 if (N.tile == TILE_W) gemm_job<TILE_W>(N, job, ka->eps, smem, wave, lane);
+                else if (N.tile == TILE_K2L) gemm_job<TILE_K2L>(N, job, ka->eps, smem, wave, lane);
                 else if (N.tile == TILE_ROW) gemm_job<TILE_ROW>(N, job, ka->eps, smem, wave, lane);
                 else gemm_job<TILE_K2>(N, job, ka->eps, smem, wave, lane);
             } else if (type == N_PREP) {
@@ -499,14 +491,22 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
                 for (int k = 0; k < kAdamGroup; k += 2) {
                     const int tc = tg * kAdamGroup + k + half;
                     if (k) __syncthreads();      // the transpose tiles are rewritten
-                    if (tc < N.nk) adamw_tile<true>(T, hy, sT, tl0 + tc, threadIdx.x & 255);
-                    else if (T.p_bf16_t) __syncthreads();
+                    if (tc < N.nk)
+                        adamw_tile<true>(T, hy, sT, tl0 + tc, threadIdx.x & 255, N.amode);
+                    else if (T.p_bf16_t && N.amode != 1)
+                        __syncthreads();
                 }
             }
-            // the producer side of the hand-off: every wave's stores drained, one wave releases
-            // and one lane counts the job (a node no later job waits on skips both: the launch's
-            // end publishes its stores)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (wave == 0) {                 // the next round's queue index (see above)
+                if (lane == 0 && table_ok)
+                    jl_next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                have_next = true;
+            }
+            // the producer side of the hand-off: every wave's stores drained, then one lane
+            // counts the job (a node no later job waits on skips both: the launch's end
+            // publishes its stores; its stores then drain under the next job)
+            if (N.signal) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (wave == 0 && N.signal) {
                 if (ka->dbg & kDbgFences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
