@@ -681,6 +681,8 @@ struct DagHost {
     std::vector<uint32_t> entries;
 };
 
+constexpr bool kSplitU = false;     // U_k's AdamW as an early update + late copies (measured: off)
+
 // Builds the job table of one step; returns 1 (and builds nothing) when this configuration has
 // no DAG form -- the caller then runs the launch path.
 int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
@@ -852,10 +854,13 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         duk[k] = gemm(base + 1 + i, 1, false);
         dep(duk[k], gprod, false);
         dep(sum(L.p_bblk[k], gr->b_blk[k], L.Bp / 32, H_, H_, 1.f, gr->b_blk[k]), gprod, false);
-        // U_k's fp32 update as soon as its gradient is final; its bf16 copies wait for dtemb,
-        // which reads U_k^T (the tail below): most of its bytes move off the step's tail
-        uupd[k] = adam(gr->w_blk[k], H_ / 64, H_ / 64, 1);
-        if (uupd[k] >= 0) dep(uupd[k], duk[k], false);
+        // (U_k's update waits for dtemb, which reads U_k^T: the tail below.  Split into an early
+        // fp32 update here and late bf16 copies -- adamw_tile modes 1 / 2, kSplitU -- its
+        // jobs took CUs from the backward chain: 321 -> 350 us per step, profiles/r05r.)
+        if (kSplitU) {
+            uupd[k] = adam(gr->w_blk[k], H_ / 64, H_ / 64, 1);
+            if (uupd[k] >= 0) dep(uupd[k], duk[k], false);
+        }
         if (k + 1 < nb) adam_w(k + 1);
         if (k == nb - 2) adam_wout();
     }
@@ -883,10 +888,10 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         dep(a, dw2, false);
         dep(a, gt, false);
     }
-    for (int k = nb - 1; k >= 0; --k) {      // U_k's bf16 copies: its update and dtemb (WAR)
-        a = adam(gr->w_blk[k], H_ / 64, H_ / 64, 2);
+    for (int k = nb - 1; k >= 0; --k) {      // U_k's update (or its bf16 copies): dtemb (WAR)
+        a = adam(gr->w_blk[k], H_ / 64, H_ / 64, kSplitU ? 2 : 0);
         if (a >= 0) {
-            dep(a, uupd[k], false);
+            dep(a, kSplitU ? uupd[k] : duk[k], false);
             dep(a, dt, false);
         }
     }
