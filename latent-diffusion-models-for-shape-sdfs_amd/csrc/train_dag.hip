@@ -421,17 +421,11 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
     // The scheduler's control flow is wave-uniform (wave 0 runs it with all its lanes; a lane-0
     // region holds no loop), so every wave meets every workgroup barrier the same number of
     // times.
-    // The next queue index is fetched as a job ends (its atomic's latency overlaps the job's
-    // store drain) and taken at the top of the next round: every fetched index is this
-    // workgroup's, and a job is bound to it only as it becomes free.
-    unsigned jl_next = 0;
-    bool have_next = false;
     for (;;) {
         if (wave == 0) {
-            unsigned jl = jl_next;
-            if (lane == 0 && table_ok && !have_next)
+            unsigned jl = 0;
+            if (lane == 0 && table_ok)
                 jl = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            have_next = false;
             const int j = table_ok ? (int)__builtin_amdgcn_readfirstlane(jl) : qlen;
             int e = -1;
             if (j < qlen) {
@@ -497,16 +491,12 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
                         __syncthreads();
                 }
             }
-            if (wave == 0) {                 // the next round's queue index (see above)
-                if (lane == 0 && table_ok)
-                    jl_next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                have_next = true;
-            }
             // the producer side of the hand-off: every wave's stores drained, then one lane
-            // counts the job (a node no later job waits on skips both: the launch's end
-            // publishes its stores; its stores then drain under the next job)
-            if (N.signal) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // counts the job (a node no later job waits on skips the count: the launch's end
+            // publishes its stores).  (Fetching the next queue index as a job ends, and skipping
+            // the drain of unwatched jobs, measured slower together with a tail reorder:
+            // profiles/r05s.)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (wave == 0 && N.signal) {
                 if (ka->dbg & kDbgFences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
