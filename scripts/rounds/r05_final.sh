@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5 final validation -> profiles/r05z/: the whole GPU suite, smoke, the default bench and
-# the rocprofv3 kernel-trace summary of the same bench command.
+# Round 5 final validation -> profiles/r05z/: the A/B of the training-step forms, the whole GPU
+# suite, smoke, the default bench and the rocprofv3 kernel-trace summary of the same command.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
@@ -13,6 +13,7 @@ step() {   # name timeout cmd...
   echo "== $n rc $rc"; tail -${TAILN:-6} $O/$n.log
   [ $rc -eq 0 ] || exit $rc
 }
+step train_ab 300 python -u scripts/train_form_ab.py 6 128
 TAILN=4 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 TAILN=2 step bench 600 python -u bench.py
