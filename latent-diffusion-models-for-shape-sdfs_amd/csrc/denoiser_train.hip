@@ -930,6 +930,18 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         T.qlen[qq] = (int)q[qq].size();
         H.entries.insert(H.entries.end(), q[qq].begin(), q[qq].end());
     }
+    // the claim scheduler's lists: each queue split into its chain jobs and the rest
+    for (int cls = 0; cls < 2; ++cls)
+        for (int qq = 0; qq < kQueues; ++qq) {
+            const int li = qq + cls * kQueues;
+            T.qoff2[li] = (int)H.entries.size();
+            for (uint32_t en : q[qq]) {
+                const Node& nd = T.node[en >> 16];
+                const bool chain = nd.type == N_PREP || (nd.type == N_GEMM && nd.row);
+                if (chain == (cls == 0)) H.entries.push_back(en);
+            }
+            T.qlen2[li] = (int)H.entries.size() - T.qoff2[li];
+        }
     if ((int)H.entries.size() > kMaxEntries) return 1;
     T.n_counters = nctr;
     T.n_entries = (int)H.entries.size();
@@ -1172,6 +1184,8 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
         put("\n");
     }
     for (int q = 0; q < dag::kQueues; ++q) put("queue %d: %d jobs at %d\n", q, T.qlen[q], T.qoff[q]);
+    for (int q = 0; q < 2 * dag::kQueues; ++q)
+        put("claim list %d: %d jobs at %d\n", q, T.qlen2[q], T.qoff2[q]);
 #undef put
     delete h;
     return 0;

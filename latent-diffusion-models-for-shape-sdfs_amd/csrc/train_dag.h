@@ -36,12 +36,13 @@ constexpr int kMaxDeps = 4;
 constexpr int kMaxNodes = 96;
 constexpr int kAdamGroup = 4;           // AdamW 64 x 64 tiles per job (one acquire for 4)
 constexpr int kCtrStride = 32;          // counters 128 bytes apart (one line each)
-// sync region (unsigned words, each on its own 128-byte line): queue heads, exit counter,
-// status, then the counters
-constexpr int kSyncHead = 0;            // kQueues lines
-constexpr int kSyncExit = kQueues;      // 1 line
-constexpr int kSyncStatus = kQueues + 1;
-constexpr int kSyncCtr0 = kQueues + 2;  // first counter line
+// sync region (unsigned words, each on its own 128-byte line): queue heads, the claim lists'
+// heads, exit counter, status, then the counters
+constexpr int kSyncHead = 0;                    // kQueues lines
+constexpr int kSyncHead2 = kQueues;             // 2 kQueues lines (the claim scheduler's lists)
+constexpr int kSyncExit = 3 * kQueues;          // 1 line
+constexpr int kSyncStatus = 3 * kQueues + 1;
+constexpr int kSyncCtr0 = 3 * kQueues + 2;      // first counter line
 
 enum NodeType : int { N_GEMM = 0, N_PREP = 1, N_SUM = 2, N_ADAM = 3 };
 
@@ -86,6 +87,9 @@ struct Table {
     uint64_t hash;                  // of the inputs the table was built from (launch checks it)
     int n_nodes, n_counters, n_entries, n_tensors, grid;
     int qlen[kQueues], qoff[kQueues];   // queue q: entries[qoff[q] .. qoff[q] + qlen[q])
+    // the claim scheduler's lists (kDbgClaim): per queue q the chain jobs (row nodes, prep) at
+    // [q] and the others at [q + kQueues], each in node order
+    int qlen2[2 * kQueues], qoff2[2 * kQueues];
     ldm_adamw_tensor_t tensor[LDM_ADAMW_MAX_TENSORS];
     Node node[kMaxNodes];
     // uint32 entries[n_entries] follow: node << 16 | job
@@ -93,6 +97,7 @@ struct Table {
 
 constexpr int kMaxEntries = 16384;
 constexpr unsigned kDbgFences = 128;
+constexpr unsigned kDbgClaim = 256;     // claim scheduler: take only READY jobs, chain first
 inline size_t table_bytes() { return sizeof(Table) + sizeof(uint32_t) * kMaxEntries; }
 inline size_t sync_bytes(int n_counters) {
     return (size_t)(kSyncCtr0 + n_counters) * kCtrStride * sizeof(unsigned);
@@ -114,7 +119,8 @@ struct LaunchArgs {
     unsigned spin_limit;    // microseconds a dependency wait may take before it gives up
     unsigned dbg;           // diagnostics (ldm_dev_train_dag_flags): bit t skips the compute of
                             // node type t (jobs still wait and signal); kDbgFences: add the
-                            // agent release / acquire fences to every hand-off (A/B)
+                            // agent release / acquire fences to every hand-off (A/B);
+                            // kDbgClaim: the claim scheduler (train_dag.hip)
 };
 
 // device side (train_dag.hip)

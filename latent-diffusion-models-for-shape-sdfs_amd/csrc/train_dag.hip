@@ -421,8 +421,68 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
     // The scheduler's control flow is wave-uniform (wave 0 runs it with all its lanes; a lane-0
     // region holds no loop), so every wave meets every workgroup barrier the same number of
     // times.
+    const bool claim = (ka->dbg & kDbgClaim) != 0;
     for (;;) {
-        if (wave == 0) {
+        if (wave == 0 && claim) {
+            // Claim scheduler: a workgroup takes only a job whose inputs are READY -- the head of
+            // its queue's chain list first, else the head of the rest -- by compare-and-swap on
+            // that list's head; it never holds a job while it waits.  Progress: the earliest
+            // unfinished job (node order is topological) has every input, and it heads its list.
+            int e = -1;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (unsigned n = 0; table_ok; ++n) {
+                bool any = false;
+                for (int cls = 0; cls < 2 && e < 0; ++cls) {
+                    const int li = q + cls * kQueues;
+                    unsigned* hd = sync + (kSyncHead2 + li) * kCtrStride;
+                    const int len = tab->qlen2[li], off = tab->qoff2[li];
+                    const int h = (int)poll(hd);
+                    if (h >= len) continue;
+                    any = true;
+                    const int ee = (int)__builtin_amdgcn_readfirstlane(entries[off + h]);
+                    KNode& Nn = tab->node[ee >> 16];
+                    const int jb = (ee & 0xffff) / Nn.tiles_n;
+                    bool ready = true;
+                    for (int d = 0; d < Nn.ndep && ready; ++d)
+                        ready = poll(ctr(sync, Nn.dep_ctr[d] + (Nn.dep_band[d] ? jb : 0))) >=
+                                Nn.dep_target[d];
+                    if (!ready) continue;
+                    unsigned won = 0;
+                    if (lane == 0) {
+                        unsigned expect = (unsigned)h;
+                        won = __hip_atomic_compare_exchange_strong(
+                                  hd, &expect, (unsigned)h + 1u, __ATOMIC_RELAXED,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+                    }
+                    if (__builtin_amdgcn_readfirstlane(won)) {
+                        e = ee;
+#if DAG_TRACE
+                        tr_idx = off + h;
+#endif
+                    } else {
+                        cls = -1;            // lost the race: look at the chain list again
+                        any = true;
+                    }
+                }
+                if (e >= 0 || !any) break;
+                __builtin_amdgcn_s_sleep(2);
+                if ((n & 15) == 15) {
+                    if (poll(status) != 0) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)limit * 100u) {
+                        if (lane == 0)
+                            __hip_atomic_store(status, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+#if DAG_TRACE
+            tr_deq = t0;
+            tr_rdy = __builtin_amdgcn_s_memrealtime();
+#endif
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) s_job = e;
+        } else if (wave == 0) {
             unsigned jl = 0;
             if (lane == 0 && table_ok)
                 jl = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

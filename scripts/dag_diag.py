@@ -62,12 +62,13 @@ ops.denoiser_train_step_adamw(pack["desc"], sd, lat, eps, t, ws, gs, loss, table
 torch.cuda.synchronize()
 print(f"step: {1e3 * (time.perf_counter() - t0):.2f} ms, form {ops.train_step_last_form()}, "
       f"loss {float(loss):.5f}")
-nsync = (10 + 512) * 128
+C0 = 26                                  # train_dag.h kSyncCtr0 (heads 0-23, exit 24, status 25)
+nsync = (C0 + 512) * 128
 w = ws[-nsync:].view(torch.int32).cpu().view(-1, 32)[:, 0]
-print("heads", w[:8].tolist(), "exit", int(w[8]), "status", int(w[9]))
+print("heads", w[:24].tolist(), "exit", int(w[24]), "status", int(w[25]))
 for nd in nodes:
-    allv = int(w[10 + nd["all"]])
-    bands = w[10 + nd["band"]:10 + nd["band"] + nd["tm"]].tolist() if nd["band"] >= 0 else []
+    allv = int(w[C0 + nd["all"]])
+    bands = w[C0 + nd["band"]:C0 + nd["band"] + nd["tm"]].tolist() if nd["band"] >= 0 else []
     tot = nd["tm"] * nd["tn"]
     flag = "" if allv == tot else "   <-- incomplete"
     print(f"node {nd['i']:2d} {nd['type']:4s} all {allv}/{tot} bands {bands}{flag}")

@@ -19,6 +19,12 @@ dev = torch.device("cuda", 0)
 lat = torch.randn(1000, 256, device=dev) * 0.5
 sch = ldm_sdf.DDPMSchedule()
 forms = os.environ.get("AB_FORMS", "dag,launches").split(",")
+if os.environ.get("DAG_FLAGS"):            # ldm_dev_train_dag_flags, e.g. 0x100: claim scheduler
+    import ctypes as C
+    from ldm_sdf import _capi as capi
+    fl = capi.load().ldm_dev_train_dag_flags
+    fl.restype, fl.argtypes = C.c_int, [C.c_uint]
+    fl(int(os.environ["DAG_FLAGS"], 0))
 states, models, gens = {}, {}, {}
 for f in forms:     # same weights, same t / eps draws per form: the params must end bit-identical
     ops.train_step_config(f)

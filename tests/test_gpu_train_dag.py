@@ -128,6 +128,28 @@ def test_dag_required_form_fails_loudly_with_side_stream(dev, form):
     assert ops.train_step_last_form() == "launches"
 
 
+def _dag_flags(v):
+    import ctypes as C
+    from ldm_sdf import _capi as capi
+    fl = capi.load().ldm_dev_train_dag_flags
+    fl.restype, fl.argtypes = C.c_int, [C.c_uint]
+    return fl(v)
+
+
+@pytest.mark.parametrize("M", [1000, 37])
+def test_dag_claim_scheduler_bitwise(dev, form, M):
+    """The claim scheduler (a workgroup takes only READY jobs, chain list first; train_dag.hip,
+    kDbgClaim) computes the same step bit for bit: the schedule never changes an arithmetic."""
+    ref = _run(dev, "launches", M=M)
+    _dag_flags(0x100)
+    try:
+        got = _run(dev, "dag", M=M)
+    finally:
+        _dag_flags(0)
+    assert got[0] == "dag"
+    _assert_same(got, ref)
+
+
 def test_trainstate_save_resume_bitwise(dev, tmp_path):
     """SURVEY §5 checkpoint / resume: 64 uninterrupted steps == 32 steps, TrainState.save
     (masters, AdamW moments, step, losses, generator state), a FRESH denoiser object loading it
