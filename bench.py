@@ -910,6 +910,26 @@ def bench_train(args, dev, gen):
                         "note": "3 x 2 x forward MACs per step (1000 samples) over the wall "
                                 "time of a step (every launch incl. AdamW, 100 timed steps)"},
            "loss_first_last": [st.losses[0], st.losses[-1]]}
+    res["form"] = ldm_sdf.ops.train_step_last_form()
+    # the other form of the same step, same model state, for the record:
+    # the one-launch DAG step when "auto" ran the launches, and the other way round
+    from ldm_sdf import ops as _ops
+    other = "dag" if res["form"] == "launches" else "launches"
+    try:
+        _ops.train_step_config(other)
+        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16", state=st)
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=args.train_steps, batch=1000,
+                           dtype="bf16", state=st)
+        torch.cuda.synchronize()
+        d_o = (time.perf_counter() - t4) / args.train_steps
+        res["other_form"] = {"form": _ops.train_step_last_form(), "steps_per_s": 1.0 / d_o,
+                             "ms_per_step": d_o * 1e3,
+                             "note": "same step, bit-identical results (tests/test_gpu_train_dag.py); "
+                                     "value is the form 'auto' picks"}
+    finally:
+        _ops.train_step_config("auto")
     if not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_train(min(10.0, args.cpu_seconds))
     return res
