@@ -283,6 +283,13 @@ int ldm_train_step_config(int form, unsigned spin_limit);
 int ldm_train_step_last_form(void);   /* the form the last step on this device ran (0: none) */
 int ldm_denoiser_train_status(const ldm_denoiser_t* w, int B, void* saved, unsigned* status_host,
                               ldm_stream_t s);
+/* Call once on a NEW `saved` workspace (fresh allocation) before its first one-launch step:
+ * zeroes its sync words (on s) and drops the host's record of a job table uploaded to that
+ * address.  The record is keyed by address and inputs, so a workspace allocated where a freed
+ * one lay -- with the same descriptor, gradient and AdamW pointers, as a caching allocator
+ * hands out -- would otherwise be taken as holding its predecessor's table and sync words,
+ * which other allocations may have overwritten since (the kernel then reports status 3). */
+int ldm_denoiser_train_ws_init(const ldm_denoiser_t* w, int B, void* saved, ldm_stream_t s);
 /* Diagnostics (host only, no device work): the job table of this configuration as text into
  * buf[len] -- per node its type, jobs, k-steps, counters and dependencies, then the queues.
  * 1: the configuration has no one-launch form. */

@@ -681,6 +681,17 @@ struct DagHost {
     std::vector<uint32_t> entries;
 };
 
+// The uploaded tables, by device table address (entries are kept for the process: an async
+// upload reads them); ldm_denoiser_train_ws_init forgets one.
+struct DagCache {
+    std::mutex mu;
+    std::unordered_map<const void*, DagHost*> by_table;
+};
+DagCache& dag_cache() {
+    static DagCache c;
+    return c;
+}
+
 constexpr bool kSplitU = false;     // U_k's AdamW as an early update + late copies (measured: off)
 
 // Builds the job table of one step; returns 1 (and builds nothing) when this configuration has
@@ -902,6 +913,33 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
     for (int i = 0; i < n; ++i) ok = ok && used[i];         // every tensor is one of ours
     for (int i = 0; i < n; ++i) T.tensor[i] = tensors[i];
     if (!ok || nctr > kMaxCounters) return 1;
+    // GEMM operands that are bf16 weight copies: a tensor's ADAM jobs rewrite its copies only
+    // after every job reading them (the dependencies above), and the launch boundary before
+    // the step made them visible, so those loads may go through the L2 (plain) instead of sc1
+    // -- every band tile of a node re-reads the node's weights.  Measured ~1 % slower at config
+    // 2 (profiles/r05v/train_ab_*.log), so only under ldm_dev_train_dag_flags kDbgWeightsL2.
+    auto is_weight = [&](const void* p) {
+        const char* c = static_cast<const char*>(p);
+        for (int i = 0; i < n; ++i) {
+            const int64_t bytes = (int64_t)tensors[i].rows * tensors[i].cols * 2;
+            for (const void* w : {tensors[i].p_bf16, tensors[i].p_bf16_t}) {
+                const char* w0 = static_cast<const char*>(w);
+                if (w0 && c >= w0 && c < w0 + bytes) return true;
+            }
+        }
+        return false;
+    };
+    for (int i = 0; i < T.n_nodes; ++i) {
+        Node& nd = T.node[i];
+        nd.stat = 0;
+        if (nd.type != N_GEMM) continue;
+        int sa = 1, sb = 2;
+        for (int s = 0; s < nd.P.n_seg; ++s) {
+            if (!is_weight(nd.P.seg[s].A)) sa = 0;
+            if (!is_weight(nd.P.seg[s].B)) sb = 0;
+        }
+        nd.stat = sa | sb;
+    }
     // every dependency points at an earlier node (the deadlock-freedom argument)
     for (int c = 0; c < T.n_nodes; ++c)
         for (int d = 0; d < T.node[c].ndep; ++d)
@@ -977,12 +1015,11 @@ int dag_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, co
     h = fnv(h, &L.dag_table, sizeof(L.dag_table));
     const size_t tb = sizeof(dag::Table);
     h = fnv(h, &tb, sizeof(tb));
-    static std::mutex mu;
-    static std::unordered_map<const void*, DagHost*> cache;      // by device table address
+    DagCache& dc = dag_cache();
     DagHost* hc = nullptr;
     {
-        std::lock_guard<std::mutex> g(mu);
-        DagHost*& slot = cache[L.dag_table];
+        std::lock_guard<std::mutex> g(dc.mu);
+        DagHost*& slot = dc.by_table[L.dag_table];
         if (!slot) slot = new DagHost();       // kept for the process: the async upload reads it
         hc = slot;
     }
@@ -1147,6 +1184,23 @@ extern "C" int ldm_denoiser_train_status(const ldm_denoiser_t* w, int B, void* s
     return 0;
 }
 
+extern "C" int ldm_denoiser_train_ws_init(const ldm_denoiser_t* w, int B, void* saved,
+                                          ldm_stream_t s) {
+    LDM_REQUIRE(w && B >= 1 && saved && w->n_blocks >= 1 && w->n_blocks <= LDM_MAX_BLOCKS,
+                LDM_EINVAL, "ldm_denoiser_train_ws_init: bad arguments");
+    const TrainWs L = layout(w, B, saved);
+    {
+        DagCache& dc = dag_cache();
+        std::lock_guard<std::mutex> g(dc.mu);
+        auto it = dc.by_table.find(L.dag_table);
+        if (it != dc.by_table.end()) it->second->hash = 0;     // re-uploaded by the next step
+    }
+    const hipError_t e =
+        hipMemsetAsync(L.dag_sync, 0, dag::sync_bytes(dag::kMaxCounters), (hipStream_t)s);
+    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_denoiser_train_ws_init: %s", hipGetErrorString(e));
+    return 0;
+}
+
 // Diagnostics: the job table a step of this configuration runs, as text (one line per node:
 // type, jobs, k-steps, k-group period, counters, dependencies; then the queue lengths), built
 // on the host exactly as the step builds it.  Returns 1 if the configuration has no DAG form.
@@ -1177,8 +1231,8 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
         T.n_entries);
     for (int i = 0; i < T.n_nodes; ++i) {
         const dag::Node& nd = T.node[i];
-        put("%d %s %dx%d nk %d kgp %d band %d all %d sig %d deps", i, kType[nd.type],
-            nd.tiles_m, nd.tiles_n, nd.nk, nd.kgp, nd.out_band, nd.out_all, nd.signal);
+        put("%d %s %dx%d nk %d kgp %d band %d all %d sig %d wt %d deps", i, kType[nd.type],
+            nd.tiles_m, nd.tiles_n, nd.nk, nd.kgp, nd.out_band, nd.out_all, nd.signal, nd.stat);
         for (int d = 0; d < nd.ndep; ++d)
             put(" [%d%s>=%u]", nd.dep_ctr[d], nd.dep_band[d] ? "+band" : "", nd.dep_target[d]);
         put("\n");

@@ -65,6 +65,9 @@ struct Node {
     int row;                        // GEMM / PREP: rows are the batch's (64-row band counters)
     int kgp;                        // GEMM: 0, or the k-group period of the launch path's tile
                                     // (two accumulators alternating every kgp 64-deep k-steps)
+    int stat;                       // GEMM: bit 0 / 1: every segment's A / B is a weight copy
+                                    // no job writes before the step's last read of it -- may be
+                                    // loaded through the L2 (plain) instead of sc1 (kDbgWeightsL2)
     int adam;                       // SUM / ADAM: tensor index (-1: no update)
     int amode;                      // ADAM: adamw_tile mode (0 all; 1 p, m, v; 2 bf16 copies)
     int col_off;                    // ADAM: first 64-column tile of this node in the tensor
@@ -98,6 +101,8 @@ struct Table {
 constexpr int kMaxEntries = 16384;
 constexpr unsigned kDbgFences = 128;
 constexpr unsigned kDbgClaim = 256;     // claim scheduler: take only READY jobs, chain first
+constexpr unsigned kDbgWeightsL2 = 512; // weight operands through the L2 (Node::stat; measured
+                                        // ~1 % slower than sc1 at config 2, profiles/r05v)
 inline size_t table_bytes() { return sizeof(Table) + sizeof(uint32_t) * kMaxEntries; }
 inline size_t sync_bytes(int n_counters) {
     return (size_t)(kSyncCtr0 + n_counters) * kCtrStride * sizeof(unsigned);

@@ -4,7 +4,7 @@
 // time in per-launch fixed cost -- argument issue, ring fill, the epilogue tail of the last
 // workgroups, the gap to the next launch -- and its AdamW (HBM-bound) starts only after the
 // last GEMM (DESIGN.md §5, round-4 stamps).  Here a workgroup that finishes a tile takes the
-// next job at once, dependent layers are handed off per 128-row band instead of per launch, and
+// next job at once, dependent layers are handed off per 64-row band (kBand) instead of per launch, and
 // the weight-gradient tiles, bias sums and AdamW tiles fill the CUs the residual chain leaves
 // idle.
 //
@@ -144,7 +144,7 @@ __device__ __forceinline__ unsigned short to_bf16(float x) {
 // summation exactly.
 template <int CFG>
 __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
-                                         unsigned short* smem, int wave, int lane) {
+                                         unsigned short* smem, int wave, int lane, int stat) {
     typedef TileCfg<CFG> C;
     constexpr int BM = C::BM, BN = C::BN, STAGES = C::STAGES, RM = C::RM, RN = C::RN;
     constexpr int KG = C::KG, WC = C::WC, A_ELEMS = C::A_ELEMS, STAGE_ELEMS = C::STAGE_ELEMS;
@@ -169,8 +169,11 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
         if (seg_left == 0) seat(++seg);
         unsigned short* st = smem + (qi % STAGES) * STAGE_ELEMS;
         ++qi;
-        srcA.template issue<16>(st, wave, false);           // sc1 operand loads (hand-offs)
-        srcB.template issue<16>(st + A_ELEMS, wave, false);
+        // sc1 operand loads (hand-offs); with kDbgWeightsL2 a weight copy (Node::stat) through the L2
+        if (stat & 1) srcA.template issue<0>(st, wave, false);
+        else srcA.template issue<16>(st, wave, false);
+        if (stat & 2) srcB.template issue<0>(st + A_ELEMS, wave, false);
+        else srcB.template issue<16>(st + A_ELEMS, wave, false);
         --seg_left;
     };
     f32x16 acc[RM][RN];
@@ -524,10 +527,13 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
             if ((ka->dbg >> type) & 1) {
                 // diagnostics: this node type's compute skipped
             } else if (type == N_GEMM) {
-                if (N.tile == TILE_W) gemm_job<TILE_W>(N, job, ka->eps, smem, wave, lane);
-                else if (N.tile == TILE_K2L) gemm_job<TILE_K2L>(N, job, ka->eps, smem, wave, lane);
-                else if (N.tile == TILE_ROW) gemm_job<TILE_ROW>(N, job, ka->eps, smem, wave, lane);
-                else gemm_job<TILE_K2>(N, job, ka->eps, smem, wave, lane);
+                const int st = (ka->dbg & kDbgWeightsL2) ? N.stat : 0;
+                if (N.tile == TILE_W) gemm_job<TILE_W>(N, job, ka->eps, smem, wave, lane, st);
+                else if (N.tile == TILE_K2L)
+                    gemm_job<TILE_K2L>(N, job, ka->eps, smem, wave, lane, st);
+                else if (N.tile == TILE_ROW)
+                    gemm_job<TILE_ROW>(N, job, ka->eps, smem, wave, lane, st);
+                else gemm_job<TILE_K2>(N, job, ka->eps, smem, wave, lane, st);
             } else if (type == N_PREP) {
                 prep_job(N, job, ka->x0, ka->eps, ka->t, smem);
             } else if (type == N_SUM) {

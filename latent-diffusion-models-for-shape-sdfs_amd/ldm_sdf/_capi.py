@@ -187,6 +187,7 @@ SIGNATURES = [
     ("ldm_train_step_config", _i, [_i, C.c_uint]),
     ("ldm_train_step_last_form", _i, []),
     ("ldm_denoiser_train_status", _i, [C.POINTER(Denoiser), _i, _vp, C.POINTER(C.c_uint), _vp]),
+    ("ldm_denoiser_train_ws_init", _i, [C.POINTER(Denoiser), _i, _vp, _vp]),
     ("ldm_denoiser_train_dag_describe", _i, [C.POINTER(Denoiser), C.POINTER(Sched), _i, _vp,
                                              C.POINTER(DenoiserGrads), C.POINTER(AdamwTensor),
                                              _i, C.c_char_p, _sz]),

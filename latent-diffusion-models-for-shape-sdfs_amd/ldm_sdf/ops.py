@@ -621,7 +621,13 @@ def train_workspace(desc: capi.Denoiser, B: int, device) -> torch.Tensor:
         raise capi.LdmError("ldm_denoiser_train_ws_bytes: unsupported denoiser shape")
     ws = torch.empty(n + 256, device=device, dtype=torch.uint8)
     off = (-ws.data_ptr()) % 256
-    return ws[off:off + n]
+    ws = ws[off:off + n]
+    # a fresh allocation may lie where a freed workspace did: zero its sync words and drop the
+    # host's record of a job table uploaded there (ldm_denoiser_train_ws_init)
+    capi.check(capi.load().ldm_denoiser_train_ws_init(C.byref(desc), int(B), ws.data_ptr(),
+                                                      capi.stream_handle(ws.device)),
+               "ldm_denoiser_train_ws_init")
+    return ws
 
 
 def denoiser_train_step(desc: capi.Denoiser, sched_desc: capi.Sched, x0: torch.Tensor,

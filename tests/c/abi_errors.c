@@ -134,9 +134,12 @@ int main(void) {
         for (int i = 0; i < 16; ++i) {
             t[i].p = fake(); t[i].g = gs[i]; t[i].m = fake(); t[i].v = fake();
             t[i].rows = rows[i]; t[i].cols = cols[i];
-            if (rows[i] > 1) t[i].p_bf16 = fake();
-            if (i == 0 || i == 4 || i == 6 || (i >= 8 && i < 12)) t[i].p_bf16_t = fake();
         }
+        /* the bf16 working copies ARE the descriptor's weights (as ldm_sdf.train builds it) */
+        t[0].p_bf16 = (void*)w.w_in; t[0].p_bf16_t = (void*)w.wt_in; t[2].p_bf16 = (void*)w.w_t1;
+        t[4].p_bf16 = (void*)w.w_t2; t[4].p_bf16_t = (void*)w.wt_t2; t[6].p_bf16 = (void*)w.w_out;
+        t[6].p_bf16_t = (void*)w.wt_out;
+        for (int k = 0; k < 4; ++k) { t[8 + k].p_bf16 = (void*)w.w_blk[k]; t[8 + k].p_bf16_t = (void*)w.wt_blk[k]; }
         static char buf[1 << 20];
         void* saved = fake();
         for (int B = 1; B <= 1000; B = B < 64 ? B * 4 : B + 312) {
@@ -145,10 +148,15 @@ int main(void) {
             EXPECT(rc == 0);
             const char* nd = strstr(buf, "nodes ");
             EXPECT(nd != NULL && atoi(nd + 6) >= 45);   /* 4 blocks: ~50 nodes */
+            /* weight operands marked for L2 loads, hand-offs (wt 0) not */
+            EXPECT(strstr(buf, " wt 2 ") != NULL && strstr(buf, " wt 0 ") != NULL);
         }
         EXPECT(ldm_denoiser_train_dag_describe(&w, &sc, 1000, saved, &g, t, 16, buf, 64) == 0);
         EXPECT_ERR(ldm_denoiser_train_dag_describe(&w, &sc, 0, saved, &g, t, 16, buf, 64));
         EXPECT_ERR(ldm_denoiser_train_dag_describe(NULL, &sc, 10, saved, &g, t, 16, buf, 64));
+        EXPECT_ERR(ldm_denoiser_train_ws_init(NULL, 10, saved, NULL));
+        EXPECT_ERR(ldm_denoiser_train_ws_init(&w, 0, saved, NULL));
+        EXPECT_ERR(ldm_denoiser_train_ws_init(&w, 10, NULL, NULL));
     }
 
     /* generic linear / GEMM / conv / misc */

@@ -136,12 +136,14 @@ def _dag_flags(v):
     return fl(v)
 
 
+@pytest.mark.parametrize("flags", [0x100, 0x200])
 @pytest.mark.parametrize("M", [1000, 37])
-def test_dag_claim_scheduler_bitwise(dev, form, M):
-    """The claim scheduler (a workgroup takes only READY jobs, chain list first; train_dag.hip,
-    kDbgClaim) computes the same step bit for bit: the schedule never changes an arithmetic."""
+def test_dag_claim_scheduler_bitwise(dev, form, M, flags):
+    """The claim scheduler (0x100: a workgroup takes only READY jobs, chain list first;
+    train_dag.hip, kDbgClaim) and the weight operands loaded through the L2 (0x200,
+    kDbgWeightsL2) compute the same step bit for bit: neither changes an arithmetic."""
     ref = _run(dev, "launches", M=M)
-    _dag_flags(0x100)
+    _dag_flags(flags)
     try:
         got = _run(dev, "dag", M=M)
     finally:
