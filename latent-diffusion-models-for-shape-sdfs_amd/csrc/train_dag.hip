@@ -384,7 +384,7 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
 }
 
 // Diagnostic build only (-DDAG_TRACE=1, scripts/trace_dag.py): per queue entry the workgroup that
-// ran it and the s_memrealtime stamps (100 MHz) of its dequeue, of its inputs being ready and of
+// ran it (and its XCD) and the s_memrealtime stamps (100 MHz) of its dequeue, of its inputs being ready and of
 // its completion (counters raised); per workgroup its start and exit.
 #ifndef DAG_TRACE
 #define DAG_TRACE 0
@@ -581,7 +581,9 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
             }
 #if DAG_TRACE
             if (threadIdx.x == 0) {
-                g_dag_trace[tr_idx][0] = (uint64_t)(unsigned)e << 32 | blockIdx.x;
+                // low word: the XCD the workgroup runs on (HW_REG_XCC_ID, read-only) << 16 | blockIdx
+                const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+                g_dag_trace[tr_idx][0] = (uint64_t)(unsigned)e << 32 | xcc << 16 | blockIdx.x;
                 g_dag_trace[tr_idx][1] = tr_deq;
                 g_dag_trace[tr_idx][2] = tr_rdy;
                 g_dag_trace[tr_idx][3] = __builtin_amdgcn_s_memrealtime();

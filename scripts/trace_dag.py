@@ -84,7 +84,8 @@ e = ent[:n_ent]
 e = e[e[:, 3] > 0]
 code = (e[:, 0] >> np.uint64(32)).astype(np.int64)
 node = code >> 16
-wg = (e[:, 0] & np.uint64(0xffffffff)).astype(np.int64)
+wg = (e[:, 0] & np.uint64(0xffff)).astype(np.int64)
+xcc = ((e[:, 0] >> np.uint64(16)) & np.uint64(15)).astype(np.int64)
 T0 = wgs[:, 0].min()
 deq, rdy, done = [(e[:, k].astype(np.int64) - T0) / 100.0 for k in (1, 2, 3)]      # us
 span = (wgs[:, 1].max() - T0) / 100.0
@@ -92,6 +93,13 @@ print(f"M={M} flags {hex(FLAGS)}: step wall {wall * 1e6:.1f} us (50 steps), trac
       f"{span:.1f} us, grid {grid}, jobs traced {len(e)} of {n_ent}; workgroup starts spread "
       f"{(wgs[:, 0].max() - T0) / 100:.1f} us, exits {(wgs[:, 1].min() - T0) / 100:.1f}.."
       f"{span:.1f} us")
+# the queue mapping assumes workgroup b runs on XCD b % 8 (round-robin dispatch)
+wx = {}
+for w_, x_ in zip(wg.tolist(), xcc.tolist()):
+    wx[w_] = x_
+bad = sum(1 for w_, x_ in wx.items() if x_ != w_ % 8)
+print(f"XCC_ID of {len(wx)} workgroups: {bad} differ from blockIdx % 8; per XCD "
+      f"{np.bincount(np.array(list(wx.values()), dtype=np.int64), minlength=8).tolist()}")
 print(" node type  jobs  nk    first_deq  first_rdy  last_done   compute_us  wait_us   "
       "(means per job)")
 for i in sorted(nodes):
