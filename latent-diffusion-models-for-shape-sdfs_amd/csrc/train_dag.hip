@@ -54,7 +54,11 @@ typedef const __attribute__((address_space(4))) ldm_gemm_prob_t KProb;
 // path's 8-wave tile at ~47 and 12 waves per CU at ~70 (profiles/r05n): the per-CU operand
 // stream scales with the waves issuing it, and fence-free hand-offs need one workgroup per CU.
 constexpr int NW = kThreads / 64, kWgPerCu = 1;
-constexpr int kLdsBytes = 128 * 1024;
+// LDS per workgroup (the ring): 128 KiB; DAG_LDS_KB=160 (A/B builds) deepens every ring
+#ifndef DAG_LDS_KB
+#define DAG_LDS_KB 128
+#endif
+constexpr int kLdsBytes = DAG_LDS_KB * 1024;
 template <int CFG>
 struct TileCfg {
     static constexpr int BM = CFG == TILE_W ? 128 : 64;
@@ -63,11 +67,13 @@ struct TileCfg {
     static constexpr int KB = CFG == TILE_K2L ? 128 : 64;      // k per ring stage
     static constexpr int WR = 2, WC = NW / KG / WR;             // waves per group: WR x WC
     static constexpr int RM = BM / WR / 32, RN = BN / WC / 32;  // 32 x 32 blocks per wave
-    static constexpr int STAGES = CFG == TILE_W || CFG == TILE_K2L ? 4 : CFG == TILE_ROW ? 5 : 8;
     static constexpr int A_ELEMS = BM * KB, STAGE_ELEMS = (BM + BN) * KB;
     typedef TileSrc<BM, NW, KB> SrcA;
     typedef TileSrc<BN, NW, KB> SrcB;
     static constexpr int G = SrcA::NP + SrcB::NP;               // DMA pieces per wave per stage
+    // as many stages as the LDS holds (128 KiB: TILE_K2 8, TILE_ROW 5, TILE_W / TILE_K2L 4)
+    static constexpr int STAGES_LDS = kLdsBytes / (STAGE_ELEMS * 2);
+    static constexpr int STAGES = STAGES_LDS < 63 / G + 1 ? STAGES_LDS : 63 / G + 1;
     static_assert(STAGES * STAGE_ELEMS * 2 <= kLdsBytes, "ring fits");
     static_assert((STAGES - 1) * G <= 63, "vmcnt immediate");
     static_assert(RM >= 1 && RN >= 1 && WC >= 1, "wave grid");
