@@ -498,11 +498,10 @@ def config5(args, rank, world, dev, group, gen):
             "bound": "launch-chain", "achieved": sps, "peak": 1.0 / model_step,
             "unit": "steps/s", "frac": sps * model_step, "launches_per_step": 18,
             "node_ns": node["node_ns"], "node_grid": node["grid"], "source": node["source"],
-            "measured_in_this_run": False,
+            "measured_in_this_run": True,
             "note": "a launch-chain MODEL, not a hardware roofline: peak = 1 / (18 x the latency "
                     "of one dependent node of a captured chain of empty kernels at the convs' "
-                    "grid size, measured by scripts/microbench/graph_chain_latency.hip on an "
-                    "MI355X in an earlier run, read from `source`); frac = that model step time / "
+                    "grid size, measured in this run on this GPU); frac = that model step time / "
                     "the measured step time of the default (graph) path"}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)
@@ -535,21 +534,19 @@ def bench_decode_b1(args, rank, world, dev, group, decoder, desc, gen):
 
 
 def graph_node_latency(grid: int = 128):
-    """One dependent hipGraph node's latency (an empty 256-thread kernel of ``grid``
-    workgroups in a captured 18 000-launch chain) measured by
-    scripts/microbench/graph_chain_latency.hip on an MI355X, from the newest
-    profiles/*/graph_node_latency.json; None when absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "graph_node_latency.json")))
-    if not files:
+    """One dependent hipGraph node's latency, measured in THIS run: an empty 256-thread kernel of
+    ``grid`` workgroups in a captured chain of 3600 launches, median of 5 replays
+    (``ldm_dev_graph_node_latency``, csrc/unet.hip; the standalone form is
+    scripts/microbench/graph_chain_latency.hip).  None if the call fails."""
+    import ctypes as C
+    from ldm_sdf import _capi as capi
+    fn = capi.load().ldm_dev_graph_node_latency
+    fn.restype, fn.argtypes = C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+    v = C.c_float(0.0)
+    if fn(int(grid), 3600, 5, C.byref(v)) != 0 or not v.value > 0:
         return None
-    try:
-        rows = [json.loads(l) for l in open(files[-1]) if l.strip().startswith("{")]
-        row = min(rows, key=lambda r: abs(r["grid"] - grid))
-    except (OSError, ValueError, KeyError):
-        return None
-    return {"node_ns": row["node_ns_median"], "grid": row["grid"],
-            "source": os.path.relpath(files[-1], ROOT)}
+    return {"node_ns": float(v.value), "grid": int(grid),
+            "source": "ldm_dev_graph_node_latency, measured in this run"}
 
 
 def free_port() -> int:
