@@ -331,12 +331,15 @@ class SlabTimer:
 
 def run_decode_steps(slab, B: int, N: int, *, steps: int, warmup: int, world: int, group,
                      device: torch.device, out: torch.Tensor, sync=None,
-                     shapes_per_group=None, on_timed=None, local=None) -> float:
+                     shapes_per_group=None, on_timed=None, local=None,
+                     step_events=None) -> float:
     """The bench's per-rank step loop (shared with the gloo test, tests/test_bench_gloo.py):
     ``warmup`` untimed steps, then barrier + sync, ``steps`` timed steps, sync + barrier, and
     the MAX of the per-rank elapsed times (all-reduce; ``local``, a list, receives this rank's
     own).  One step = the (sharded) decode of B
-    shapes on an N^3 grid into ``out``; ``slab(k0, k1, dst, b0, b1)`` computes a slab."""
+    shapes on an N^3 grid into ``out``; ``slab(k0, k1, dst, b0, b1)`` computes a slab.
+    ``step_events`` (a list, GPU only): receives one (start, end) HIP event pair per timed step,
+    recorded on the current stream around it (per-step hipEvent times, median)."""
     from ldm_sdf.dist import decode_sharded
     sync = sync or (lambda: None)
 
@@ -354,9 +357,16 @@ def run_decode_steps(slab, B: int, N: int, *, steps: int, warmup: int, world: in
     sync()
     if on_timed:
         on_timed()
+    ev = step_events is not None and device.type == "cuda"
     t0 = time.perf_counter()
     for _ in range(steps):
+        if ev:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         step()
+        if ev:
+            e1.record()
+            step_events.append((e0, e1))
     sync()
     if world > 1:
         dist.barrier(group)
@@ -368,6 +378,17 @@ def run_decode_steps(slab, B: int, N: int, *, steps: int, warmup: int, world: in
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
         elapsed = float(tt)
     return elapsed
+
+
+def event_summary(pairs) -> dict:
+    """Per-step HIP event times (ms) of the timed steps: median, min, max, mean, count."""
+    ms = sorted(a.elapsed_time(b) for a, b in pairs)
+    if not ms:
+        return None
+    return {"median_ms": ms[len(ms) // 2] if len(ms) % 2 else 0.5 * (ms[len(ms) // 2 - 1] +
+                                                                        ms[len(ms) // 2]),
+            "min_ms": ms[0], "max_ms": ms[-1], "mean_ms": sum(ms) / len(ms), "n": len(ms),
+            "source": "hipEvent pair per timed step on the decode stream"}
 
 
 def rank_breakdown(step_ms: float, kernel_ms: float, group, device) -> dict:
@@ -489,20 +510,34 @@ def config5(args, rank, world, dev, group, gen):
            "unet_sample_steps_per_s": sps, "unet_batch_per_rank": nl,
            "unet_path": "hipGraph of 1000 steps x 18 ldm_conv1d launches (direct staging)",
            "unet_conv_weight_bytes_per_step": wbytes}
-    # the graph path's bound: 18 dependent launches per step, each at least one dependent graph
-    # node (the conv grids are 64-128 workgroups at B = 1: ldm_conv1d's tile rule)
-    node = graph_node_latency(128 if nl <= 2 else 512)
+    # roofline of the sampler step from its algorithmic work (unet.step_cost): the convs'
+    # FLOPs against the fp32 MFMA peak (v_mfma_f32_16x16x4f32: fp32 activations, bf16 weights
+    # widened) and their bytes against HBM; the larger of the two times is the bound.  Both
+    # are far below the measured step: it is a chain of 18 dependent launches (DESIGN.md §9;
+    # the launch-chain model of scripts/microbench/graph_chain_latency.hip is reported beside,
+    # as a model, not as the roofline)
+    cost = unet.step_cost(nl)
+    t_mfma = cost["flops"] / (PEAK_TFLOPS["fp32"] * 1e12)
+    t_hbm = cost["bytes"] / 8e12
+    mf = t_mfma >= t_hbm
+    res["unet_roofline"] = {
+        "bound": "mfma" if mf else "hbm",
+        "achieved": sps * (cost["flops"] / 1e12 if mf else cost["bytes"] / 1e9),
+        "peak": PEAK_TFLOPS["fp32"] if mf else 8000.0, "unit": "TFLOP/s" if mf else "GB/s",
+        "frac": sps * (t_mfma if mf else t_hbm),
+        "flops_per_step": cost["flops"], "bytes_per_step": cost["bytes"],
+        "hbm_frac": sps * t_hbm, "mfma_fp32_frac": sps * t_mfma,
+        "note": "algorithmic FLOPs / bytes of the 18 convs of one step at this batch "
+                "(UNet1DDenoiser.step_cost) x steps/s, against the fp32 MFMA peak the convs "
+                "run on and HBM; the step is launch-chain-bound, far from either"}
+    node = committed_graph_node_latency()
     if node is not None:
-        model_step = 18 * node["node_ns"] * 1e-9
-        res["unet_roofline"] = {
-            "bound": "launch-chain", "achieved": sps, "peak": 1.0 / model_step,
-            "unit": "steps/s", "frac": sps * model_step, "launches_per_step": 18,
-            "node_ns": node["node_ns"], "node_grid": node["grid"], "source": node["source"],
-            "measured_in_this_run": True,
-            "note": "a launch-chain MODEL, not a hardware roofline: peak = 1 / (18 x the latency "
-                    "of one dependent node of a captured chain of empty kernels at the convs' "
-                    "grid size, measured in this run on this GPU); frac = that model step time / "
-                    "the measured step time of the default (graph) path"}
+        res["unet_launch_chain_model"] = {
+            "steps_per_s": 1.0 / (18 * node * 1e-9), "node_ns": node, "launches_per_step": 18,
+            "frac": sps * 18 * node * 1e-9,
+            "source": "profiles/r04a/graph_node_latency.json (scripts/microbench/"
+                      "graph_chain_latency.hip, empty-kernel chain)",
+            "note": "a MODEL (18 x one dependent graph node of empty kernels), not a roofline"}
     if rank == 0 and not args.no_cpu:
         res["unet_cpu_baseline"] = cpu_baseline_unet(min(5.0, args.cpu_seconds), nl)
     return res
@@ -511,18 +546,21 @@ def config5(args, rank, world, dev, group, gen):
 def bench_decode_b1(args, rank, world, dev, group, decoder, desc, gen):
     """SURVEY §8(d) "B = 1 for the headline number": one shape's ``--grid``^3 decode (16.8 M
     queries at 256^3), z-slab over the ranks, ``--dtype``; kernel time from HIP events on its
-    stream; max-over-ranks wall time of 3 timed decodes after 1 warm-up."""
+    stream; §8(d)'s method: 3 warm-up and 10 timed decodes, the max-over-ranks wall time of the
+    10 and the MEDIAN of the per-decode hipEvent times."""
     from ldm_sdf import ops
     N = args.grid
     lat1 = torch.randn(1, 256, device=dev, generator=gen) * 0.1
     out1 = torch.empty(1, N, N, N, device=dev)
     slab = SlabTimer(desc, lambda: ops.decoder_fold(desc, lat1), N,
                      torch.cuda.current_stream(dev))
-    reps = 3
-    el = run_decode_steps(slab, 1, N, steps=reps, warmup=1, world=world, group=group,
+    reps = 10
+    ev = []
+    el = run_decode_steps(slab, 1, N, steps=reps, warmup=3, world=world, group=group,
                           device=dev, out=out1, sync=torch.cuda.synchronize,
-                          on_timed=lambda: setattr(slab, "timed", True))
+                          on_timed=lambda: setattr(slab, "timed", True), step_events=ev)
     kms, qpl = slab.kernel_stats()
+    evs = event_summary(ev)
     ach = FLOPS_PER_QUERY * qpl / (kms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
     return {"metric": f"SDF queries/sec, ONE shape on a {N}^3 grid", "value": N ** 3 * reps / el,
@@ -530,23 +568,22 @@ def bench_decode_b1(args, rank, world, dev, group, decoder, desc, gen):
             "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
                          "frac": ach / peak, "kernel": "dec_fs_kernel",
                          "queries_per_launch": qpl, "avg_launch_ms": kms},
-            "target_ms_at_40pct": N ** 3 * FLOPS_PER_QUERY / (0.4 * peak * 1e12) * 1e3}
+            "target_ms_at_40pct": N ** 3 * FLOPS_PER_QUERY / (0.4 * peak * 1e12) * 1e3,
+            "step_time_events": evs,
+            "value_from_median": N ** 3 / (evs["median_ms"] * 1e-3) if evs else None}
 
 
-def graph_node_latency(grid: int = 128):
-    """One dependent hipGraph node's latency, measured in THIS run: an empty 256-thread kernel of
-    ``grid`` workgroups in a captured chain of 3600 launches, median of 5 replays
-    (``ldm_dev_graph_node_latency``, csrc/unet.hip; the standalone form is
-    scripts/microbench/graph_chain_latency.hip).  None if the call fails."""
-    import ctypes as C
-    from ldm_sdf import _capi as capi
-    fn = capi.load().ldm_dev_graph_node_latency
-    fn.restype, fn.argtypes = C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
-    v = C.c_float(0.0)
-    if fn(int(grid), 3600, 5, C.byref(v)) != 0 or not v.value > 0:
+def committed_graph_node_latency():
+    """The per-node latency of a dependent hipGraph chain of empty kernels, as measured by
+    scripts/microbench/graph_chain_latency.hip (profiles/r04a/graph_node_latency.json, median
+    over its grid sizes); None when absent."""
+    f = os.path.join(ROOT, "profiles", "r04a", "graph_node_latency.json")
+    try:
+        rows = [json.loads(l) for l in open(f) if l.strip().startswith("{")]
+        v = sorted(float(r["node_ns_median"]) for r in rows if "node_ns_median" in r)
+    except (OSError, ValueError, KeyError):
         return None
-    return {"node_ns": float(v.value), "grid": int(grid),
-            "source": "ldm_dev_graph_node_latency, measured in this run"}
+    return v[len(v) // 2] if v else None
 
 
 def free_port() -> int:
@@ -607,10 +644,12 @@ def main():
     slab = SlabTimer(desc, lambda: ops.decoder_fold(desc, latents), N, stream)
     spg = args.shapes_per_group or None
     local = []
+    step_ev = []
     elapsed = run_decode_steps(slab, B, N, steps=args.steps, warmup=args.warmup, world=world,
                                group=group, device=dev, out=out, sync=torch.cuda.synchronize,
                                shapes_per_group=spg,
-                               on_timed=lambda: setattr(slab, "timed", True), local=local)
+                               on_timed=lambda: setattr(slab, "timed", True), local=local,
+                               step_events=step_ev)
     slab.timed = False
     kms, qpl = slab.kernel_stats()
     multi = None
@@ -652,6 +691,7 @@ def main():
                          "flops_per_query": FLOPS_PER_QUERY,
                          "queries_per_launch": qpl, "avg_launch_ms": kms,
                          "launches_per_step": len(slab.events) // max(1, args.steps)},
+            "step_time_events": event_summary(step_ev),
             "decode_b1": b1,
         }
         if multi is not None:

@@ -224,7 +224,11 @@ int ldm_q_sample_loss(const ldm_sched_t* sc, const float* x0, const float* eps,
                       float* loss_out, float* grad_out, ldm_stream_t s);
 /* One whole DDPM training step's forward + backward (Alg. 1 without the optimizer):
  * q_sample -> net -> eps-MSE (loss_out[0]) -> every gradient, the loss gradient fused into
- * the out-projection's epilogue.  17 launches, no host synchronisation (graph-capturable). */
+ * the out-projection's epilogue.  The data-parallel step (the update waits for the gradient
+ * all-reduce).  Form per ldm_train_step_config: the launch path (17 launches, no host
+ * synchronisation, graph-capturable) or the one-launch job DAG without AdamW nodes (its first
+ * call per configuration uploads the table: one stream synchronisation, not inside a capture);
+ * the same bits either way. */
 int ldm_denoiser_train_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0,
                             const float* eps, const int32_t* t, int B, void* saved,
                             const ldm_denoiser_grads_t* grads, float* loss_out, ldm_stream_t s);

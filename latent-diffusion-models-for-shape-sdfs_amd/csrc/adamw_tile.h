@@ -29,6 +29,9 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
     const int rows = T.rows, cols = T.cols;
     const int tcn = (cols + 63) / 64;
     const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
+    LDM_DASSERT(tl >= 0 && r0 < rows);                  // the tile lies inside the tensor
+    // extents (wt_store.h): fp32 p, g, m, v and the bf16 copies, rows x cols each
+    const uint32_t x4 = ext_bytes(rows, cols, cols, 4), x2 = ext_bytes(rows, cols, cols, 2);
     const int cq = (tid & 15) * 4;
     const float decay = hy.decay, omb1 = hy.omb1, b2 = hy.b2, omb2 = hy.omb2, eps = hy.eps,
                 step_size = hy.step_size, bc2_sqrt = hy.bc2_sqrt;
@@ -47,22 +50,22 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         off[i] = (int64_t)r * cols + c0 + cq;
         if (mode == 2) {                          // the copies: the stored p only
             if (vec) {
-                p4[i] = vld_at<WT, f32x4>(P, off[i]);
+                p4[i] = vld_at<WT, f32x4>(P, x4, off[i]);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    p4[i][e] = vld_at<WT, float>(P, c0 + cq + e < cols ? off[i] + e : off[i]);
+                    p4[i][e] = vld_at<WT, float>(P, x4, c0 + cq + e < cols ? off[i] + e : off[i]);
             }
         } else if (vec) {
             p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
-            g4[i] = vld_at<WT, f32x4>(Gp, off[i]);     // (WT: the handed-off gradient, sc1)
+            g4[i] = vld_at<WT, f32x4>(Gp, x4, off[i]);     // (WT: the handed-off gradient, sc1)
             m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
             v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int64_t x = c0 + cq + e < cols ? off[i] + e : off[i];
-                p4[i][e] = P[x]; g4[i][e] = vld_at<WT, float>(Gp, x); m4[i][e] = M[x];
+                p4[i][e] = P[x]; g4[i][e] = vld_at<WT, float>(Gp, x4, x); m4[i][e] = M[x];
                 v4[i][e] = V[x];
             }
         }
@@ -86,27 +89,27 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         if (!rin) continue;
         if (vec) {
             if (mode != 2) {
-                vst_at<WT>(P, off[i], p4[i]);
-                vst_at<WT>(M, off[i], m4[i]);
-                vst_at<WT>(V, off[i], v4[i]);
+                vst_at<WT>(P, x4, off[i], p4[i]);
+                vst_at<WT>(M, x4, off[i], m4[i]);
+                vst_at<WT>(V, x4, off[i], v4[i]);
             }
             if (T.p_bf16 && mode != 1) {
                 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 w = {(unsigned)q[0] | ((unsigned)q[1] << 16),
                                  (unsigned)q[2] | ((unsigned)q[3] << 16)};
-                vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), off[i], w);
+                vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), x2, off[i], w);
             }
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (c0 + cq + e >= cols) continue;
                 if (mode != 2) {
-                    vst_at<WT>(P, off[i] + e, p4[i][e]);
-                    vst_at<WT>(M, off[i] + e, m4[i][e]);
-                    vst_at<WT>(V, off[i] + e, v4[i][e]);
+                    vst_at<WT>(P, x4, off[i] + e, p4[i][e]);
+                    vst_at<WT>(M, x4, off[i] + e, m4[i][e]);
+                    vst_at<WT>(V, x4, off[i] + e, v4[i][e]);
                 }
                 if (T.p_bf16 && mode != 1)
-                    vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), off[i] + e, q[e]);
+                    vst_at<WT>(reinterpret_cast<unsigned short*>(T.p_bf16), x2, off[i] + e, q[e]);
             }
         }
     }
@@ -125,13 +128,13 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
             w0[e] = (unsigned)sT[cl][rb + 2 * e] | ((unsigned)sT[cl][rb + 2 * e + 1] << 16);
             w1[e] = (unsigned)sT[cl][rb + 8 + 2 * e] | ((unsigned)sT[cl][rb + 9 + 2 * e] << 16);
         }
-        vst_at<WT>(dst, cr + r0 + rb, w0);
-        vst_at<WT>(dst, cr + r0 + rb + 8, w1);
+        vst_at<WT>(dst, x2, cr + r0 + rb, w0);
+        vst_at<WT>(dst, x2, cr + r0 + rb + 8, w1);
     } else {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int r = r0 + rb + e;
-            if (r < rows) vst_at<WT>(dst, cr + r, sT[cl][rb + e]);
+            if (r < rows) vst_at<WT>(dst, x2, cr + r, sT[cl][rb + e]);
         }
     }
 }

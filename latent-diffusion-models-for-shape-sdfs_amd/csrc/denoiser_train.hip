@@ -25,6 +25,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -458,25 +459,6 @@ extern "C" int ldm_denoiser_bwd(const ldm_denoiser_t* w, void* saved, const floa
     return finalize(L, grads, deps, nullptr, 1.f, st);
 }
 
-extern "C" int ldm_denoiser_train_step(const ldm_denoiser_t* w, const ldm_sched_t* sc,
-                                       const float* x0, const float* eps, const int32_t* t, int B,
-                                       void* saved, const ldm_denoiser_grads_t* grads,
-                                       float* loss_out, ldm_stream_t s) {
-    LDM_TRY(check_desc(w, B, true));
-    LDM_TRY(check_grads(w, grads));
-    LDM_REQUIRE(sc && sc->abi_version == LDM_ABI_VERSION && sc->sqrt_ab && sc->sqrt_1mab,
-                LDM_EINVAL, "ldm_denoiser_train_step: bad schedule");
-    LDM_REQUIRE(x0 && eps && t && saved && LDM_ALIGNED(saved, 256), LDM_EINVAL,
-                "ldm_denoiser_train_step: x0, eps, t and a 256-B aligned workspace are required");
-    const TrainWs L = layout(w, B, saved);
-    hipStream_t st = (hipStream_t)s;
-    const float n = (float)B * (float)w->D;
-    LDM_TRY(prep_inputs(w, L, x0, eps, t, sc, st));
-    LDM_TRY(forward(w, L, eps, nullptr, 2.f / n, st));
-    LDM_TRY(backward(w, L, grads, nullptr, st));
-    return finalize(L, grads, nullptr, loss_out, 1.f / n, st);
-}
-
 // ---- A9 head -------------------------------------------------------------------------------
 extern "C" int ldm_q_sample_loss(const ldm_sched_t* sc, const float* x0, const float* eps,
                                  const int32_t* t, int B, int D, float* xt_out,
@@ -681,11 +663,16 @@ struct DagHost {
     std::vector<uint32_t> entries;
 };
 
-// The uploaded tables, by device table address (entries are kept for the process: an async
-// upload reads them); ldm_denoiser_train_ws_init forgets one.
+// The uploaded tables, by device table address.  An entry's host copy is only read by its
+// upload, which synchronises before dag_step returns, so entries may go at any time after that:
+// ldm_denoiser_train_ws_init drops the one of its workspace, and the map is cleared when it
+// reaches kMaxCached entries (a workload that keeps allocating workspaces of new sizes stays
+// bounded; a dropped configuration re-uploads at its next step).  shared_ptr: a step in flight
+// on another thread keeps its entry alive.
 struct DagCache {
+    static constexpr size_t kMaxCached = 32;
     std::mutex mu;
-    std::unordered_map<const void*, DagHost*> by_table;
+    std::unordered_map<const void*, std::shared_ptr<DagHost>> by_table;
 };
 DagCache& dag_cache() {
     static DagCache c;
@@ -693,6 +680,132 @@ DagCache& dag_cache() {
 }
 
 constexpr bool kSplitU = false;     // U_k's AdamW as an early update + late copies (measured: off)
+
+// ---- operand extents vs the allocations (round 6, after the r05h illegal access) -----------
+// Every byte range a job of the table may touch -- each GEMM operand over its problem's rows and
+// leading dimension (ext_bytes, the same extents the kernel gives its buffer resources), the
+// prep outputs, the sums' partials, each AdamW tensor -- must lie inside ONE allocation the
+// caller handed over: the training workspace, a weight / bias / table of the descriptor, a
+// gradient, an AdamW tensor, the schedule.  A table that fails is refused (LDM_EINVAL, named
+// node and operand), so an indexing bug in the builder never reaches the GPU as a stray access.
+struct Region {
+    const char* p;
+    int64_t bytes;
+};
+struct Regions {
+    std::vector<Region> r;
+    void add(const void* p, int64_t bytes) {
+        if (p && bytes > 0) r.push_back({static_cast<const char*>(p), bytes});
+    }
+    bool holds(const void* p, int64_t bytes) const {
+        const char* c = static_cast<const char*>(p);
+        for (const Region& x : r)
+            if (c >= x.p && c + bytes <= x.p + x.bytes) return true;
+        return false;
+    }
+};
+
+int check_dag_extents(const dag::Table& T, const ldm_denoiser_t* w, const ldm_sched_t* sc,
+                      const TrainWs& L, const ldm_denoiser_grads_t* gr,
+                      const ldm_adamw_tensor_t* tensors, int n, const void* eps_tag) {
+    using namespace dag;
+    const int64_t D = w->D, H = w->H, TE = w->TE, Tn = w->T;
+    Regions R;
+    R.add(L.xt_b, (int64_t)L.bytes);                        // the workspace (xt_b is its start)
+    R.add(w->w_in, H * D * 2); R.add(w->w_t1, H * TE * 2); R.add(w->w_t2, H * H * 2);
+    R.add(w->w_out, D * H * 2); R.add(w->wt_in, D * H * 2); R.add(w->wt_t2, H * H * 2);
+    R.add(w->wt_out, H * D * 2);
+    R.add(w->b_in, H * 4); R.add(w->b_t1, H * 4); R.add(w->b_t2, H * 4); R.add(w->b_out, D * 4);
+    R.add(w->emb_table, Tn * TE * 4);
+    for (int k = 0; k < w->n_blocks; ++k) {
+        R.add(w->w_blk[k], H * 2 * H * 2); R.add(w->wt_blk[k], 2 * H * H * 2);
+        R.add(w->b_blk[k], H * 4);
+        R.add(gr->w_blk[k], H * 2 * H * 4); R.add(gr->b_blk[k], H * 4);
+    }
+    R.add(gr->w_in, H * D * 4); R.add(gr->b_in, H * 4); R.add(gr->w_t1, H * TE * 4);
+    R.add(gr->b_t1, H * 4); R.add(gr->w_t2, H * H * 4); R.add(gr->b_t2, H * 4);
+    R.add(gr->w_out, D * H * 4); R.add(gr->b_out, D * 4);
+    for (int i = 0; i < n; ++i) {
+        const ldm_adamw_tensor_t& t = tensors[i];
+        const int64_t e = (int64_t)t.rows * t.cols;
+        R.add(t.p, e * 4); R.add(t.g, e * 4); R.add(t.m, e * 4); R.add(t.v, e * 4);
+        R.add(t.p_bf16, e * 2); R.add(t.p_bf16_t, e * 2);
+    }
+    R.add(sc->sqrt_ab, (int64_t)sc->T * 4); R.add(sc->sqrt_1mab, (int64_t)sc->T * 4);
+    const char* what = nullptr;
+    int bad = -1;
+    auto need = [&](int node, const char* name, const void* p, int64_t bytes) {
+        if (!p || bytes <= 0 || bad >= 0 || p == eps_tag) return;   // eps: a launch argument
+        if (bytes >= (int64_t)kMaxExtent || !R.holds(p, bytes)) {
+            bad = node;
+            what = name;
+        }
+    };
+    for (int i = 0; i < T.n_nodes; ++i) {
+        const Node& nd = T.node[i];
+        if (nd.type == N_GEMM) {
+            const ldm_gemm_prob_t& P = nd.P;
+            const int64_t M = P.M, Nc = P.N, Mv = P.M_valid;
+            // the job grid covers the problem and no more than one tile beyond it
+            if ((int64_t)nd.tiles_m * tile_rows(nd.tile) < M ||
+                (int64_t)(nd.tiles_m - 1) * tile_rows(nd.tile) >= M ||
+                (int64_t)nd.tiles_n * tile_cols(nd.tile) < Nc ||
+                (int64_t)(nd.tiles_n - 1) * tile_cols(nd.tile) >= Nc || Mv > M) {
+                bad = i;
+                what = "job grid vs problem";
+            }
+            int64_t ks = 0;
+            for (int g = 0; g < P.n_seg; ++g) {
+                const ldm_gemm_seg_t& S = P.seg[g];
+                need(i, "A operand", S.A, ext_bytes(M, S.lda, S.K, 2));
+                need(i, "B operand", S.B, ext_bytes(Nc, S.ldb, S.K, 2));
+                if (S.K % 64 != 0) { bad = i; what = "segment K"; }
+                ks += S.K / 64;
+            }
+            if (ks != nd.nk && bad < 0) { bad = i; what = "k-steps"; }
+            need(i, "C", P.C, ext_bytes(Mv, P.ldc, Nc, 4));
+            need(i, "P", P.P, ext_bytes(Mv, P.ldp, Nc, 4));
+            if (P.mode != LDM_GEMM_ACCUM) need(i, "R", P.R, ext_bytes(Mv, P.ldr, Nc, 4));
+            need(i, "P_in", P.P_in, ext_bytes(Mv, P.ldp_in, Nc, 4));
+            need(i, "Rb", P.Rb, ext_bytes(Mv, P.ldrb, Nc, 2));
+            need(i, "Cb", P.Cb, ext_bytes(M, P.ldcb, Nc, 2));
+            need(i, "CbT", P.CbT, ext_bytes(Nc, P.ldct, M, 2));
+            need(i, "colsum", P.colsum, ext_bytes((M - 1) / 32 + 1, Nc, Nc, 4));
+            need(i, "loss_part", P.loss_part,
+                 ext_bytes((M - 1) / 32 + 1, (Nc + 31) / 32, (Nc + 31) / 32, 4));
+            need(i, "bias", P.bias, Nc * 4);
+        } else if (nd.type == N_PREP) {
+            need(i, "xt_b", nd.xt_b, ext_bytes(nd.Bp, nd.D, nd.D, 2));
+            need(i, "xt_T", nd.xt_T, ext_bytes(nd.D, nd.Bp, nd.Bp, 2));
+            need(i, "e_b", nd.e_b, ext_bytes(nd.Bp, nd.TE, nd.TE, 2));
+            need(i, "e_T", nd.e_T, ext_bytes(nd.TE, nd.Bp, nd.Bp, 2));
+            need(i, "emb", nd.emb, Tn * nd.TE * 4);
+            if ((int64_t)nd.tiles_m * kBand < nd.Bp && bad < 0) { bad = i; what = "prep bands"; }
+        } else if (nd.type == N_SUM) {
+            need(i, "sum src", nd.src, ext_bytes(nd.rows, nd.ld, nd.len, 4));
+            need(i, "sum dst", nd.dst, (int64_t)nd.len * 4);
+        } else if (nd.type == N_ADAM) {
+            if (nd.adam < 0 || nd.adam >= n) {
+                if (bad < 0) { bad = i; what = "AdamW tensor index"; }
+                continue;
+            }
+            const ldm_adamw_tensor_t& t = tensors[nd.adam];
+            if ((int64_t)nd.tiles_m * 64 < t.rows ||
+                nd.col_off + nd.nk > (t.cols + 63) / 64) {
+                if (bad < 0) { bad = i; what = "AdamW tiles vs tensor"; }
+            }
+        }
+        if (nd.type == N_SUM && nd.adam >= 0 && nd.adam < n &&
+            (int64_t)tensors[nd.adam].rows * tensors[nd.adam].cols != nd.len && bad < 0) {
+            bad = i;
+            what = "bias sum length vs its AdamW tensor";
+        }
+    }
+    LDM_REQUIRE(bad < 0, LDM_EINVAL,
+                "train dag: node %d: %s lies outside every allocation the step was given "
+                "(or exceeds 2 GiB); table refused", bad, what ? what : "?");
+    return 0;
+}
 
 // Builds the job table of one step; returns 1 (and builds nothing) when this configuration has
 // no DAG form -- the caller then runs the launch path.
@@ -940,6 +1053,8 @@ int build_dag(const ldm_denoiser_t* w, const ldm_sched_t* sc, const TrainWs& L,
         }
         nd.stat = sa | sb;
     }
+    // every operand range inside an allocation the caller handed over (round 6)
+    LDM_TRY(check_dag_extents(T, w, sc, L, gr, tensors, n, kEps));
     // every dependency points at an earlier node (the deadlock-freedom argument)
     for (int c = 0; c < T.n_nodes; ++c)
         for (int d = 0; d < T.node[c].ndep; ++d)
@@ -1016,11 +1131,13 @@ int dag_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, co
     const size_t tb = sizeof(dag::Table);
     h = fnv(h, &tb, sizeof(tb));
     DagCache& dc = dag_cache();
-    DagHost* hc = nullptr;
+    std::shared_ptr<DagHost> hc;
     {
         std::lock_guard<std::mutex> g(dc.mu);
-        DagHost*& slot = dc.by_table[L.dag_table];
-        if (!slot) slot = new DagHost();       // kept for the process: the async upload reads it
+        if (dc.by_table.size() >= DagCache::kMaxCached && !dc.by_table.count(L.dag_table))
+            dc.by_table.clear();
+        std::shared_ptr<DagHost>& slot = dc.by_table[L.dag_table];
+        if (!slot) slot = std::make_shared<DagHost>();
         hc = slot;
     }
     if (hc->hash != h) {
@@ -1062,6 +1179,43 @@ int dag_step(const ldm_denoiser_t* w, const ldm_sched_t* sc, const float* x0, co
 
 }  // namespace
 }  // namespace ldm
+
+// The forward + backward without the optimizer (the data-parallel step: the update waits for
+// the gradient all-reduce).  The form follows ldm_train_step_config like the step with AdamW:
+// the one-launch job DAG built WITHOUT AdamW nodes (no tensor table: the bias sums only store
+// their gradients) or the launches.  Bit-identical either way (tests/test_gpu_train_dag.py).
+extern "C" int ldm_denoiser_train_step(const ldm_denoiser_t* w, const ldm_sched_t* sc,
+                                       const float* x0, const float* eps, const int32_t* t, int B,
+                                       void* saved, const ldm_denoiser_grads_t* grads,
+                                       float* loss_out, ldm_stream_t s) {
+    LDM_TRY(check_desc(w, B, true));
+    LDM_TRY(check_grads(w, grads));
+    LDM_REQUIRE(sc && sc->abi_version == LDM_ABI_VERSION && sc->sqrt_ab && sc->sqrt_1mab,
+                LDM_EINVAL, "ldm_denoiser_train_step: bad schedule");
+    LDM_REQUIRE(x0 && eps && t && saved && LDM_ALIGNED(saved, 256), LDM_EINVAL,
+                "ldm_denoiser_train_step: x0, eps, t and a 256-B aligned workspace are required");
+    TrainCfg& cfg = train_cfg();
+    if (cfg.form == LDM_TRAIN_DAG || (cfg.form == LDM_TRAIN_AUTO && dag_auto(B))) {
+        const float h7[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const int r = dag_step(w, sc, x0, eps, t, B, saved, grads, loss_out, nullptr, 0, h7,
+                               nullptr, cfg.spin, cfg.dbg, (hipStream_t)s);
+        if (r == 0) {
+            cfg.last = LDM_TRAIN_DAG;
+            return 0;
+        }
+        if (r != 1) return r;
+        LDM_REQUIRE(cfg.form != LDM_TRAIN_DAG, LDM_ENOSYS, "ldm_denoiser_train_step: no "
+                    "one-launch form for this configuration (LDM_TRAIN_DAG was required)");
+    }
+    cfg.last = LDM_TRAIN_LAUNCHES;
+    const TrainWs L = layout(w, B, saved);
+    hipStream_t st = (hipStream_t)s;
+    const float n = (float)B * (float)w->D;
+    LDM_TRY(prep_inputs(w, L, x0, eps, t, sc, st));
+    LDM_TRY(forward(w, L, eps, nullptr, 2.f / n, st));
+    LDM_TRY(backward(w, L, grads, nullptr, st));
+    return finalize(L, grads, nullptr, loss_out, 1.f / n, st);
+}
 
 extern "C" int ldm_adamw_multi(const ldm_adamw_tensor_t* tensors, int n, double lr,
                                double beta1, double beta2, double eps, double weight_decay,
@@ -1193,7 +1347,7 @@ extern "C" int ldm_denoiser_train_ws_init(const ldm_denoiser_t* w, int B, void* 
         DagCache& dc = dag_cache();
         std::lock_guard<std::mutex> g(dc.mu);
         auto it = dc.by_table.find(L.dag_table);
-        if (it != dc.by_table.end()) it->second->hash = 0;     // re-uploaded by the next step
+        if (it != dc.by_table.end()) dc.by_table.erase(it);     // re-built by the next step
     }
     const hipError_t e =
         hipMemsetAsync(L.dag_sync, 0, dag::sync_bytes(dag::kMaxCounters), (hipStream_t)s);
@@ -1245,10 +1399,14 @@ extern "C" int ldm_denoiser_train_dag_describe(const ldm_denoiser_t* w, const ld
     return 0;
 }
 
-// Diagnostics only (not in include/ldm_sdf.h): skip the compute of DAG node types (bit t: type t
-// of train_dag.h NodeType; the jobs still wait and signal) and / or add the release / acquire
-// fences to every hand-off (bit 7, dag::kDbgFences).
+#ifdef LDM_DEV_KNOBS
+// Development build only (`make DEV=1`; not in include/ldm_sdf.h, not exported by the product
+// library): skip the compute of DAG node types (bit t: type t of train_dag.h NodeType; the jobs
+// still wait and signal), add the release / acquire fences to every hand-off (bit 7,
+// dag::kDbgFences), the claim scheduler (kDbgClaim), weight operands through the L2
+// (kDbgWeightsL2).
 extern "C" int ldm_dev_train_dag_flags(unsigned flags) {
     train_cfg().dbg = flags;
     return 0;
 }
+#endif

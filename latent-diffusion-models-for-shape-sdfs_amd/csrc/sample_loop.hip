@@ -533,15 +533,26 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 // all its layers -- 0 own granules landed, 1 the workgroup's staging barrier (the slowest wave's
 // granules), 2 the row dot products, 3 the reduce-scatter, 4 epilogue + publish -- and writes
 // them at its end (g_sl_stamp[workgroup][wave]); slot 5 counts the layers.
-// ON in the product build (round 5): the loop built WITH its stamps ran 86.5-88.2k steps/s at
-// B = 8 against 72.0-74.4k without, in four runs on three boxes (profiles/r05j, r05k, r05o:
-// the stamped sample_loop.o linked with the product's other objects, libldm_slstamp, is the
-// fast one; the marks alone without the layer counter, SL_MARKS = 31, are not).  The codegen
-// differs in the loop's index arithmetic (the stamped build does it in SALU, s_mul_i32 x 11,
-// where the other uses VALU v_mul_lo_u32 / v_mad); the stamps themselves cost a few SALU
-// instructions per layer.  -DSL_STAMP=0 builds the loop without them.
+// Diagnostic builds only (-DSL_STAMP=1).  Round 5 shipped them ON because the stamped build ran
+// 86.5-88.2k steps/s at B = 8 against 72.0-74.4k without; its explanation (index products in
+// SALU instead of VALU) was wrong -- those v_mul_lo_u32 sit in the barrier form's arrival code,
+// which the tagged hand-offs never run.  Round 6 found the real difference in the assembly: both
+// builds SPILLED (116-132 bytes of scratch at 255-256 VGPRs), and each step reloaded 5-6 of a
+// residual block's register-resident weight vectors from scratch, one serial
+// scratch_load + s_waitcnt vmcnt(0) after another; the stamps merely moved one reload.  The fix
+// is SL_LDSBLK below: no spills at all, with or without stamps (tests/test_sampler_codegen.py
+// pins it).
 #ifndef SL_STAMP
-#define SL_STAMP 1
+#define SL_STAMP 0
+#endif
+// Residual blocks whose weights live in LDS instead of registers (the LAST SL_LDSBLK blocks):
+// the 4 blocks' register-resident weights (128 VGPRs) + the loop's state overflowed the 256
+// VGPRs a wave has at 2 waves per SIMD, so the compiler spilled weight vectors and reloaded them
+// serially every step.  One block in LDS (64 KiB per workgroup, read as 8 ds_read_b128 per wave
+// per step) frees 32 VGPRs: no scratch at all.  Same arithmetic (the
+// lane's 8 bf16 weights, the same fma chain), so the loop stays bit-identical to the graph path.
+#ifndef SL_LDSBLK
+#define SL_LDSBLK 1
 #endif
 // SL_MARKS (A/B builds only): a bit mask of the marks to keep without the rest of the stamps
 #ifndef SL_MARKS
@@ -586,10 +597,10 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     constexpr int NV = R * MBX, LB = NV >= 16 ? 4 : NV >= 8 ? 3 : NV >= 4 ? 2 : 1;
     constexpr int NT = 64 * NWV;
     static_assert(RO * MBX <= NV, "out-projection values fit the reduce-scatter");
-    // LDS: [4] flags | xs [MBX][H] | in-proj weights [4 waves][R][NJD][64 lanes] u32x4 |
-    //      out-proj weights [4 waves][RO][NJH][64] u32x4.  The 4 residual blocks' weights (256
-    //      VGPRs of bf16 pairs) live in registers; the two projections' in LDS (registers
-    //      would spill).
+    // LDS: [4] flags | xs [MBX][H] | in-proj weights [8 waves][R][NJD][64 lanes] u32x4 |
+    //      out-proj weights [8 waves][RO][NJH][64] u32x4 | the last SL_LDSBLK blocks' weights
+    //      [SL_LDSBLK][8 waves][R][NJH][64] u32x4.  The other residual blocks' weights (32 VGPRs
+    //      of bf16 pairs each) live in registers.
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int* ok = reinterpret_cast<int*>(smem);
     float* xs = smem + 4;
@@ -616,9 +627,23 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     const int gw = (int)s_rank * NWV + wave;                  // 0 .. 32 NWV - 1
     const int row0 = gw * R, orow0 = gw * RO;
 
-    u32x4 wb[NB][R][NJH];
+    constexpr int NBR = NB - SL_LDSBLK;                  // blocks with register weights
+    static_assert(NBR >= 1 && NBR <= NB, "SL_LDSBLK in 0..3");
+    u32x4 wb[NBR][R][NJH];
 #pragma unroll
-    for (int k = 0; k < NB; ++k) load_rows_bf16<R, NJH>(wb[k], a.w_blk[k], row0, 2 * H, H, lane);
+    for (int k = 0; k < NBR; ++k) load_rows_bf16<R, NJH>(wb[k], a.w_blk[k], row0, 2 * H, H, lane);
+    // blocks NBR.. in LDS: [block][wave][R][NJH][64 lanes] u32x4, past the projections
+    u32x4* lwb = lwi + NWV * R * NJD * 64 + NWV * RO * NJH * 64;
+#pragma unroll
+    for (int k = NBR; k < NB; ++k) {
+        u32x4 wl[R][NJH];
+        load_rows_bf16<R, NJH>(wl, a.w_blk[k], row0, 2 * H, H, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < NJH; ++j)
+                lwb[((((k - NBR) * NWV + wave) * R + r) * NJH + j) * 64 + lane] = wl[r][j];
+    }
     {
         u32x4 wi[R][NJD], wo[RO][NJH];
         load_rows_bf16<R, NJD>(wi, a.w_in, row0, D, D, lane);
@@ -736,8 +761,13 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                 return;
             }
             float v[NV];
-            rows_partial<R, R, NJH, MBX>(v, [&](int r, int j) { return wb[k][r][j]; }, xs, H,
-                                         lane);
+            if constexpr (k < NBR)
+                rows_partial<R, R, NJH, MBX>(v, [&](int r, int j) { return wb[k][r][j]; }, xs,
+                                             H, lane);
+            else
+                rows_partial<R, R, NJH, MBX>(v, [&](int r, int j) {
+                    return lwb[((((k - NBR) * NWV + wave) * R + r) * NJH + j) * 64 + lane];
+                }, xs, H, lane);
             stp.mark(2);
             const float acc = reduce_scatter<NV>(v, lane);
             stp.mark(3);
@@ -835,7 +865,8 @@ int cur_dev() {
 size_t replica_lds(int D, int MBX) {
     const int H = 1024, W = kRepWaves, R = H / (32 * W), RO = D / (32 * W);
     const int NJD = (D + 511) / 512, NJH = 2;
-    return 16 + (size_t)MBX * H * 4 + (size_t)W * (R * NJD + RO * NJH) * 64 * 16;
+    return 16 + (size_t)MBX * H * 4 +
+           (size_t)W * (R * NJD + RO * NJH + SL_LDSBLK * R * NJH) * 64 * 16;
 }
 
 template <int D_, int MBX>

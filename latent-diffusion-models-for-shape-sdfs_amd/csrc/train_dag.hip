@@ -159,6 +159,8 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
     const int tn_n = N.tiles_n;
     const int tm = job / tn_n, tn = job - tm * tn_n;
     const int m0 = tm * BM, n0 = tn * BN;
+    // (DEBUG builds) the job's tile lies inside its problem, its k-steps are the segments'
+    LDM_DASSERT(tm >= 0 && m0 < P.M && n0 < P.N && P.n_seg >= 1 && N.nk % KS == 0);
     const int grp = wave / (NW / KG), wl = wave % (NW / KG);   // k-group, wave in the group
     const int wr = wl / WC, wc = wl % WC, r32 = lane & 31, h = lane >> 5;
     const int nk = N.nk / KS, kgp = N.kgp / KS;     // in ring stages (TILE_K2L: kgp 2 -> 1)
@@ -166,7 +168,9 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
     typename C::SrcB srcB;
     int seg = 0, seg_left = 0, qi = 0;
     auto seat = [&](int sg) {
+        LDM_DASSERT(sg < P.n_seg);
         const __attribute__((address_space(4))) ldm_gemm_seg_t& S = P.seg[sg];
+        LDM_DASSERT(S.K > 0 && S.K % KB == 0);
         srcA.init(reinterpret_cast<const unsigned short*>(S.A), S.lda, m0, P.M, wave, lane);
         srcB.init(reinterpret_cast<const unsigned short*>(S.B), S.ldb, n0, P.N, wave, lane);
         seg_left = S.K / KB;
@@ -319,6 +323,8 @@ __device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, con
     unsigned short* rows_out = is_x ? N.xt_b : N.e_b;
     unsigned short* cols_out = is_x ? N.xt_T : N.e_T;
     unsigned short (*tile)[66] = reinterpret_cast<unsigned short (*)[66]>(smem);
+    LDM_DASSERT(band * kBand < Bp && c0 < width);
+    const uint32_t xrows = ext_bytes(Bp, width, width, 2), xcols = ext_bytes(width, Bp, Bp, 2);
     for (int i = threadIdx.x; i < kBand * 16; i += kThreads) {
         const int r = i >> 4, cl = 4 * (i & 15), c = c0 + cl, b = band * kBand + r;
         if (c >= width || b >= Bp) continue;
@@ -340,14 +346,14 @@ __device__ __forceinline__ void prep_job(KNode& N, int job, const float* x0, con
             q[u] = to_bf16(v);
             tile[r][cl + u] = q[u];
         }
-        vst_at<true>(rows_out, (int64_t)b * width + c,
+        vst_at<true>(rows_out, xrows, (int64_t)b * width + c,
                   u32x2{(unsigned)q[0] | (unsigned)q[1] << 16, (unsigned)q[2] | (unsigned)q[3] << 16});
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * (kBand / 4); i += kThreads) {
         const int cc = i / (kBand / 4), r = 4 * (i % (kBand / 4));
         if (c0 + cc >= width || band * kBand + r >= Bp) continue;
-        vst_at<true>(cols_out, (int64_t)(c0 + cc) * Bp + band * kBand + r,
+        vst_at<true>(cols_out, xcols, (int64_t)(c0 + cc) * Bp + band * kBand + r,
                   u32x2{(unsigned)tile[r][cc] | (unsigned)tile[r + 1][cc] << 16,
                         (unsigned)tile[r + 2][cc] | (unsigned)tile[r + 3][cc] << 16});
     }
@@ -363,6 +369,7 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
     const float scale = N.scale;
     float* dst = N.dst ? N.dst : loss_out;
     const int ti = N.adam;
+    const uint32_t xsrc = ext_bytes(rows, ld, len, 4), xdst = ext_bytes(1, len, len, 4);
     for (int c = threadIdx.x; c < len; c += kThreads) {
         const float* src = N.src;                // (uniform base for the sc1 loads)
         float s = 0.f;
@@ -370,21 +377,22 @@ __device__ __forceinline__ void sum_job(KTab* tab, KNode& N, float* loss_out,
         for (; r + 8 <= rows; r += 8) {
             float v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = vld_at<true, float>(src, (int64_t)(r + u) * ld + c);
+            for (int u = 0; u < 8; ++u) v[u] = vld_at<true, float>(src, xsrc, (int64_t)(r + u) * ld + c);
 #pragma unroll
             for (int u = 0; u < 8; ++u) s += v[u];
         }
-        for (; r < rows; ++r) s += vld_at<true, float>(src, (int64_t)r * ld + c);
+        for (; r < rows; ++r) s += vld_at<true, float>(src, xsrc, (int64_t)r * ld + c);
         const float g = scale * s;
-        vst_at<true>(dst, c, g);
+        vst_at<true>(dst, xdst, c, g);
         if (ti >= 0) {
             const __attribute__((address_space(4))) ldm_adamw_tensor_t& T = tab->tensor[ti];
             float p = T.p[c], m = T.m[c], v = T.v[c];
             adamw_update(p, g, m, v, hy.decay, hy.omb1, hy.b2, hy.omb2, hy.eps, hy.step_size,
                          hy.bc2_sqrt);
-            vst_at<true>(T.p, c, p);
-            vst_at<true>(T.m, c, m);
-            vst_at<true>(T.v, c, v);
+            LDM_DASSERT((int64_t)T.rows * T.cols == len);
+            vst_at<true>(T.p, xdst, c, p);
+            vst_at<true>(T.m, xdst, c, m);
+            vst_at<true>(T.v, xdst, c, v);
         }
     }
 }
@@ -551,6 +559,7 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void train_dag_kernel(LaunchArg
                 // transpose tile; a half without a tile still meets the tile's barrier
                 const int tr = job / N.tiles_n, tg = job - tr * N.tiles_n;
                 const int tl0 = tr * ((T.cols + 63) / 64) + N.col_off;
+                LDM_DASSERT(tr * 64 < T.rows && N.col_off + N.nk <= (T.cols + 63) / 64);
                 const int half = threadIdx.x >> 8;
                 unsigned short(&sT)[64][64 + 8] =
                     *reinterpret_cast<unsigned short(*)[64][64 + 8]>(smem + half * 64 * 72);

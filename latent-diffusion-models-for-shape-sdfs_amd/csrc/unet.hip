@@ -1006,61 +1006,3 @@ extern "C" int ldm_dev_conv_stamps(uint64_t* host, unsigned* n) {
     return 0;
 }
 #endif
-
-// Diagnostics (product build): one dependent hipGraph node's latency, the floor of the UNet
-// sampler's graph path -- an empty 256-thread kernel of `grid` workgroups, `nodes`
-// launches captured in a chain on a private stream, replayed once untimed and `reps` times
-// between events; *node_ns = the median replay time / nodes.  bench.py's config5.unet_roofline
-// measures its peak with this in the run itself (scripts/microbench/graph_chain_latency.hip is
-// the standalone form).
-namespace ldm {
-namespace {
-__global__ __launch_bounds__(256) void graph_empty_node(int* sink, int tag) {
-    if (tag < 0 && sink) sink[threadIdx.x] = tag;   // never taken: keeps the argument live
-}
-}  // namespace
-}  // namespace ldm
-
-extern "C" int ldm_dev_graph_node_latency(int grid, int nodes, int reps, float* node_ns) {
-    using namespace ldm;
-    LDM_REQUIRE(grid >= 1 && grid <= 65535 && nodes >= 1 && nodes <= 100000 && reps >= 1 &&
-                    reps <= 64 && node_ns,
-                LDM_EINVAL, "ldm_dev_graph_node_latency: grid 1..65535, nodes 1..1e5, reps 1..64");
-    hipStream_t s = nullptr;
-    hipGraph_t g = nullptr;
-    hipGraphExec_t ge = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    std::vector<float> ns;
-    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreate(&e0);
-    if (e == hipSuccess) e = hipEventCreate(&e1);
-    if (e == hipSuccess) e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
-    if (e == hipSuccess) {
-        for (int i = 0; i < nodes; ++i)
-            hipLaunchKernelGGL(graph_empty_node, dim3(grid), dim3(256), 0, s, (int*)nullptr, i);
-        const hipError_t el = hipGetLastError();
-        e = hipStreamEndCapture(s, &g);
-        if (e == hipSuccess) e = el;
-    }
-    if (e == hipSuccess) e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-    if (e == hipSuccess) e = hipGraphLaunch(ge, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    for (int r = 0; r < reps && e == hipSuccess; ++r) {
-        e = hipEventRecord(e0, s);
-        if (e == hipSuccess) e = hipGraphLaunch(ge, s);
-        if (e == hipSuccess) e = hipEventRecord(e1, s);
-        if (e == hipSuccess) e = hipEventSynchronize(e1);
-        float ms = 0.f;
-        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-        if (e == hipSuccess) ns.push_back(ms * 1e6f / (float)nodes);
-    }
-    if (ge) (void)hipGraphExecDestroy(ge);
-    if (g) (void)hipGraphDestroy(g);
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    if (s) (void)hipStreamDestroy(s);
-    LDM_REQUIRE(e == hipSuccess, (int)e, "ldm_dev_graph_node_latency: %s", hipGetErrorString(e));
-    std::sort(ns.begin(), ns.end());
-    *node_ns = ns[ns.size() / 2];
-    return 0;
-}

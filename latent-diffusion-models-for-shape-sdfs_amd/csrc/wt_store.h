@@ -6,24 +6,61 @@
 // "stores of each flavour", release ~1.7 us clean, ~6.5 us with 16 KB freshly dirtied per
 // block; profiles/r05g: the releases took a third of the step).  The launch kernels keep plain
 // stores (their launch boundary writes back once).
+//
+// Bounds (round 6, after the r05h illegal access): every access names the EXTENT
+// of the operand it touches, in bytes from `base` (ext_bytes below: the problem's rows x leading
+// dimension, never more).  The write-through forms build their buffer resource with
+// num_records = that extent, so an access past the operand is DROPPED by the hardware (a load
+// returns 0) instead of landing in a neighbouring tensor or faulting; the offset is formed in
+// 64 bits and an offset outside [0, extent) is sent to `extent` itself (dropped) rather than
+// truncated into range.  `make DEBUG=1` (LDM_DEBUG) turns every such access into a trap with
+// its location (LDM_DASSERT), for the plain forms too.  The host side (build_dag) refuses a job
+// table whose operand extents do not lie inside the allocations the caller handed over.
 #pragma once
 #include "ldm_internal.h"
 
 namespace ldm {
 
-// base[idx] = v (V: 2-, 4-, 8- or 16-byte value).  The write-through form is a raw buffer store
-// with the sc1 cache policy (aux bit 4) on a buffer resource over `base`: the compiler sees the
-// store (its waits and scheduling account for it), `base` should be wave-uniform (else the
-// compiler makes a waterfall loop of it) and idx * sizeof(T) < 2 GiB.
+constexpr uint32_t kMaxExtent = 0x7ffffff0u;      // buffer offsets are 32-bit: extents < 2 GiB
+
+// Bytes of a row-major operand of `rows` rows, leading dimension `ld` elements, whose rows are
+// used up to column `cols`, element size `esz`: ((rows - 1) ld + cols) esz (0 for no rows),
+// clamped to kMaxExtent (the host check keeps every extent below it).
+__host__ __device__ __forceinline__ uint32_t ext_bytes(int64_t rows, int64_t ld, int64_t cols,
+                                                       int esz) {
+    const int64_t b = rows <= 0 ? 0 : ((rows - 1) * ld + cols) * esz;
+    return (uint32_t)(b < (int64_t)kMaxExtent ? b : (int64_t)kMaxExtent);
+}
+
+// byte offset of element idx of T, or `nbytes` (out of range: the access is dropped) when the
+// V-sized access would not lie inside [0, nbytes)
+template <typename V, typename T>
+__device__ __forceinline__ uint32_t checked_off(int64_t idx, uint32_t nbytes) {
+    const int64_t off = idx * (int64_t)sizeof(T);
+    const bool in = off >= 0 && off + (int64_t)sizeof(V) <= (int64_t)nbytes;
+    LDM_DASSERT(in);
+    return in ? (uint32_t)off : nbytes;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ext_rsrc(const void* base, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes,
+                                             0x00020000);
+}
+
+// base[idx] = v (V: 2-, 4-, 8- or 16-byte value) inside an operand of `nbytes` bytes.  The
+// write-through form is a raw buffer store with the sc1 cache policy (aux bit 4) on a buffer
+// resource over [base, base + nbytes): the compiler sees the store (its waits and scheduling
+// account for it); `base` should be wave-uniform (else the compiler makes a waterfall loop).
 template <bool WT, typename V, typename T>
-__device__ __forceinline__ void vst_at(T* base, int64_t idx, const V& v) {
+__device__ __forceinline__ void vst_at(T* base, uint32_t nbytes, int64_t idx, const V& v) {
     if constexpr (!WT) {
+        LDM_DASSERT(idx >= 0 && (idx * (int64_t)sizeof(T) + (int64_t)sizeof(V)) <= (int64_t)nbytes);
+        (void)nbytes;
         *reinterpret_cast<V*>(base + idx) = v;
     } else {
         constexpr int kSc1 = 16;
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)base, (short)0, 0x7ffffff0, 0x00020000);
-        const int off = (int)(idx * (int64_t)sizeof(T));
+        const __amdgpu_buffer_rsrc_t r = ext_rsrc(base, nbytes);
+        const int off = (int)checked_off<V, T>(idx, nbytes);
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
         typedef unsigned u4 __attribute__((ext_vector_type(4)));
         if constexpr (sizeof(V) == 16) {
@@ -41,19 +78,20 @@ __device__ __forceinline__ void vst_at(T* base, int64_t idx, const V& v) {
     }
 }
 
-// v = base[idx], plain or (WT) an sc1 raw buffer load (bypasses this CU's L1: reads what
-// another CU stored write-through and drained before its signal -- the MI355X guide's
-// inter-workgroup hand-off with sc1 stores and sc1 loads, no release / acquire fences; one
-// workgroup per CU).  `base` wave-uniform, idx * sizeof(T) < 2 GiB.
+// v = base[idx] inside an operand of `nbytes` bytes, plain or (WT) an sc1 raw buffer load
+// (bypasses this CU's L1: reads what another CU stored write-through and drained before its
+// signal -- the MI355X guide's inter-workgroup hand-off with sc1 stores and sc1 loads, no
+// release / acquire fences; one workgroup per CU).  `base` wave-uniform.
 template <bool WT, typename V, typename T>
-__device__ __forceinline__ V vld_at(const T* base, int64_t idx) {
+__device__ __forceinline__ V vld_at(const T* base, uint32_t nbytes, int64_t idx) {
     if constexpr (!WT) {
+        LDM_DASSERT(idx >= 0 && (idx * (int64_t)sizeof(T) + (int64_t)sizeof(V)) <= (int64_t)nbytes);
+        (void)nbytes;
         return *reinterpret_cast<const V*>(base + idx);
     } else {
         constexpr int kSc1 = 16;
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)base, (short)0, 0x7ffffff0, 0x00020000);
-        const int off = (int)(idx * (int64_t)sizeof(T));
+        const __amdgpu_buffer_rsrc_t r = ext_rsrc(base, nbytes);
+        const int off = (int)checked_off<V, T>(idx, nbytes);
         if constexpr (sizeof(V) == 16) {
             return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
         } else if constexpr (sizeof(V) == 8) {

@@ -14,6 +14,7 @@ path in the product (the CPU restatement is oracle/, test infrastructure only).
 from __future__ import annotations
 
 import warnings
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -37,9 +38,19 @@ BF16_MAX_LATENT_RMS = 0.2
 # SURVEY §8(c)'s fp16 bound -- at 1.0; larger latents also approach fp16's 65504 range): above
 # it "auto" decodes in exact fp32
 FP16_MAX_LATENT_RMS = 1.0
-# "auto" costs one device->host read of the latents' RMS; it is cached per latents tensor
-# (identity, storage, in-place version), so repeated decodes of the same latents do not sync
-_AUTO_CACHE: Dict[tuple, str] = {}
+# "auto" costs one device->host read of the latents' RMS; it is cached per latents tensor, so
+# repeated decodes of the same latents do not sync.  An entry holds a WEAK reference to the
+# tensor it was computed for and counts as a hit only while that same object is alive and
+# unmodified (storage, in-place version, shape): CPython reuses the id of a freed tensor and the
+# caching allocator its block, so (id, data_ptr, _version) alone matched a NEW tensor with other
+# values.  Writes made behind torch's back (through a C-ABI data_ptr) do not bump
+# _version: after such a write, pass an explicit dtype or call clear_auto_cache().
+_AUTO_CACHE: Dict[int, tuple] = {}
+
+
+def clear_auto_cache() -> None:
+    """Forget every cached dtype="auto" decision."""
+    _AUTO_CACHE.clear()
 
 
 def resolve_decode_dtype(dtype: str, latents: torch.Tensor) -> str:
@@ -49,18 +60,17 @@ def resolve_decode_dtype(dtype: str, latents: torch.Tensor) -> str:
     explicit dtype to keep a decode free of host synchronisation (graph capture)."""
     if dtype != "auto":
         return dtype
-    key = (id(latents), latents.data_ptr(), latents._version, tuple(latents.shape),
-           str(latents.device))
-    hit = _AUTO_CACHE.get(key)
-    if hit is not None:
-        return hit
+    key = (latents.data_ptr(), latents._version, tuple(latents.shape), str(latents.device))
+    ent = _AUTO_CACHE.get(id(latents))
+    if ent is not None and ent[0]() is latents and ent[1] == key:
+        return ent[2]
     lat = latents.float().reshape(latents.shape[0] if latents.dim() > 1 else 1, -1)
     rms = float(lat.pow(2).mean(dim=1).sqrt().max())
     pick = "bf16" if rms <= BF16_MAX_LATENT_RMS else "fp16" if rms <= FP16_MAX_LATENT_RMS \
         else "fp32"
     if len(_AUTO_CACHE) > 64:
         _AUTO_CACHE.clear()
-    _AUTO_CACHE[key] = pick
+    _AUTO_CACHE[id(latents)] = (weakref.ref(latents), key, pick)
     return pick
 
 
@@ -318,6 +328,18 @@ class TrainState:
         for n in names:
             if tuple(ck["masters"][n].shape) != tuple(denoiser.params[n].shape):
                 raise ValueError(f"{path}: {n} has shape {tuple(ck['masters'][n].shape)}")
+        # which parameter each tensor of a caller's optimizer is (by identity, before the
+        # denoiser's tensors are replaced): its param_groups are re-pointed at the loaded
+        # masters below, so optimizer.step() updates what train() trains
+        opt_names = None
+        if optimizer is not None:
+            ident = {id(t): n for n, t in denoiser.params.items()}
+            opt_names = []
+            for g in optimizer.param_groups:
+                if any(id(p) not in ident for p in g["params"]):
+                    raise ValueError("TrainState.load: the optimizer holds tensors that are not "
+                                     "this denoiser's parameters")
+                opt_names.append([ident[id(p)] for p in g["params"]])
         denoiser.params = {n: ck["masters"][n].to(torch.float32) for n in names}
         denoiser.to_device(device)               # also drops packs, tables, workspaces
         denoiser.invalidate()
@@ -333,6 +355,9 @@ class TrainState:
         if optimizer is not None:
             if "optimizer" not in ck:
                 raise ValueError(f"{path}: no optimizer state saved")
+            for g, gn in zip(optimizer.param_groups, opt_names):
+                g["params"] = [st.masters[n] for n in gn]
+            optimizer.state.clear()               # keyed by the old tensors; reloaded below
             optimizer.load_state_dict(ck["optimizer"])
             st.optimizer = optimizer
         if generator is not None:
@@ -342,14 +367,47 @@ class TrainState:
         return st
 
 
+def _reduce_grads(denoiser, grads, loss, B_local: int, global_batch: Optional[int], group):
+    """Data-parallel gradient of the GLOBAL batch's mean loss: each rank's gradients (and loss)
+    are of its local mean over B_local rows, so rank r scales by B_r / B before one summing
+    all-reduce of the flat gradient buffer -- exact for uneven shards (a plain mean over ranks
+    is not).  The loss rides in the same all-reduce when the buffer has its ``__loss`` slot.
+    ``global_batch`` None: the plain mean over ranks."""
+    world, _ = ldist.world_and_rank(group)
+    if world == 1:
+        return loss
+    ts = [grads[n] for n in denoiser.names()]
+    lslot = grads.get("__loss")
+    if lslot is not None:
+        lslot.copy_(loss.reshape(1))
+        ts.append(lslot)
+    if global_batch is None:
+        ldist.allreduce_mean_(ts, group=group)
+    else:
+        ldist.allreduce_weighted_(ts, B_local / float(global_batch), group=group)
+    if lslot is None:
+        loss = loss.clone()
+        if global_batch is None:
+            ldist.allreduce_mean_([loss], group=group)
+        else:
+            ldist.allreduce_weighted_([loss], B_local / float(global_batch), group=group)
+        return loss
+    return lslot.clone()
+
+
 def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
                t: torch.Tensor, eps: torch.Tensor, *, dtype: str = "bf16",
                grads: Optional[Dict[str, torch.Tensor]] = None,
-               group=None) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+               group=None, global_batch: Optional[int] = None
+               ) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
     """One DDPM training forward/backward (Alg. 1): q_sample -> eps_hat -> MSE -> grads.
     ``dtype`` "fp32": exact fp32 GEMMs; "bf16": bf16 weights and matrix-core GEMMs with
-    operands rounded to bf16 (fp32 accumulate).  Returns (loss [1], grads) -- gradients are
-    averaged over ranks when a group is given."""
+    operands rounded to bf16 (fp32 accumulate).  Returns (loss [1], grads).  With a group the
+    gradients and the loss are those of the mean over the GLOBAL batch of ``global_batch`` rows
+    (each rank weighted by its share; None: the plain mean over ranks).  bf16 runs the fused
+    forward + backward C call, ``ldm_denoiser_train_step``, in the form
+    ``ops.train_step_config`` selects -- the one-launch job DAG (without its AdamW nodes: the
+    update waits for the all-reduce) or the launch path."""
     device = x0.device
     dev = denoiser.device_pack(dtype, device, with_tables=False)
     sd = schedule.device(device)
@@ -364,7 +422,7 @@ def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
         ops.denoiser_train_step(dev["desc"], sd["desc"], x0.float().contiguous(),
                                 eps.float().contiguous(), t.to(torch.int32).contiguous(), ws,
                                 denoiser.grads_struct(grads), loss)
-        ldist.allreduce_mean_([grads[n] for n in denoiser.names()], group=group)
+        loss = _reduce_grads(denoiser, grads, loss, B, global_batch, group)
         return loss, grads
     xt = ops.q_sample(sd["desc"], x0.contiguous(), eps.contiguous(), t.to(torch.int32).contiguous())
     cp = capi.COMPUTE_CODES[dtype]
@@ -372,7 +430,7 @@ def train_step(denoiser: MLPDenoiser, schedule: DDPMSchedule, x0: torch.Tensor,
                                              compute=cp)
     loss, g_out = ops.eps_mse_loss(eps_hat, eps.contiguous())
     ops.denoiser_backward_train(denoiser, dev, sv, g_out, grads, compute=cp)
-    ldist.allreduce_mean_([grads[n] for n in denoiser.names()], group=group)
+    loss = _reduce_grads(denoiser, grads, loss, x0.shape[0], global_batch, group)
     return loss, grads
 
 
@@ -421,8 +479,11 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
         state.hparams = dict(lr=lr, weight_decay=weight_decay)
     # gradients live in ONE flat buffer (one view per parameter): the data-parallel all-reduce
     # then reduces that buffer in place, with no per-step concatenation or copy back
+    # (+ a one-float "__loss" slot at its end: at world > 1 the loss rides in the gradients'
+    # all-reduce)
     grads = state.adam_grads if state.adam_grads is not None else \
-        ldist.flat_buffers({n: tuple(v.shape) for n, v in state.masters.items()}, device)[1]
+        ldist.flat_buffers({**{n: tuple(v.shape) for n, v in state.masters.items()},
+                            "__loss": (1,)}, device)[1]
     T = schedule.T
     # single rank, built-in AdamW: the fused C step (no gradient all-reduce to wait for)
     fused = dtype == "bf16" and state.optimizer is None and world == 1 and fused_step
@@ -471,7 +532,7 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
             state.losses.append(loss)
             continue
         loss, grads = train_step(denoiser, schedule, x0, t[lo:hi], eps[lo:hi], dtype=dtype,
-                                 grads=grads, group=group)
+                                 grads=grads, group=group, global_batch=batch)
         if state.optimizer is not None:          # caller-supplied torch optimizer
             for n, p in state.masters.items():
                 p.grad = grads[n]

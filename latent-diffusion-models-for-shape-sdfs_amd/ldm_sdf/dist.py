@@ -201,6 +201,13 @@ def allreduce_sum_(tensors, group=None) -> None:
     _allreduce_(tensors, group, mean=False)
 
 
+def allreduce_weighted_(tensors, weight: float, group=None) -> None:
+    """``sum_r weight_r * t_r`` in place on every rank (one bucket, one all-reduce): the
+    data-parallel gradient of a loss that is a mean over a global batch sharded unevenly --
+    rank r passes ``weight = B_r / B`` for gradients of its local mean (train())."""
+    _allreduce_(tensors, group, mean=False, pre_scale=weight)
+
+
 def flat_buffers(shapes: Dict[str, Tuple[int, ...]], device, dtype=torch.float32
                  ) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
     """One flat buffer and a view of it per named shape, in order, each view starting at a
@@ -239,7 +246,7 @@ def _flat_base(tensors: List[torch.Tensor]) -> Optional[torch.Tensor]:
     return base[:pos]
 
 
-def _allreduce_(tensors, group, mean: bool) -> None:
+def _allreduce_(tensors, group, mean: bool, pre_scale: Optional[float] = None) -> None:
     world, _ = world_and_rank(group)
     if world == 1:
         return
@@ -248,11 +255,15 @@ def _allreduce_(tensors, group, mean: bool) -> None:
     if flat is not None:
         # views of one persistent buffer: reduce it in place (padding between views is zero on
         # every rank and stays zero)
+        if pre_scale is not None:
+            flat.mul_(pre_scale)
         dist.all_reduce(flat, group=group)
         if mean:
             flat.div_(world)
         return
     flat = torch.cat([t.reshape(-1) for t in tensors])
+    if pre_scale is not None:
+        flat.mul_(pre_scale)
     dist.all_reduce(flat, group=group)
     if mean:
         flat.div_(world)

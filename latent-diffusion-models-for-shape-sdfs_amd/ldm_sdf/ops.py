@@ -686,9 +686,11 @@ TRAIN_FORMS = {"auto": 0, "launches": 1, "dag": 2}
 
 def train_step_config(form: str = "auto", spin_limit: int = 0) -> None:
     """Form of ``denoiser_train_step_adamw`` on the current device (``ldm_train_step_config``):
-    "auto" (the one-launch DAG step whenever the configuration has one), "launches" (one launch
-    per GEMM group + AdamW), "dag" (required).  Same bits either way.  ``spin_limit``: polls
-    before a DAG wait gives up (0 = default; tiny values exercise the timeout path)."""
+    "auto" (the form measured faster for the configuration: denoiser_train.hip ``dag_auto``),
+    "launches" (one launch per GEMM group + AdamW), "dag" (the one-launch step, required).  Same
+    bits either way.  ``spin_limit``: MICROSECONDS (s_memrealtime time) one DAG dependency wait
+    may take before the launch gives up (0 = the default, 2 s; 1 us makes waits give up at once
+    and exercises the timeout path)."""
     capi.check(capi.load().ldm_train_step_config(TRAIN_FORMS[form], int(spin_limit)),
                "ldm_train_step_config")
 

@@ -80,6 +80,52 @@ class UNet1DDenoiser:
     def n_params(self) -> int:
         return sum(v.numel() for v in self.params.values())
 
+    def conv_list(self) -> List[Tuple[str, int, int, int, int, int, bool]]:
+        """The 18 convs of one forward, in launch order: (name, cin (all segments, the 1x1
+        shortcut's included as k=1 taps below), cout, k, L_in, L_out, identity residual)."""
+        c0, c1, c2 = self.C
+        D = self.D
+        out = [("conv_in", 1, c0, 3, D, D, False)]
+        lv = {0: (c0, D), 1: (c1, D // 2), 2: (c2, D // 4), 3: (c2, D // 4), 4: (c1, D // 2),
+              5: (c0, D)}
+
+        def res(i):
+            ci, co = unet_res_specs(self.C)[i]
+            L = lv[i][1]
+            out.append((f"res{i}.w1", ci, co, 3, L, L, False))
+            out.append((f"res{i}.w2", co, co, 3, L, L, ci == co))
+            if ci != co:
+                out.append((f"res{i}.ws", ci, co, 1, L, L, False))
+        res(0)
+        out.append(("down0", c0, c1, 3, D, D // 2, False))
+        res(1)
+        out.append(("down1", c1, c2, 3, D // 2, D // 4, False))
+        res(2)
+        res(3)
+        out.append(("up1", c2, c1, 3, D // 4, D // 2, False))
+        res(4)
+        out.append(("up0", c1, c0, 3, D // 2, D, False))
+        res(5)
+        out.append(("conv_out", c0, 1, 3, D, D, False))
+        return out
+
+    def step_cost(self, n: int, weight_bytes: int = 2) -> Dict[str, float]:
+        """Algorithmic work of one reverse step at batch ``n`` (bench.py config5.unet_roofline):
+        FLOPs = 2 n Cout L_out Cin k summed over the convs (the 1x1 shortcuts are segments of
+        their block's second conv: 18 launches); bytes = every weight once (``weight_bytes`` per
+        element) + every fp32 activation a conv reads (input window, identity residual) and
+        writes, + the latent in / out of the step."""
+        flops = 0
+        wbytes = 0
+        abytes = 0
+        for (_, ci, co, k, Lin, Lout, ident) in self.conv_list():
+            flops += 2 * n * co * Lout * ci * k
+            wbytes += weight_bytes * co * ci * k
+            abytes += 4 * n * (ci * Lin + co * Lout + (co * Lout if ident else 0))
+        return {"flops": float(flops), "bytes": float(wbytes + abytes),
+                "weight_bytes": float(wbytes), "activation_bytes": float(abytes),
+                "launches": 18}
+
     def invalidate(self) -> None:
         self._dev.clear()
 

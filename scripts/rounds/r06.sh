@@ -1,0 +1,53 @@
+#!/bin/bash
+# Round 6 GPU calls, one batch per argument (bash scripts/rounds/r06.sh <batch> <outdir>); every
+# step runs under its own time limit and the batch stops at the first failure.  Output goes to
+# gpurun_out/<outdir>/; the logs that back a DESIGN.md statement are copied to profiles/<outdir>/.
+#   guards   the one-launch training step against the product library and the DEBUG=1 library
+#            (LDM_DASSERT bounds traps, wt_store.h extents), then the whole GPU suite and smoke
+#   bench    the default bench and the rocprofv3 kernel-trace summary of the same command
+#   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
+#   decoder  the decoder part stamps (scripts/stamp_split.py on the FS_STAMP library)
+#   first    config 3's first call in a fresh process, with a kernel + HIP API trace
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+B=${1:?batch}
+O=gpurun_out/${2:?outdir}
+mkdir -p $O
+step() {   # name timeout cmd...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1
+  local rc=$?
+  echo "== $n rc $rc"; tail -${TAILN:-6} $O/$n.log
+  [ $rc -eq 0 ] || exit $rc
+}
+LIB=$PWD/latent-diffusion-models-for-shape-sdfs_amd/ldm_sdf
+PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+case $B in
+  guards)
+    TAILN=4 step dag_product 400 $PYT tests/test_gpu_train_dag.py
+    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step dag_debug 600 $PYT tests/test_gpu_train_dag.py
+    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step gemm_debug 600 $PYT tests/test_gpu_gemm.py tests/test_gpu_train_capi.py
+    TAILN=4 step pytest_gpu 900 $PYT tests -m gpu
+    step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+    ;;
+  bench)
+    TAILN=2 step bench 600 python -u bench.py
+    TAILN=3 step rocprof 900 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py
+    find $O/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/bench_kernel_stats.csv
+    head -12 $O/bench_kernel_stats.csv
+    ;;
+  sampler)
+    for L in ${SL_LIBS:?}; do
+      LDM_SDF_LIB=$LIB/$L TAILN=3 step sampler_${L%.so} 300 python -u scripts/sampler_time.py
+    done
+    ;;
+  decoder)
+    LDM_SDF_LIB=$LIB/${FS_LIB:-libldm_fsstamp.so} TAILN=40 step stamp_split 300 python -u scripts/stamp_split.py
+    ;;
+  first)
+    TAILN=20 step first_call 300 python -u scripts/config3_first_call.py
+    TAILN=3 step first_trace 600 rocprofv3 --kernel-trace --hip-runtime-trace --stats -d $O/first -o first --output-format csv -- python3 scripts/config3_first_call.py
+    ;;
+  *) echo "unknown batch $B"; exit 2 ;;
+esac

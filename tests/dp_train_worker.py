@@ -1,0 +1,45 @@
+"""World-N data-parallel train() worker for tests/test_gpu_train_dp.py (not a test module).
+
+Launched by the test as ``python -m torch.distributed.run --nproc-per-node N ...`` (a CHILD
+process of the test: nothing here replaces a GPU-initialised program); every rank uses cuda:0
+and the gloo backend (one GPU box), runs ``ldm_sdf.train`` on the same global batch with the
+group, and rank 0 writes the losses, parameters and the last step's gradients to ``out``."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "latent-diffusion-models-for-shape-sdfs_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def run(out: str, form: str, M: int, steps: int) -> None:
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser, ops
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    ldm_sdf.load_library()
+    ops.train_step_config(form)
+    model = MLPDenoiser(seed=11)
+    model.to_device(dev)
+    sch = ldm_sdf.DDPMSchedule()
+    lat = torch.randn(M, 256, generator=torch.Generator().manual_seed(5)).to(dev) * 0.5
+    gen = torch.Generator(device=dev).manual_seed(3)
+    st = ldm_sdf.train(model, sch, lat, steps=steps, batch=M, lr=1e-3, weight_decay=0.01,
+                       dtype="bf16", generator=gen, group=dist.group.WORLD)
+    torch.cuda.synchronize()
+    if dist.get_rank() == 0:
+        torch.save({"losses": list(st.losses), "form": ops.train_step_last_form(),
+                    "world": dist.get_world_size(),
+                    "params": {n: t.cpu() for n, t in model.params.items()},
+                    "grads": {n: g.cpu() for n, g in st.adam_grads.items()}}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    run(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))

@@ -1,0 +1,132 @@
+"""Data-parallel training (SURVEY.md §8(e) "Training: shard the latents and all-reduce
+gradients") on one MI355X: ``train(group=...)`` at world 2 (two ranks on cuda:0,
+gloo) against world 1 on the same global batch.
+
+At world > 1 a step is the fused forward + backward C call (``ldm_denoiser_train_step``: the
+one-launch job DAG without its AdamW nodes, or the launch path), one summing all-reduce of the
+flat gradient buffer (+ the loss) with each rank weighted by its share of the global batch, then
+one ``ldm_adamw_multi``.  The gradients of the global batch's mean loss are then the world-1
+gradients up to fp32 summation order: the batch rows' contributions are the same bf16 products,
+only the split of the row sums between ranks (and the order of the two halves) differs."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ldm_sdf
+    ldm_sdf.load_library()
+    return torch.device("cuda", 0)
+
+
+def _world(tmp_path, form, world, M, steps):
+    """Run the worker at ``world`` ranks as a child process; return rank 0's record."""
+    out = str(tmp_path / f"dp_{form}_{world}_{M}_{steps}.pt")
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.join(ROOT, "tests", "dp_train_worker.py"), out, form, str(M), str(steps)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return torch.load(out, weights_only=True)
+
+
+def _world1(dev, form, M, steps):
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser, ops
+    ops.train_step_config(form)
+    try:
+        model = MLPDenoiser(seed=11)
+        model.to_device(dev)
+        sch = ldm_sdf.DDPMSchedule()
+        lat = torch.randn(M, 256, generator=torch.Generator().manual_seed(5)).to(dev) * 0.5
+        gen = torch.Generator(device=dev).manual_seed(3)
+        st = ldm_sdf.train(model, sch, lat, steps=steps, batch=M, lr=1e-3, weight_decay=0.01,
+                           dtype="bf16", generator=gen)
+        torch.cuda.synchronize()
+        return {"losses": list(st.losses),
+                "params": {n: t.cpu() for n, t in model.params.items()},
+                "grads": {n: g.cpu() for n, g in st.adam_grads.items()}}
+    finally:
+        ops.train_step_config("auto")
+
+
+@pytest.mark.parametrize("M", [512, 300])
+def test_dp_world2_first_step_gradients_match_world1(dev, tmp_path, M):
+    """One step: every gradient of the global batch (512: two even shards; 300: 150 + 150 rows,
+    ragged 64-row bands) equals world 1's within fp32 summation order (relative 1e-5 of the
+    tensor's largest entry), and so does the loss."""
+    ref = _world1(dev, "launches", M, 1)
+    got = _world(tmp_path, "launches", 2, M, 1)
+    assert got["world"] == 2
+    assert abs(got["losses"][0] - ref["losses"][0]) <= 1e-6 * abs(ref["losses"][0])
+    for n, g in ref["grads"].items():
+        if n == "__loss":
+            continue
+        err = (got["grads"][n] - g).abs().max().item()
+        assert err <= 1e-5 * g.abs().max().item() + 1e-12, (n, err)
+
+
+def test_dp_world2_training_tracks_world1_and_forms_agree(dev, tmp_path):
+    """Six steps at world 2 through both forms of the forward + backward (the one-launch DAG
+    without AdamW nodes, and the launch path): the two are bit-identical to each other, and
+    both track world 1 (losses within 1e-5 relative; parameters within the fp32-order drift
+    AdamW lets through, as in test_train_bf16_loop_learns_and_matches_torch_adamw)."""
+    M, steps = 512, 6
+    ref = _world1(dev, "launches", M, steps)
+    a = _world(tmp_path, "launches", 2, M, steps)
+    b = _world(tmp_path, "dag", 2, M, steps)
+    assert a["form"] == "launches" and b["form"] == "dag"
+    assert a["losses"] == b["losses"]
+    for n in a["params"]:
+        assert torch.equal(a["params"][n], b["params"][n]), n
+    for la, lr in zip(a["losses"], ref["losses"]):
+        assert abs(la - lr) <= 1e-5 * abs(lr)
+    for n, p in ref["params"].items():
+        err = (a["params"][n] - p).abs().max().item()
+        assert err <= 3e-3 * p.abs().max().item() + 1e-6, (n, err)
+
+
+def test_train_step_dag_form_bitwise_vs_launches(dev):
+    """The forward + backward C call (``ldm_denoiser_train_step``, no optimizer) in its
+    one-launch form -- the step's job DAG built without AdamW nodes -- gives the launch path's
+    loss and gradients bit for bit (B = 1000 and a ragged 37)."""
+    import ldm_sdf
+    from ldm_sdf import MLPDenoiser, ops
+    for B in (1000, 37):
+        outs = []
+        for form in ("launches", "dag"):
+            ops.train_step_config(form)
+            try:
+                model = MLPDenoiser(seed=11)
+                model.to_device(dev)
+                sch = ldm_sdf.DDPMSchedule()
+                g = torch.Generator().manual_seed(9)
+                x0 = (torch.randn(B, 256, generator=g) * 0.5).to(dev)
+                eps = torch.randn(B, 256, generator=g).to(dev)
+                t = torch.randint(0, 1000, (B,), generator=g).to(dev)
+                loss, grads = ldm_sdf.train_step(model, sch, x0, t, eps, dtype="bf16")
+                torch.cuda.synchronize()
+                outs.append((ops.train_step_last_form(), loss.item(),
+                             {n: v.clone() for n, v in grads.items()}))
+            finally:
+                ops.train_step_config("auto")
+        assert outs[0][0] == "launches" and outs[1][0] == "dag"
+        assert outs[0][1] == outs[1][1]
+        for n in outs[0][2]:
+            assert torch.equal(outs[0][2][n], outs[1][2][n]), (B, n)

@@ -220,18 +220,3 @@ def test_unet_has_no_persistent_loop(dev):
     with pytest.raises(RuntimeError, match="no persistent"):
         ldm_sdf.Sampler(m, ldm_sdf.DDPMSchedule(), 1, steps=5, dtype="bf16", device=dev,
                         persistent=True)
-
-
-def test_graph_node_latency_diagnostic(dev):
-    """bench.py's config5.unet_roofline peak is measured in the run by
-    ldm_dev_graph_node_latency (an empty-kernel hipGraph chain, csrc/unet.hip): a plausible
-    per-node latency, and bad arguments fail with an error code."""
-    import ctypes as C
-    from ldm_sdf import _capi as capi
-    fn = capi.load().ldm_dev_graph_node_latency
-    fn.restype, fn.argtypes = C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
-    v = C.c_float(0.0)
-    assert fn(128, 900, 3, C.byref(v)) == 0
-    assert 100.0 < v.value < 50000.0          # ns per dependent node
-    assert fn(0, 900, 3, C.byref(v)) != 0
-    assert fn(128, 900, 3, None) != 0
