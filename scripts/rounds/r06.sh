@@ -2,11 +2,13 @@
 # Round 6 GPU calls, one batch per argument (bash scripts/rounds/r06.sh <batch> <outdir>); every
 # step runs under its own time limit and the batch stops at the first failure.  Output goes to
 # gpurun_out/<outdir>/; the logs that back a DESIGN.md statement are copied to profiles/<outdir>/.
-#   guards   the one-launch training step against the product library and the DEBUG=1 library
-#            (LDM_DASSERT bounds traps, wt_store.h extents), then the whole GPU suite and smoke
+#   guards   the one-launch / data-parallel training tests, the whole GPU suite and smoke
+#   debug    the same training tests and the GEMM tests against the DEBUG=1 library
+#            (LDM_DASSERT bounds traps, wt_store.h extents)
 #   bench    the default bench and the rocprofv3 kernel-trace summary of the same command
 #   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
 #   decoder  the decoder part stamps (scripts/stamp_split.py on the FS_STAMP library)
+#   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
 #   first    config 3's first call in a fresh process, with a kernel + HIP API trace
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -25,11 +27,13 @@ LIB=$PWD/latent-diffusion-models-for-shape-sdfs_amd/ldm_sdf
 PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 case $B in
   guards)
-    TAILN=4 step dag_product 400 $PYT tests/test_gpu_train_dag.py
-    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step dag_debug 600 $PYT tests/test_gpu_train_dag.py
-    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step gemm_debug 600 $PYT tests/test_gpu_gemm.py tests/test_gpu_train_capi.py
+    TAILN=4 step dag_product 400 $PYT tests/test_gpu_train_dag.py tests/test_gpu_train_dp.py
     TAILN=4 step pytest_gpu 900 $PYT tests -m gpu
     step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+    ;;
+  debug)
+    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step dag_debug 600 $PYT tests/test_gpu_train_dag.py tests/test_gpu_train_dp.py
+    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step gemm_debug 600 $PYT tests/test_gpu_gemm.py tests/test_gpu_train_capi.py
     ;;
   bench)
     TAILN=2 step bench 600 python -u bench.py
@@ -44,6 +48,9 @@ case $B in
     ;;
   decoder)
     LDM_SDF_LIB=$LIB/${FS_LIB:-libldm_fsstamp.so} TAILN=40 step stamp_split 300 python -u scripts/stamp_split.py
+    ;;
+  lds)
+    TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency
     ;;
   first)
     TAILN=20 step first_call 300 python -u scripts/config3_first_call.py
