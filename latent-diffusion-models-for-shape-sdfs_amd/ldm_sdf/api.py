@@ -304,6 +304,12 @@ class TrainState:
                           for n, (m, v) in self.adam.items()}
         if self.optimizer is not None:
             ck["optimizer"] = self.optimizer.state_dict()
+            # the state dict is positional: record which parameter each position is, so a load
+            # can rebuild the groups in this order whatever order the caller's optimizer uses
+            ident = {id(t): n for n, t in self.masters.items()}
+            if all(id(p) in ident for g in self.optimizer.param_groups for p in g["params"]):
+                ck["optimizer_names"] = [[ident[id(p)] for p in g["params"]]
+                                         for g in self.optimizer.param_groups]
         if generator is not None:
             ck["rng"] = generator.get_state().cpu()
             ck["rng_device"] = str(generator.device)
@@ -355,6 +361,15 @@ class TrainState:
         if optimizer is not None:
             if "optimizer" not in ck:
                 raise ValueError(f"{path}: no optimizer state saved")
+            saved = ck.get("optimizer_names")
+            if saved is not None:
+                # the saved order (positional state), whatever order the caller built in
+                if len(saved) != len(optimizer.param_groups) or \
+                        sorted(n for g in saved for n in g) != sorted(n for g in opt_names
+                                                                      for n in g):
+                    raise ValueError(f"{path}: the optimizer's parameter groups do not match "
+                                     "the saved ones")
+                opt_names = saved
             for g, gn in zip(optimizer.param_groups, opt_names):
                 g["params"] = [st.masters[n] for n in gn]
             optimizer.state.clear()               # keyed by the old tensors; reloaded below

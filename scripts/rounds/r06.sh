@@ -9,6 +9,7 @@
 #   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
 #   decoder  the decoder part stamps (scripts/stamp_split.py on the FS_STAMP library)
 #   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
+#            and scripts/microbench/acc_range (a k-step on each of two live accumulator sets)
 #   first    config 3's first call in a fresh process, with a kernel + HIP API trace
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -51,6 +52,7 @@ case $B in
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency
+    TAILN=4 step acc_range 120 ./scripts/microbench/acc_range
     ;;
   first)
     TAILN=20 step first_call 300 python -u scripts/config3_first_call.py
