@@ -142,6 +142,9 @@ int ldm_grid_coords(int N, int k0, int k1, float vs, float origin, float* xyz_ou
 /* A2: beta_out fp32 [B][2][H]; z fp32 [B][L]. */
 int ldm_decoder_fold(const ldm_decoder_t* w, const float* z, int B, float* beta_out,
                      ldm_stream_t s);
+/* out[0] (device) = max over shapes b of sqrt(mean_l z[b][l]^2), z fp32 [B][L]: the latent
+ * scale the Python decode's dtype="auto" picks its 16-bit format by. */
+int ldm_latent_rms_max(const float* z, int B, int L, float* out, ldm_stream_t s);
 /* A1+A3 grid mode: out fp32 [B][(k1-k0)*N*N] (the z-slab [k0,k1) of each shape's N^3 grid). */
 int ldm_decoder_grid_fwd(const ldm_decoder_t* w, const float* beta, int B, int N, int k0,
                          int k1, float vs, float origin, float* out, void* ws,

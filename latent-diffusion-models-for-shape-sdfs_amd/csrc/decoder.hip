@@ -52,6 +52,32 @@ __global__ void fold_kernel(const float* __restrict__ wz, const float* __restric
 }
 
 // ------------------------------------------------------------------------------------------
+// max over shapes b of sqrt(mean_l z[b][l]^2): the input of dtype="auto" (api.resolve_decode_dtype).
+// One workgroup of 4 waves; wave w takes shapes w, w + 4, ...: per shape a lane sums its
+// elements' squares in order, the wave sums the lanes (xor shuffles), and the largest RMS goes
+// through LDS.  Here rather than as torch reductions: the process's first torch pow / mean /
+// sqrt / max on the GPU loads their code objects (~0.25 s on a fresh process, DESIGN.md §7 round
+// 6), while this kernel sits in the code object the decode itself loads.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rms_max_kernel(const float* __restrict__ z, int B, int L,
+                                                      float* __restrict__ out) {
+    __shared__ float wmax[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float m = 0.f;
+    for (int b = wave; b < B; b += 4) {
+        const float* zz = z + (size_t)b * L;
+        float s = 0.f;
+        for (int k = lane; k < L; k += 64) s = fmaf(zz[k], zz[k], s);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        m = fmaxf(m, sqrtf(s / (float)L));
+    }
+    if (lane == 0) wmax[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+}
+
+// ------------------------------------------------------------------------------------------
 // fp32 parity kernel: 32 points per workgroup, activations in LDS [512][32], weights W^T
 // streamed from L2 with coalesced loads, 8x8 register tile per thread, fmaf accumulation.
 // Blob layout: for l = 1..7: WT_l [K_l][M_l] then b_l [M_l].
@@ -273,6 +299,12 @@ extern "C" int ldm_decoder_fold(const ldm_decoder_t* w, const float* z, int B, f
     hipLaunchKernelGGL(fold_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, w->wz,
                        w->bz, z, B, w->latent_dim, w->hidden, beta_out);
     return launch_status("ldm_decoder_fold");
+}
+
+extern "C" int ldm_latent_rms_max(const float* z, int B, int L, float* out, ldm_stream_t s) {
+    LDM_REQUIRE(z && out && B >= 1 && L >= 1, LDM_EINVAL, "ldm_latent_rms_max: bad arguments");
+    hipLaunchKernelGGL(rms_max_kernel, dim3(1), dim3(256), 0, (hipStream_t)s, z, B, L, out);
+    return launch_status("ldm_latent_rms_max");
 }
 
 extern "C" int ldm_decoder_grid_fwd(const ldm_decoder_t* w, const float* beta, int B, int N,

@@ -61,6 +61,13 @@ constexpr int kFsWl = 512 * 4;                      // permuted final-layer weig
 #define FS_STAMP 0
 #endif
 constexpr int kFsStamp = FS_STAMP ? 128 * 8 : 0;
+// Diagnostic ablations (stamp builds only, results wrong; scripts/stamp_split.py, DESIGN.md §4
+// round 6): FS_ABL bit 0 = no weight stream (the ring keeps its registers), bit 1 = no epilogue
+// units, bit 2 = no in-stream barriers
+#ifndef FS_ABL
+#define FS_ABL 0
+#endif
+static_assert(FS_ABL == 0 || FS_STAMP, "ablations are diagnostic builds");
 constexpr int kFsLds = kFsAct + kFsRed + kFsWl + kFsStamp;
 static_assert(kFsLds <= 160 * 1024, "LDS");
 
@@ -215,6 +222,7 @@ __device__ __forceinline__ float* red_w(const FCtx<FV>& c) {
 // LDS barrier: LDS writes done (lgkmcnt), then s_barrier.  The weight loads in flight
 // (vmcnt) are NOT waited for: they feed registers only.
 __device__ __forceinline__ void fs_bar() {
+    if (FS_ABL & 4) return;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
@@ -238,6 +246,7 @@ template <int FV>
 __device__ __forceinline__ void issue(FCtx<FV>& c, int r) {
     const uint32_t so = c.s_iss + (uint32_t)(r >> 1) * 2u * kFsStep;
     const uint32_t vo = c.voff + (uint32_t)(r & 1) * kFsStep;
+    if (FS_ABL & 1) return;
     c.ring[r][0] = bld(c.rw, vo, so);
     c.ring[r][1] = bld(c.rw, vo + 1024u, so);
 }
@@ -261,6 +270,7 @@ template <typename T, int EK, int FV>
 __device__ __forceinline__ void epi_unit(FCtx<FV>& c, const f32x16 (&accY)[2][4], int u) {
     const int t = u >> 1, s = u & 1;
     const int i = t >> 2, n = t & 3;
+    if (FS_ABL & 2) return;
     if (EK == FE_LATE || EK == FE_EARLY) {   // part 1 of the previous layer / part 0 of this
         u32x4 f;
 #pragma unroll

@@ -141,6 +141,7 @@ SIGNATURES = [
     ("ldm_workspace_bytes_layout", _sz, [_i, _i, _i, _i, _i]),
     ("ldm_grid_coords", _i, [_i, _i, _i, _f, _f, _fp, _vp]),
     ("ldm_decoder_fold", _i, [C.POINTER(Decoder), _fp, _i, _fp, _vp]),
+    ("ldm_latent_rms_max", _i, [_fp, _i, _i, _fp, _vp]),
     ("ldm_decoder_grid_fwd", _i, [C.POINTER(Decoder), _fp, _i, _i, _i, _i, _f, _f, _fp, _vp,
                                   _sz, _vp]),
     ("ldm_decoder_points_fwd", _i, [C.POINTER(Decoder), _fp, _fp, _i, _i, _fp, _vp, _sz, _vp]),

@@ -64,8 +64,13 @@ def resolve_decode_dtype(dtype: str, latents: torch.Tensor) -> str:
     ent = _AUTO_CACHE.get(id(latents))
     if ent is not None and ent[0]() is latents and ent[1] == key:
         return ent[2]
-    lat = latents.float().reshape(latents.shape[0] if latents.dim() > 1 else 1, -1)
-    rms = float(lat.pow(2).mean(dim=1).sqrt().max())
+    if latents.is_cuda:
+        # the library's own reduction (ldm_latent_rms_max): the first torch pow / mean / sqrt /
+        # max of a process load their kernels, ~0.25 s (config 3's first call)
+        rms = ops.latent_rms_max(latents)
+    else:                         # (host tensors: the decision only; decode itself refuses them)
+        lat = latents.float().reshape(latents.shape[0] if latents.dim() > 1 else 1, -1)
+        rms = float(lat.pow(2).mean(dim=1).sqrt().max())
     pick = "bf16" if rms <= BF16_MAX_LATENT_RMS else "fp16" if rms <= FP16_MAX_LATENT_RMS \
         else "fp32"
     if len(_AUTO_CACHE) > 64:

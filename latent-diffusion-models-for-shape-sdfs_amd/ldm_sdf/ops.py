@@ -56,6 +56,18 @@ def decoder_fold(desc: capi.Decoder, z: torch.Tensor) -> torch.Tensor:
     return beta
 
 
+def latent_rms_max(z: torch.Tensor) -> float:
+    """max over shapes of the latent RMS (``ldm_latent_rms_max``; one read-back)."""
+    capi.require_device(z)
+    z = z.float().contiguous()
+    zz = z.reshape(z.shape[0] if z.dim() > 1 else 1, -1)
+    out = torch.empty(1, device=z.device, dtype=torch.float32)
+    capi.check(capi.load().ldm_latent_rms_max(zz.data_ptr(), zz.shape[0], zz.shape[1],
+                                              out.data_ptr(), capi.stream_handle(z.device)),
+               "ldm_latent_rms_max")
+    return float(out.item())
+
+
 # ---------------------------------------------------------------------------------------- A3
 def decoder_grid_fwd(desc: capi.Decoder, beta: torch.Tensor, N: int, k0: int, k1: int,
                      bbox=(-1.0, 1.0), out: Optional[torch.Tensor] = None,

@@ -7,7 +7,7 @@
 #            (LDM_DASSERT bounds traps, wt_store.h extents)
 #   bench    the default bench and the rocprofv3 kernel-trace summary of the same command
 #   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
-#   decoder  the decoder part stamps (scripts/stamp_split.py on the FS_STAMP library)
+#   decoder  the decoder part stamps (scripts/stamp_split.py on each FS_STAMP library in $FS_LIBS)
 #   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
 #            and scripts/microbench/acc_range (a k-step on each of two live accumulator sets)
 #   first    config 3's first call in a fresh process, with a kernel + HIP API trace
@@ -48,7 +48,9 @@ case $B in
     done
     ;;
   decoder)
-    LDM_SDF_LIB=$LIB/${FS_LIB:-libldm_fsstamp.so} TAILN=40 step stamp_split 300 python -u scripts/stamp_split.py
+    for L in ${FS_LIBS:?}; do
+      LDM_SDF_LIB=$LIB/$L TAILN=70 step stamp_${L%.so} 300 python -u scripts/stamp_split.py
+    done
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency

@@ -85,9 +85,11 @@ def test_dp_world2_first_step_gradients_match_world1(dev, tmp_path, M):
 def test_dp_world2_training_tracks_world1_and_forms_agree(dev, tmp_path):
     """Six steps at world 2 through both forms of the forward + backward (the one-launch DAG
     without AdamW nodes, and the launch path): the two are bit-identical to each other, and
-    both track world 1 (losses within 1e-4 relative -- measured 1.1e-5 after six AdamW steps on
-    the MI355X, the first step's loss agrees to 1e-6; parameters within the fp32-order drift
-    AdamW lets through, as in test_train_bf16_loop_learns_and_matches_torch_adamw)."""
+    both track world 1: losses within 1e-4 relative (measured 1.1e-5 after six AdamW steps on
+    the MI355X; the first step's loss agrees to 1e-6).  Parameters: AdamW normalises every
+    update to ~lr, so an element whose gradient is ~0 can step either way on an fp32-order
+    difference -- the bound for any element is 2 lr per step (measured max 5.5e-4 at lr 1e-3,
+    six steps) -- while the median element must agree to 1e-6."""
     M, steps = 512, 6
     ref = _world1(dev, "launches", M, steps)
     a = _world(tmp_path, "launches", 2, M, steps)
@@ -98,9 +100,12 @@ def test_dp_world2_training_tracks_world1_and_forms_agree(dev, tmp_path):
         assert torch.equal(a["params"][n], b["params"][n]), n
     for la, lr in zip(a["losses"], ref["losses"]):
         assert abs(la - lr) <= 1e-4 * abs(lr)
+    lr = 1e-3
     for n, p in ref["params"].items():
-        err = (a["params"][n] - p).abs().max().item()
-        assert err <= 3e-3 * p.abs().max().item() + 1e-6, (n, err)
+        d = (a["params"][n] - p).abs()
+        print(f"{n}: max {d.max().item():.3e} median {d.median().item():.3e}")
+        assert d.max().item() <= 2 * lr * steps, n
+        assert d.median().item() <= 1e-6, n
 
 
 def test_train_step_dag_form_bitwise_vs_launches(dev):
