@@ -725,13 +725,17 @@ int check_dag_extents(const dag::Table& T, const ldm_denoiser_t* w, const ldm_sc
     R.add(gr->w_in, H * D * 4); R.add(gr->b_in, H * 4); R.add(gr->w_t1, H * TE * 4);
     R.add(gr->b_t1, H * 4); R.add(gr->w_t2, H * H * 4); R.add(gr->b_t2, H * 4);
     R.add(gr->w_out, D * H * 4); R.add(gr->b_out, D * 4);
+    R.add(sc->sqrt_ab, (int64_t)sc->T * 4); R.add(sc->sqrt_1mab, (int64_t)sc->T * 4);
+    // (R so far: what the descriptors size.  An AdamW tensor's gradient and bf16 copies must
+    // lie in it -- they are the step's own gradients and the descriptor's weights -- so a
+    // tensor that claims more rows / columns than its gradient holds is refused below; its
+    // fp32 master and moments are the caller's alone and join the regions here.)
+    const Regions K = R;
     for (int i = 0; i < n; ++i) {
         const ldm_adamw_tensor_t& t = tensors[i];
         const int64_t e = (int64_t)t.rows * t.cols;
-        R.add(t.p, e * 4); R.add(t.g, e * 4); R.add(t.m, e * 4); R.add(t.v, e * 4);
-        R.add(t.p_bf16, e * 2); R.add(t.p_bf16_t, e * 2);
+        R.add(t.p, e * 4); R.add(t.m, e * 4); R.add(t.v, e * 4);
     }
-    R.add(sc->sqrt_ab, (int64_t)sc->T * 4); R.add(sc->sqrt_1mab, (int64_t)sc->T * 4);
     const char* what = nullptr;
     int bad = -1;
     auto need = [&](int node, const char* name, const void* p, int64_t bytes) {
@@ -790,6 +794,11 @@ int check_dag_extents(const dag::Table& T, const ldm_denoiser_t* w, const ldm_sc
                 continue;
             }
             const ldm_adamw_tensor_t& t = tensors[nd.adam];
+            const int64_t e = (int64_t)t.rows * t.cols;
+            for (const void* q : {static_cast<const void*>(t.g)})
+                if (bad < 0 && q && !K.holds(q, e * 4)) { bad = i; what = "AdamW gradient"; }
+            for (const void* q : {t.p_bf16, t.p_bf16_t})
+                if (bad < 0 && q && !K.holds(q, e * 2)) { bad = i; what = "AdamW bf16 copy"; }
             if ((int64_t)nd.tiles_m * 64 < t.rows ||
                 nd.col_off + nd.nk > (t.cols + 63) / 64) {
                 if (bad < 0) { bad = i; what = "AdamW tiles vs tensor"; }

@@ -554,6 +554,19 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 #ifndef SL_LDSBLK
 #define SL_LDSBLK 1
 #endif
+// After a layer's publish (A/B, scripts/sampler_time.py): 0 nothing; 1 a scheduling barrier;
+// 2 an s_memrealtime whose value is consumed (the round-5 stamp's mark 4 alone: SL_MARKS = 16
+// ran 94-98k steps/s against 85-86k without, spill-free, profiles/r06d)
+#ifndef SL_PUBFENCE
+#define SL_PUBFENCE 0
+#endif
+__device__ __forceinline__ void after_publish() {
+    if (SL_PUBFENCE == 1) __builtin_amdgcn_sched_barrier(0);
+    if (SL_PUBFENCE == 2) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        asm volatile("" ::"s"(t));
+    }
+}
 // SL_MARKS (A/B builds only): a bit mask of the marks to keep without the rest of the stamps
 #ifndef SL_MARKS
 #define SL_MARKS 0
@@ -743,6 +756,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                 if (tagged) publish_tagged(hgr + (size_t)qb * H + mh, acc + bi, phase);
                 else publish(hrep + (size_t)qb * H + mh, acc + bi);
             }
+            after_publish();
             stp.mark(4);
             if (SL_STAMP) stp.acc[5] += 1;
         }
@@ -778,6 +792,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                 if (tagged) publish_tagged(hgr + (size_t)((k + 1) & 1) * MBX * H + (size_t)qb * H + mh, hv, phase);
                 else publish(hout + (size_t)qb * H + mh, hv);
             }
+            after_publish();
             stp.mark(4);
             if (SL_STAMP) stp.acc[5] += 1;
             alive = boundary();
@@ -808,6 +823,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                     publish_tagged(xgr + (size_t)((s & 1) ^ 1) * MBX * D + (size_t)qb * D + mo,
                                    xv, phase);
             }
+            after_publish();
             stp.mark(4);
             if (SL_STAMP) stp.acc[5] += 1;
         }

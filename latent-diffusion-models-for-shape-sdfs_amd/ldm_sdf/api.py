@@ -578,12 +578,15 @@ def train(denoiser: MLPDenoiser, schedule: DDPMSchedule, latents: torch.Tensor, 
                     w.copy_(p)                   # an fp32 working copy that is not the master
         state.step += 1
         state.losses.append(loss)
-    if fused and ops.train_step_last_form() == "dag":
+    if dtype == "bf16" and steps > 0 and ops.train_step_last_form() == "dag":
         # the one-launch step's waits are bounded: a non-zero status means a step gave up and
         # the weights are not to be trusted (one read-back per train() call, where the losses
-        # are read back anyway)
+        # are read back anyway) -- the data-parallel path (the DAG without AdamW nodes) too:
+        # its workspace is the rank's shard's
+        lo_, hi_ = ldist.batch_shard(batch, rank, world)
         dev_ = denoiser.device_pack(dtype, device, with_tables=False)
-        st = ops.train_status(dev_["desc"], batch, denoiser.train_workspace(batch, device))
+        st = ops.train_status(dev_["desc"], hi_ - lo_,
+                              denoiser.train_workspace(hi_ - lo_, device))
         if st != 0:
             raise capi.LdmError(f"train: the one-launch training step reported status {st} "
                                 "(1: a dependency wait timed out, 3: stale job table); the "

@@ -152,6 +152,13 @@ int main(void) {
             EXPECT(strstr(buf, " wt 2 ") != NULL && strstr(buf, " wt 0 ") != NULL);
         }
         EXPECT(ldm_denoiser_train_dag_describe(&w, &sc, 1000, saved, &g, t, 16, buf, 64) == 0);
+        /* the host extent check (check_dag_extents): an AdamW tensor that claims more rows than
+         * its gradient (w_out: 256 x 1024) holds is refused before any upload */
+        t[6].rows = 512;
+        EXPECT_ERR(ldm_denoiser_train_dag_describe(&w, &sc, 1000, saved, &g, t, 16, buf, 64));
+        EXPECT(strstr(ldm_last_error(), "outside every allocation") != NULL);
+        t[6].rows = 256;
+        EXPECT(ldm_denoiser_train_dag_describe(&w, &sc, 1000, saved, &g, t, 16, buf, 64) == 0);
         EXPECT_ERR(ldm_denoiser_train_dag_describe(&w, &sc, 0, saved, &g, t, 16, buf, 64));
         EXPECT_ERR(ldm_denoiser_train_dag_describe(NULL, &sc, 10, saved, &g, t, 16, buf, 64));
         EXPECT_ERR(ldm_denoiser_train_ws_init(NULL, 10, saved, NULL));

