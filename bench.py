@@ -256,12 +256,15 @@ def bench_autodecoder(args, dev):
     sdf = xyz.norm(dim=2) - radii[:, None]
     dec = ldm_sdf.SDFDecoder(seed=1234)
     dec.weights[8] = dec.weights[8] * 0.01
+    # (group=LOCAL: rank 0 only at world > 1, as for config 2)
+    from ldm_sdf.dist import LOCAL
     st = ldm_sdf.train_autodecoder(dec, xyz, sdf, steps=1, shapes_per_batch=S,
-                                   samples_per_shape=P, dtype="bf16", generator=g)
+                                   samples_per_shape=P, dtype="bf16", generator=g, group=LOCAL)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st = ldm_sdf.train_autodecoder(dec, xyz, sdf, steps=args.ad_steps, shapes_per_batch=S,
-                                   samples_per_shape=P, dtype="bf16", generator=g, state=st)
+                                   samples_per_shape=P, dtype="bf16", generator=g, state=st,
+                                   group=LOCAL)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.ad_steps
     fwd = sum(2 * i * o for (i, o) in ldm_sdf.decoder_layer_dims(256, 512))   # per sample
@@ -618,6 +621,12 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LDM_BENCH_BACKEND=gloo (a rehearsal of the multi-rank flow on a ONE-GPU box: every rank on
+    # cuda:0, collectives over gloo -- RCCL refuses two ranks on one device); default: RCCL,
+    # one GPU per rank
+    backend = os.environ.get("LDM_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
@@ -625,7 +634,10 @@ def main():
         # RCCL fails fast: an error / timeout on one rank aborts the communicator instead of
         # leaving the others blocked in a collective (SURVEY §5 "Fault/elastic")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD
 
     import ldm_sdf
@@ -927,11 +939,15 @@ def bench_train(args, dev, gen):
     den_t = ldm_sdf.MLPDenoiser(seed=4321)
     sch_t = ldm_sdf.DDPMSchedule()
     lat_t = torch.randn(1000, 256, device=dev, generator=gen) * 0.5
-    st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16")   # warm-up
+    # (group=LOCAL: config 2 is a 1-GPU workload; at world > 1 only rank 0 runs this leg, so
+    # train() must not enter a collective the other ranks never join)
+    from ldm_sdf.dist import LOCAL
+    st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16",
+                       group=LOCAL)   # warm-up
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     st = ldm_sdf.train(den_t, sch_t, lat_t, steps=args.train_steps, batch=1000,
-                       dtype="bf16", state=st)
+                       dtype="bf16", state=st, group=LOCAL)
     torch.cuda.synchronize()
     dtt = (time.perf_counter() - t3) / args.train_steps
     H, D, nb = den_t.H, den_t.D, den_t.n_blocks
@@ -954,11 +970,12 @@ def bench_train(args, dev, gen):
     other = "dag" if res["form"] == "launches" else "launches"
     try:
         _ops.train_step_config(other)
-        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16", state=st)
+        st = ldm_sdf.train(den_t, sch_t, lat_t, steps=3, batch=1000, dtype="bf16", state=st,
+                           group=LOCAL)
         torch.cuda.synchronize()
         t4 = time.perf_counter()
         st = ldm_sdf.train(den_t, sch_t, lat_t, steps=args.train_steps, batch=1000,
-                           dtype="bf16", state=st)
+                           dtype="bf16", state=st, group=LOCAL)
         torch.cuda.synchronize()
         d_o = (time.perf_counter() - t4) / args.train_steps
         res["other_form"] = {"form": _ops.train_step_last_form(), "steps_per_s": 1.0 / d_o,

@@ -163,15 +163,22 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
 
     const int rb = L.m0 + wr * (BM / 2) + i * 32;      // first row of this 32-row block
     // every operand's extent in bytes (wt_store.h): the rows the problem names, never more --
-    // the write-through forms clamp their buffer resources to these, DEBUG builds trap past them
-    const uint32_t xC = ext_bytes(Mv, ldc, Nc, 4), xP = ext_bytes(Mv, ldp, Nc, 4),
-                   xR = ext_bytes(Mv, ldr, Nc, 4), xPin = ext_bytes(Mv, ldpin, Nc, 4),
-                   xRb = ext_bytes(Mv, ldrb, Nc, 2), xCb = ext_bytes(Mr, ldcb, Nc, 2),
-                   xCbT = kt ? ext_bytes((Mr + kt - 1) / kt, (int64_t)Nc * kt, (int64_t)Nc * kt, 2)
-                             : ext_bytes(Nc, ldct, Mr, 2),
-                   xcs = ext_bytes((Mr - 1) / 32 + 1, Nc, Nc, 4),
-                   xlp = ext_bytes((Mr - 1) / 32 + 1, (Nc + 31) / 32, (Nc + 31) / 32, 4),
-                   xws = ext_bytes(Mv, Nc, Nc, 4);
+    // the write-through forms clamp their buffer resources to these, DEBUG builds trap past them.
+    // Formed at each use (short live ranges: computed once up front they held 10 scalar
+    // registers across the epilogue and pushed the one-launch kernel into spills)
+    auto xC = [&]() { return ext_bytes(Mv, ldc, Nc, 4); };
+    auto xP = [&]() { return ext_bytes(Mv, ldp, Nc, 4); };
+    auto xR = [&]() { return ext_bytes(Mv, ldr, Nc, 4); };
+    auto xPin = [&]() { return ext_bytes(Mv, ldpin, Nc, 4); };
+    auto xRb = [&]() { return ext_bytes(Mv, ldrb, Nc, 2); };
+    auto xCb = [&]() { return ext_bytes(Mr, ldcb, Nc, 2); };
+    auto xCbT = [&]() {
+        return kt ? ext_bytes((Mr + kt - 1) / kt, (int64_t)Nc * kt, (int64_t)Nc * kt, 2)
+                  : ext_bytes(Nc, ldct, Mr, 2);
+    };
+    auto xcs = [&]() { return ext_bytes((Mr - 1) / 32 + 1, Nc, Nc, 4); };
+    auto xlp = [&]() { return ext_bytes((Mr - 1) / 32 + 1, (Nc + 31) / 32, (Nc + 31) / 32, 4); };
+    auto xws = [&]() { return ext_bytes(Mv, Nc, Nc, 4); };
     LDM_DASSERT(rb >= 0 && nb >= 0 && nb + 32 <= Nc);
     float* sc = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + epi_off) +
                 wave * 1024;
@@ -191,7 +198,7 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int b = rb + rl + 8 * p;
-            if (b < Mv) vst_at<WT>(dst, xws, (int64_t)b * Nc + n4, cv[p]);
+            if (b < Mv) vst_at<WT>(dst, xws(), (int64_t)b * Nc + n4, cv[p]);
         }
         asm volatile("" ::: "memory");
         return;
@@ -212,7 +219,7 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
         const bool has1 = X1C || (X1R && Rp != nullptr);
         const float* x1 = X1C ? Cp : Rp;
         const int64_t ld1 = X1C ? ldc : ldr;
-        const uint32_t x1x = X1C ? xC : xR;
+        const uint32_t x1x = X1C ? xC() : xR();
 #pragma unroll
         for (int p = 0; p < 4; ++p) {    // padding rows read row 0 (valid) and drop it
             const int b = rb + rl + 8 * p;
@@ -225,9 +232,9 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
                     v1[p] = vld_at<WT, f32x4>(x1, x1x, (int64_t)bb * ld1 + n4);
             }
             if constexpr (X2)
-                v2[p] = vld_at<WT, f32x4>(Pin, xPin, (int64_t)bb * ldpin + n4);
+                v2[p] = vld_at<WT, f32x4>(Pin, xPin(), (int64_t)bb * ldpin + n4);
             if constexpr (XB)
-                vb[p] = vld_at<WT, u32x2>(Rbp, xRb, (int64_t)bb * ldrb + n4);
+                vb[p] = vld_at<WT, u32x2>(Rbp, xRb(), (int64_t)bb * ldrb + n4);
         }
         // one row at a time from the batched operand loads: only the values the write-back
         // needs (keep) live across rows (the 128 x 128 kernels spilled with all of it live)
@@ -264,12 +271,12 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
                 out[e] = live ? o : 0.f;
             }
             if (Cp && live)
-                vst_at<WT>(Cp, xC, (int64_t)b * ldc + n4, MODE == LDM_GEMM_DGRAD_SILU ? dh : out);
+                vst_at<WT>(Cp, xC(), (int64_t)b * ldc + n4, MODE == LDM_GEMM_DGRAD_SILU ? dh : out);
             if constexpr (MODE == LDM_GEMM_SILU || MODE == LDM_GEMM_RESID_SILU) {
-                if (Pp && live) vst_at<WT>(Pp, xP, (int64_t)b * ldp + n4, pre_v);
+                if (Pp && live) vst_at<WT>(Pp, xP(), (int64_t)b * ldp + n4, pre_v);
             }
             if (Cbp && b < Mr)
-                vst_at<WT>(Cbp, xCb, (int64_t)b * ldcb + n4,
+                vst_at<WT>(Cbp, xCb(), (int64_t)b * ldcb + n4,
                         u32x2{pack2_bf16(out[0], out[1]), pack2_bf16(out[2], out[3])});
             keep[p] = LS ? dd : out;
         }
@@ -301,7 +308,7 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
                                          pack2_bf16(oa[4 * g + 2], oa[4 * g + 3])};
                         const int64_t at = kt ? ((int64_t)(b / kt) * Nc + n) * kt + b % kt
                                               : (int64_t)n * ldct + b;
-                        vst_at<WT>(CbTp, xCbT, at, w);
+                        vst_at<WT>(CbTp, xCbT(), at, w);
                     }
                 }
             }
@@ -310,14 +317,14 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
 #pragma unroll
                 for (int v = 0; v < 16; ++v) cs += oa[v];
                 cs += __shfl_xor(cs, 32);
-                if (h == 0 && rb < Mr) vst_at<WT>(csp, xcs, (int64_t)(rb / 32) * Nc + n, cs);
+                if (h == 0 && rb < Mr) vst_at<WT>(csp, xcs(), (int64_t)(rb / 32) * Nc + n, cs);
             }
             if constexpr (LS) {
                 if (lpp) {
 #pragma unroll
                     for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
                     if (lane == 0 && rb < Mr)      // the block lies inside N here
-                        vst_at<WT>(lpp, xlp, (int64_t)(rb / 32) * ((Nc + 31) / 32) + nb / 32, lsum);
+                        vst_at<WT>(lpp, xlp(), (int64_t)(rb / 32) * ((Nc + 31) / 32) + nb / 32, lsum);
                 }
             }
         }

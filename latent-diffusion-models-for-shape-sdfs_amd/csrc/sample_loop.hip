@@ -566,7 +566,29 @@ __device__ __forceinline__ void after_publish() {
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         asm volatile("" ::"s"(t));
     }
+    if (SL_PUBFENCE == 3) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
+// SL_PUBFENCE 4: the round-5 stamp's mark 4 alone, kept in a register (no global stamp buffer):
+// the elapsed time since the previous publish accumulated per wave, consumed at the end
+struct PubClock {
+    uint64_t t = 0, acc = 0;
+    __device__ __forceinline__ void start() {
+        if (SL_PUBFENCE == 4) t = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ void mark() {
+        if (SL_PUBFENCE == 4) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            acc += now - t;
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void end() {
+        if (SL_PUBFENCE == 4) asm volatile("" ::"s"(acc));
+    }
+};
 // SL_MARKS (A/B builds only): a bit mask of the marks to keep without the rest of the stamps
 #ifndef SL_MARKS
 #define SL_MARKS 0
@@ -721,6 +743,8 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         return *ok != 0;
     };
     stp.start();
+    PubClock pclk;
+    pclk.start();
 
     for (int s = 0; s < a.steps; ++s) {
         const int t = a.t_hi - s;
@@ -757,6 +781,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                 else publish(hrep + (size_t)qb * H + mh, acc + bi);
             }
             after_publish();
+            pclk.mark();
             stp.mark(4);
             if (SL_STAMP) stp.acc[5] += 1;
         }
@@ -793,6 +818,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                 else publish(hout + (size_t)qb * H + mh, hv);
             }
             after_publish();
+            pclk.mark();
             stp.mark(4);
             if (SL_STAMP) stp.acc[5] += 1;
             alive = boundary();
@@ -824,12 +850,14 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
                                    xv, phase);
             }
             after_publish();
+            pclk.mark();
             stp.mark(4);
             if (SL_STAMP) stp.acc[5] += 1;
         }
         if (!boundary()) return;
     }
     stp.flush(wave);
+    pclk.end();
 }
 
 // Residency: every workgroup of the grid must be resident at once (the grid barriers wait for

@@ -11,10 +11,9 @@
 // of the operand it touches, in bytes from `base` (ext_bytes below: the problem's rows x leading
 // dimension, never more).  The write-through forms build their buffer resource with
 // num_records = that extent, so an access past the operand is DROPPED by the hardware (a load
-// returns 0) instead of landing in a neighbouring tensor or faulting; the offset is formed in
-// 64 bits and an offset outside [0, extent) is sent to `extent` itself (dropped) rather than
-// truncated into range.  `make DEBUG=1` (LDM_DEBUG) turns every such access into a trap with
-// its location (LDM_DASSERT), for the plain forms too.  The host side (build_dag) refuses a job
+// returns 0) instead of landing in a neighbouring tensor or faulting (checked_off below).
+// `make DEBUG=1` (LDM_DEBUG) turns every such access into a trap with its location
+// (LDM_DASSERT), for the plain forms too.  The host side (build_dag) refuses a job
 // table whose operand extents do not lie inside the allocations the caller handed over.
 #pragma once
 #include "ldm_internal.h"
@@ -32,14 +31,19 @@ __host__ __device__ __forceinline__ uint32_t ext_bytes(int64_t rows, int64_t ld,
     return (uint32_t)(b < (int64_t)kMaxExtent ? b : (int64_t)kMaxExtent);
 }
 
-// byte offset of element idx of T, or `nbytes` (out of range: the access is dropped) when the
-// V-sized access would not lie inside [0, nbytes)
+// byte offset of element idx of T, formed in 64 bits; DEBUG builds trap unless the V-sized
+// access lies inside [0, nbytes).  The product build passes the low 32 bits: the buffer
+// resource's range check drops any offset >= nbytes (a negative one too, which wraps to >= 2^31
+// while every extent is < 2 GiB -- the host check's bound), and no index of these kernels can
+// reach the 4 GiB wrap (each is a product of the problem's dimensions, whose extents the host
+// check bounds).  (A 64-bit compare + select here cost the one-launch kernel 30 VGPRs and
+// doubled its scratch: 7 % of the step.)
 template <typename V, typename T>
 __device__ __forceinline__ uint32_t checked_off(int64_t idx, uint32_t nbytes) {
     const int64_t off = idx * (int64_t)sizeof(T);
-    const bool in = off >= 0 && off + (int64_t)sizeof(V) <= (int64_t)nbytes;
-    LDM_DASSERT(in);
-    return in ? (uint32_t)off : nbytes;
+    LDM_DASSERT(off >= 0 && off + (int64_t)sizeof(V) <= (int64_t)nbytes);
+    (void)nbytes;
+    return (uint32_t)off;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ext_rsrc(const void* base, uint32_t nbytes) {

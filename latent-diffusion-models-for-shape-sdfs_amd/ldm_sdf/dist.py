@@ -31,8 +31,22 @@ def init_process_group(backend: str = "nccl", **kw) -> None:
     dist.init_process_group(backend, **kw)
 
 
+class _Local:
+    """``group=LOCAL``: this rank alone, even inside an initialised process group (a rank
+    that runs a single-GPU workload while the others wait -- bench.py's rank-0 legs).  Every
+    collective of this module is then a no-op, as at world size 1."""
+
+    def __repr__(self) -> str:
+        return "ldm_sdf.dist.LOCAL"
+
+
+LOCAL = _Local()
+
+
 def world_and_rank(group=None) -> Tuple[int, int]:
-    if not dist.is_available() or not dist.is_initialized():
+    """(world size, rank) of ``group`` (None: the default group once initialised; LOCAL or
+    no process group: (1, 0))."""
+    if group is LOCAL or not dist.is_available() or not dist.is_initialized():
         return 1, 0
     return dist.get_world_size(group), dist.get_rank(group)
 

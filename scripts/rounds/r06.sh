@@ -8,6 +8,7 @@
 #   bench    the default bench and the rocprofv3 kernel-trace summary of the same command
 #   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
 #   decoder  the decoder part stamps (scripts/stamp_split.py on each FS_STAMP library in $FS_LIBS)
+#   multirank  bench.py --gpus 2 with both ranks on cuda:0 over gloo (the N > 1 control flow)
 #   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
 #            and scripts/microbench/acc_range (a k-step on each of two live accumulator sets)
 #   first    config 3's first call in a fresh process, with a kernel + HIP API trace
@@ -51,6 +52,11 @@ case $B in
     for L in ${FS_LIBS:?}; do
       LDM_SDF_LIB=$LIB/$L TAILN=70 step stamp_${L%.so} 300 python -u scripts/stamp_split.py
     done
+    ;;
+  multirank)
+    # the N > 1 flow of bench.py (z-slab gathers, rank-0 legs, barriers) rehearsed on one GPU:
+    # 2 ranks on cuda:0 over gloo (timings meaningless: both ranks share the device)
+    LDM_BENCH_BACKEND=gloo TAILN=3 step bench_gloo2 900 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --train-steps 5 --ad-steps 1
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency

@@ -147,6 +147,37 @@ def _allreduce(rank, world):
     return bool(torch.allclose(a, torch.full_like(a, m)) and torch.allclose(b, torch.full_like(b, 2 * m)))
 
 
+def _weighted_and_local(rank, world):
+    """allreduce_weighted_ (train()'s data-parallel gradient: sum_r w_r t_r with w_r = B_r/B)
+    on uneven shards equals the global-batch mean; group=LOCAL is this rank alone inside the
+    initialised group (bench.py's rank-0 legs): no collective, every function a world-1 no-op
+    -- rank 1 never joins anything here, so a collective would hang the test."""
+    from ldm_sdf.dist import (LOCAL, all_gather_rows, allreduce_mean_, allreduce_weighted_,
+                              batch_shard, world_and_rank)
+    n = 7
+    lo, hi = batch_shard(n, rank, world)
+    rows = torch.arange(n, dtype=torch.float64)[lo:hi]
+    g = torch.tensor([rows.mean().item()], dtype=torch.float64)       # local mean
+    allreduce_weighted_([g], (hi - lo) / n)
+    ok = abs(g.item() - torch.arange(n, dtype=torch.float64).mean().item()) < 1e-12
+    if rank == 0:
+        ok = ok and world_and_rank(LOCAL) == (1, 0)
+        t = torch.full((3,), 5.0)
+        allreduce_mean_([t], group=LOCAL)
+        allreduce_weighted_([t], 0.5, group=LOCAL)
+        ok = ok and torch.equal(t, torch.full((3,), 5.0))
+        x = torch.ones(2, 4)
+        ok = ok and all_gather_rows(x, 2, group=LOCAL) is x
+    dist.barrier()
+    return bool(ok)
+
+
+def test_weighted_allreduce_and_local_group():
+    for world in (2, 3):
+        res = _run("_weighted_and_local", world)
+        assert all(res[r] is True for r in range(world)), res
+
+
 def _latent_rows(rank, world):
     """train_autodecoder's latent exchange: every rank draws the same shapes, owns a contiguous
     share, writes its rows scaled by its share of the batch, and one all-reduce (sum) gives every
