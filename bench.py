@@ -609,11 +609,26 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def leg(name: str) -> None:
+    """LDM_BENCH_TRACE=1: one stderr line per leg and rank, so a stalled multi-rank run shows
+    where each rank is (with LDM_BENCH_WATCHDOG=<s>: every thread's stack after s seconds, then
+    exit)."""
+    if os.environ.get("LDM_BENCH_TRACE"):
+        print(f"[bench rank {os.environ.get('RANK', '0')}] {name} "
+              f"t={time.perf_counter() - _T0:.1f}s", file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    if os.environ.get("LDM_BENCH_WATCHDOG"):
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["LDM_BENCH_WATCHDOG"]), exit=True)
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
               f"torchrun --nproc-per-node {args.gpus} (or plain python, which spawns them)",
@@ -640,6 +655,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD
 
+    leg("process group up")
     import ldm_sdf
     from ldm_sdf import ops
     from ldm_sdf.dist import slab_bounds
@@ -663,6 +679,7 @@ def main():
                                on_timed=lambda: setattr(slab, "timed", True), local=local,
                                step_events=step_ev)
     slab.timed = False
+    leg("decode steps done")
     kms, qpl = slab.kernel_stats()
     multi = None
     if world > 1:
@@ -677,7 +694,9 @@ def main():
     traffic, traffic_src = decoder_traffic(qpl)
 
     # SURVEY §8(d)'s single-shape headline: ONE shape's 256^3 grid (16.8 M queries), same kernel
+    leg("rank breakdown done")
     b1 = bench_decode_b1(args, rank, world, dev, group, decoder, desc, gen)
+    leg("decode_b1 done")
 
     res = None
     if rank == 0:
@@ -709,18 +728,23 @@ def main():
         if multi is not None:
             res["multi_gpu"] = multi
     if not args.no_ddpm:
+        leg("ddpm")
         r = bench_ddpm(args, rank, world, dev, group, gen, decoder)
         if rank == 0:
             res["ddpm"] = r
     if rank == 0 and not args.no_mc:
+        leg("mc")
         res["mc"] = bench_mc(out[0], args)
     if not args.no_config5:
+        leg("config5")
         res_c5 = config5(args, rank, world, dev, group, gen)
         if rank == 0:
             res["config5"] = res_c5
     if rank == 0 and not args.no_train:
+        leg("train")
         res["train"] = bench_train(args, dev, gen)
     if rank == 0 and not args.no_autodecoder:
+        leg("autodecoder")
         res["autodecoder"] = bench_autodecoder(args, dev)
     if rank == 0 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_decode(N, args.cpu_seconds)
@@ -741,6 +765,7 @@ def main():
                     "gpu_over_cpu": e2e_c / res["ddpm"]["config3_sample_plus_decode128_s"]}
     if rank == 0:
         print(json.dumps(res), flush=True)
+    leg("final barrier")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

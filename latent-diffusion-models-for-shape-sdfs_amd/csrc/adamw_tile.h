@@ -42,19 +42,23 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
     // every load of the thread's 4 rows x 4 columns first (16-byte vectors when the row is
     // aligned and whole), then the updates, then the stores: one memory round trip
     const bool vec = (cols & 3) == 0 && c0 + cq + 4 <= cols;
+    // (ragged columns: a lane past the row's end loads the row's last element instead -- its
+    // value is never stored -- so no load leaves the tensor; round 6, found by the DEBUG build:
+    // the fall-back used to be the lane's first column, itself past the end when c0 + cq >= cols)
     f32x4 p4[4], g4[4], m4[4], v4[4];
-    int64_t off[4];
+    int64_t off[4], in_row[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = min(r0 + (tid >> 4) + 16 * i, rows - 1);
         off[i] = (int64_t)r * cols + c0 + cq;
+        in_row[i] = (int64_t)r * cols;
         if (mode == 2) {                          // the copies: the stored p only
             if (vec) {
                 p4[i] = vld_at<WT, f32x4>(P, x4, off[i]);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    p4[i][e] = vld_at<WT, float>(P, x4, c0 + cq + e < cols ? off[i] + e : off[i]);
+                    p4[i][e] = vld_at<WT, float>(P, x4, in_row[i] + min(c0 + cq + e, cols - 1));
             }
         } else if (vec) {
             p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
@@ -64,7 +68,7 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int64_t x = c0 + cq + e < cols ? off[i] + e : off[i];
+                const int64_t x = in_row[i] + min(c0 + cq + e, cols - 1);
                 p4[i][e] = P[x]; g4[i][e] = vld_at<WT, float>(Gp, x4, x); m4[i][e] = M[x];
                 v4[i][e] = V[x];
             }

@@ -554,11 +554,17 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 #ifndef SL_LDSBLK
 #define SL_LDSBLK 1
 #endif
-// After a layer's publish (A/B, scripts/sampler_time.py): 0 nothing; 1 a scheduling barrier;
-// 2 an s_memrealtime whose value is consumed (the round-5 stamp's mark 4 alone: SL_MARKS = 16
-// ran 94-98k steps/s against 85-86k without, spill-free, profiles/r06d)
+// After a layer's publish: the publishing store stays ahead of the next layer's granule polls
+// in issue order (a scheduling barrier), and the wave sleeps one interval (64 cycles) before it
+// starts polling -- fewer polls hit the lines the other producers are still writing.  What the
+// round-5 stamps did by accident (their mark after the publish: SL_MARKS = 16 alone carried the
+// whole gain, profiles/r06d), now on purpose.  A/B on one box (profiles/r06f, B = 8, steps/s):
+// 0 nothing 84.9-85.9k; 1 the barrier alone 92.4-93.0k; 2 an s_memrealtime read instead 92.9-
+// 93.6k; 3 barrier + s_sleep 1 (product) 96.5-99.0k; 4 the stamp's clock arithmetic kept in a
+// register 97.1-98.1k; the round-5 mark itself 96.7-98.1k.  tests/test_sampler_codegen.py pins
+// the sleep behind every publish.
 #ifndef SL_PUBFENCE
-#define SL_PUBFENCE 0
+#define SL_PUBFENCE 3
 #endif
 __device__ __forceinline__ void after_publish() {
     if (SL_PUBFENCE == 1) __builtin_amdgcn_sched_barrier(0);

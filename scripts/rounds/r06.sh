@@ -4,7 +4,7 @@
 # gpurun_out/<outdir>/; the logs that back a DESIGN.md statement are copied to profiles/<outdir>/.
 #   guards   the one-launch / data-parallel training tests, the whole GPU suite and smoke
 #   debug    the same training tests and the GEMM tests against the DEBUG=1 library
-#            (LDM_DASSERT bounds traps, wt_store.h extents)
+#            (LDM_DASSERT bounds traps, wt_store.h extents), then the whole GPU suite on it
 #   bench    the default bench and the rocprofv3 kernel-trace summary of the same command
 #   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
 #   decoder  the decoder part stamps (scripts/stamp_split.py on each FS_STAMP library in $FS_LIBS)
@@ -36,6 +36,7 @@ case $B in
   debug)
     LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step dag_debug 600 $PYT tests/test_gpu_train_dag.py tests/test_gpu_train_dp.py
     LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step gemm_debug 600 $PYT tests/test_gpu_gemm.py tests/test_gpu_train_capi.py
+    LDM_SDF_LIB=$LIB/libldm_sdf_debug.so TAILN=4 step pytest_gpu_debug 900 $PYT tests -m gpu -k "not test_native_library_is_loaded"
     ;;
   bench)
     TAILN=2 step bench 600 python -u bench.py
@@ -56,7 +57,7 @@ case $B in
   multirank)
     # the N > 1 flow of bench.py (z-slab gathers, rank-0 legs, barriers) rehearsed on one GPU:
     # 2 ranks on cuda:0 over gloo (timings meaningless: both ranks share the device)
-    LDM_BENCH_BACKEND=gloo TAILN=3 step bench_gloo2 900 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --train-steps 5 --ad-steps 1
+    LDM_BENCH_BACKEND=gloo LDM_BENCH_TRACE=1 LDM_BENCH_WATCHDOG=150 TAILN=40 step bench_gloo2 300 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --no-ddpm --no-config5 --train-steps 5 --ad-steps 1
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency

@@ -5,9 +5,12 @@ Round 5's fast sampler depended on a build accident: the loop's weights overflow
 VGPRs a wave has at two waves per SIMD, the compiler spilled residual-block weight vectors to
 scratch and reloaded them SERIALLY every step (scratch_load + s_waitcnt vmcnt(0), 5-6 times),
 and the diagnostic stamps merely changed which values spilled.  Round 6 keeps the last residual
-block's weights in LDS (SL_LDSBLK), which leaves the kernel without any scratch.  This test fails
-if a change (or a compiler update) brings the spills back to the bench's configuration
-(D = 256, B <= 8: sample_replica_kernel<256, 1>), with or without the stamps."""
+block's weights in LDS (SL_LDSBLK), which leaves the kernel without any scratch; and what the
+stamps really bought -- the wave pausing right after a layer's publish before it polls for the
+next layer -- is now built on purpose (SL_PUBFENCE: a scheduling barrier + s_sleep 1).  This test
+fails if a change (or a compiler update) brings the spills back to the bench's configuration
+(D = 256, B <= 8: sample_replica_kernel<256, 1>), with or without the stamps, or separates a
+publish from its pause."""
 import os
 import re
 import shutil
@@ -48,3 +51,17 @@ def test_replica_loop_has_no_scratch(tmp_path, stamp):
     s = _asm(tmp_path, f"-DSL_STAMP={stamp}")
     priv, nscr = _kernel_stats(s, 256, 1)
     assert priv == 0 and nscr == 0, (priv, nscr)
+
+
+def test_every_publish_is_followed_by_its_pause(tmp_path):
+    """The six tagged publishes of a step (8-byte agent-scope stores: global_store_dwordx2 ...
+    sc1) each have the s_sleep of after_publish() within the next few instructions."""
+    s = _asm(tmp_path)
+    n = [x for x in re.findall(r"^(_ZN3ldm\w+sample_replica_kernel\w+):", s, re.M)
+         if "ILi256ELi1E" in x][0]
+    body = s[s.index(n + ":"):s.index(".Lfunc_end", s.index(n + ":"))]
+    ins = [l.strip() for l in body.split("\n") if l.strip() and not l.strip().startswith((";", "."))]
+    pubs = [k for k, l in enumerate(ins) if l.startswith("global_store_dwordx2") and "sc1" in l]
+    assert len(pubs) >= 6, len(pubs)
+    for k in pubs:
+        assert any(l.startswith("s_sleep") for l in ins[k + 1:k + 13]), ins[k:k + 13]
