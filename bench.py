@@ -651,6 +651,12 @@ def main():
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if backend == "gloo":
             dist.init_process_group("gloo")
+            # gloo's coalesced all-gather of DEVICE tensors never completed here (r06i: both
+            # ranks waited on the group's handle for 150 s); the rehearsal takes the per-shape
+            # form, which tests/test_dist_gloo.py pins bitwise to the coalesced one (RCCL runs
+            # the coalesced form)
+            from ldm_sdf.dist import set_gather_mode
+            set_gather_mode("per_shape")
         else:
             dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD

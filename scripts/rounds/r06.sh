@@ -58,6 +58,7 @@ case $B in
     # the N > 1 flow of bench.py (z-slab gathers, rank-0 legs, barriers) rehearsed on one GPU:
     # 2 ranks on cuda:0 over gloo (timings meaningless: both ranks share the device)
     LDM_BENCH_BACKEND=gloo LDM_BENCH_TRACE=1 LDM_BENCH_WATCHDOG=150 TAILN=40 step bench_gloo2 300 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --no-ddpm --no-config5 --train-steps 5 --ad-steps 1
+    LDM_BENCH_BACKEND=gloo LDM_BENCH_TRACE=1 LDM_BENCH_WATCHDOG=170 TAILN=40 step bench_gloo2_all 300 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --train-steps 5 --ad-steps 1
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency
