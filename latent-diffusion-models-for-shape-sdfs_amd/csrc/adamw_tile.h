@@ -22,14 +22,17 @@ struct AdamHyper {
 // mode (the one-launch step's split update, train_dag.hip): 0 the whole update; 1 p, m, v only
 // (no bf16 copies, no barrier); 2 the bf16 copies only, from the p a mode-1 tile stored (read
 // sc1 when WT).  Modes 1 then 2 store exactly what mode 0 stores.
-template <bool WT = false, typename TT>
-__device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
-                                           unsigned short (&sT)[64][64 + 8], int tl,
-                                           int tid = threadIdx.x, int mode = 0) {
+//
+// VEC (the dispatcher below): the tile spans 64 whole columns of a row length divisible by 4,
+// so every lane's 4 columns are one aligned 16-byte vector -- a tile-uniform property, decided
+// once per tile.  (Round 6: decided per lane inside the row loop, the two load forms merged
+// into one set of registers, and the compiler waited for each row's first load before issuing
+// the next row's -- four serial round trips per tile instead of one.)
+template <bool WT, bool VEC, typename TT>
+__device__ __forceinline__ void adamw_tile_body(TT& T, const AdamHyper& hy,
+                                                unsigned short (&sT)[64][64 + 8], int r0, int c0,
+                                                int tid, int mode) {
     const int rows = T.rows, cols = T.cols;
-    const int tcn = (cols + 63) / 64;
-    const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
-    LDM_DASSERT(tl >= 0 && r0 < rows);                  // the tile lies inside the tensor
     // extents (wt_store.h): fp32 p, g, m, v and the bf16 copies, rows x cols each
     const uint32_t x4 = ext_bytes(rows, cols, cols, 4), x2 = ext_bytes(rows, cols, cols, 2);
     const int cq = (tid & 15) * 4;
@@ -39,9 +42,9 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
     const float* __restrict__ Gp = T.g;
     float* __restrict__ M = T.m;
     float* __restrict__ V = T.v;
-    // every load of the thread's 4 rows x 4 columns first (16-byte vectors when the row is
-    // aligned and whole), then the updates, then the stores: one memory round trip
-    const bool vec = (cols & 3) == 0 && c0 + cq + 4 <= cols;
+    // every load of the thread's 4 rows x 4 columns first (16-byte vectors when VEC), then the
+    // updates, then the stores: one memory round trip
+    constexpr bool vec = VEC;
     // (ragged columns: a lane past the row's end loads the row's last element instead -- its
     // value is never stored -- so no load leaves the tensor; round 6, found by the DEBUG build:
     // the fall-back used to be the lane's first column, itself past the end when c0 + cq >= cols)
@@ -52,28 +55,39 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
         const int r = min(r0 + (tid >> 4) + 16 * i, rows - 1);
         off[i] = (int64_t)r * cols + c0 + cq;
         in_row[i] = (int64_t)r * cols;
-        if (mode == 2) {                          // the copies: the stored p only
-            if (vec) {
+    }
+    // the mode test outside the row loop, and a scheduling barrier after the loads: left free,
+    // the scheduler started row 0's update (with its waits) before issuing rows 1-3's loads
+    if (mode == 2) {                              // the copies: the stored p only
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (vec) {
                 p4[i] = vld_at<WT, f32x4>(P, x4, off[i]);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     p4[i][e] = vld_at<WT, float>(P, x4, in_row[i] + min(c0 + cq + e, cols - 1));
             }
-        } else if (vec) {
-            p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
-            g4[i] = vld_at<WT, f32x4>(Gp, x4, off[i]);     // (WT: the handed-off gradient, sc1)
-            m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
-            v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
-        } else {
+        }
+    } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t x = in_row[i] + min(c0 + cq + e, cols - 1);
-                p4[i][e] = P[x]; g4[i][e] = vld_at<WT, float>(Gp, x4, x); m4[i][e] = M[x];
-                v4[i][e] = V[x];
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (vec) {
+                p4[i] = *reinterpret_cast<const f32x4*>(P + off[i]);
+                g4[i] = vld_at<WT, f32x4>(Gp, x4, off[i]);  // (WT: the handed-off gradient, sc1)
+                m4[i] = *reinterpret_cast<const f32x4*>(M + off[i]);
+                v4[i] = *reinterpret_cast<const f32x4*>(V + off[i]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t x = in_row[i] + min(c0 + cq + e, cols - 1);
+                    p4[i][e] = P[x]; g4[i][e] = vld_at<WT, float>(Gp, x4, x); m4[i][e] = M[x];
+                    v4[i][e] = V[x];
+                }
             }
         }
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int rl = (tid >> 4) + 16 * i;
@@ -91,7 +105,7 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
             sT[cq + e][rl] = rin ? q[e] : (unsigned short)0;
         }
         if (!rin) continue;
-        if (vec) {
+        if constexpr (vec) {
             if (mode != 2) {
                 vst_at<WT>(P, x4, off[i], p4[i]);
                 vst_at<WT>(M, x4, off[i], m4[i]);
@@ -141,6 +155,20 @@ __device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
             if (r < rows) vst_at<WT>(dst, x2, cr + r, sT[cl][rb + e]);
         }
     }
+}
+
+template <bool WT = false, typename TT>
+__device__ __forceinline__ void adamw_tile(TT& T, const AdamHyper& hy,
+                                           unsigned short (&sT)[64][64 + 8], int tl,
+                                           int tid = threadIdx.x, int mode = 0) {
+    const int cols = T.cols;
+    const int tcn = (cols + 63) / 64;
+    const int r0 = (tl / tcn) * 64, c0 = (tl % tcn) * 64;
+    LDM_DASSERT(tl >= 0 && r0 < T.rows);                // the tile lies inside the tensor
+    if ((cols & 3) == 0 && c0 + 64 <= cols)
+        adamw_tile_body<WT, true>(T, hy, sT, r0, c0, tid, mode);
+    else
+        adamw_tile_body<WT, false>(T, hy, sT, r0, c0, tid, mode);
 }
 
 }  // namespace ldm

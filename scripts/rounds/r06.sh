@@ -9,6 +9,7 @@
 #   sampler  the sampler build A/B (scripts/sampler_time.py against each library in $SL_LIBS)
 #   decoder  the decoder part stamps (scripts/stamp_split.py on each FS_STAMP library in $FS_LIBS)
 #   multirank  bench.py --gpus 2 with both ranks on cuda:0 over gloo (the N > 1 control flow)
+#   adam     AdamW tile A/B over the libraries in $AD_LIBS (kernel time, config-2 step)
 #   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
 #            and scripts/microbench/acc_range (a k-step on each of two live accumulator sets)
 #   first    config 3's first call in a fresh process, with a kernel + HIP API trace
@@ -59,6 +60,16 @@ case $B in
     # 2 ranks on cuda:0 over gloo (timings meaningless: both ranks share the device)
     LDM_BENCH_BACKEND=gloo LDM_BENCH_TRACE=1 LDM_BENCH_WATCHDOG=150 TAILN=40 step bench_gloo2 300 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --no-ddpm --no-config5 --train-steps 5 --ad-steps 1
     LDM_BENCH_BACKEND=gloo LDM_BENCH_TRACE=1 LDM_BENCH_WATCHDOG=170 TAILN=40 step bench_gloo2_all 300 python -u bench.py --gpus 2 --steps 1 --warmup 1 --no-cpu --train-steps 5 --ad-steps 1
+    ;;
+  adam)
+    # the AdamW tile A/B: correctness first, then kernel time and the config-2 step per library
+    TAILN=3 step adam_tests 400 $PYT tests/test_gpu_train_capi.py tests/test_gpu_train_dag.py
+    for rep in 1 2; do
+      for L in ${AD_LIBS:?}; do
+        LDM_SDF_LIB=$LIB/$L TAILN=1 step adamw_${L%.so}_$rep 120 python -u scripts/adamw_time.py
+        LDM_SDF_LIB=$LIB/$L TAILN=3 step train_${L%.so}_$rep 300 python -u scripts/train_form_ab.py 3 128
+      done
+    done
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency
