@@ -10,6 +10,8 @@
 #   decoder  the decoder part stamps (scripts/stamp_split.py on each FS_STAMP library in $FS_LIBS)
 #   multirank  bench.py --gpus 2 with both ranks on cuda:0 over gloo (the N > 1 control flow)
 #   adam     AdamW tile A/B over the libraries in $AD_LIBS (kernel time, config-2 step)
+#   dlib     decoder build A/B over the libraries in $DEC_LIBS (scripts/decode_time.py)
+#   mregs    scripts/microbench/mfma_regs (a k-step's speed vs the registers of its operands)
 #   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
 #            and scripts/microbench/acc_range (a k-step on each of two live accumulator sets)
 #   first    config 3's first call in a fresh process, with a kernel + HIP API trace
@@ -70,6 +72,18 @@ case $B in
         LDM_SDF_LIB=$LIB/$L TAILN=3 step train_${L%.so}_$rep 300 python -u scripts/train_form_ab.py 3 128
       done
     done
+    ;;
+  dlib)
+    # decoder build A/B: scripts/decode_time.py per library in $DEC_LIBS, alternating
+    for rep in 1 2 3; do
+      for L in ${DEC_LIBS:?}; do
+        LDM_SDF_LIB=$LIB/$L TAILN=1 step dec_${L%.so}_$rep 120 python -u scripts/decode_time.py 8 256 5
+      done
+    done
+    ;;
+  mregs)
+    TAILN=30 step mfma_regs 120 ./scripts/microbench/mfma_regs
+    TAILN=28 step loop_replay 120 ./scripts/microbench/loop_replay
     ;;
   lds)
     TAILN=14 step lds_half 120 ./scripts/microbench/lds_half_latency
