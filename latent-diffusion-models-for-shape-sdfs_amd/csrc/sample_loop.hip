@@ -556,15 +556,23 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 #endif
 // After a layer's publish: the publishing store stays ahead of the next layer's granule polls
 // in issue order (a scheduling barrier), and the wave sleeps one interval (64 cycles) before it
-// starts polling -- fewer polls hit the lines the other producers are still writing.  What the
+// starts polling -- fewer polls hit the lines the other producers are still writing (the
+// pause's length: SL_PUBSLEEP below).  What the
 // round-5 stamps did by accident (their mark after the publish: SL_MARKS = 16 alone carried the
 // whole gain, profiles/r06d), now on purpose.  A/B on one box (profiles/r06f, B = 8, steps/s):
 // 0 nothing 84.9-85.9k; 1 the barrier alone 92.4-93.0k; 2 an s_memrealtime read instead 92.9-
-// 93.6k; 3 barrier + s_sleep 1 (product) 96.5-99.0k; 4 the stamp's clock arithmetic kept in a
+// 93.6k; 3 barrier + s_sleep 1 96.5-99.0k (the product form); 4 the stamp's clock arithmetic kept in a
 // register 97.1-98.1k; the round-5 mark itself 96.7-98.1k.  tests/test_sampler_codegen.py pins
 // the sleep behind every publish.
 #ifndef SL_PUBFENCE
 #define SL_PUBFENCE 3
+#endif
+// The pause, in s_sleep units of 64 cycles.  Swept on one box (profiles/r06s, r06t, B = 8,
+// steps/s): 1 96.3-98.6k, 2 100.6-101.8k, 3 101.8-104.5k, 4 104.1-104.7k, 6 102.1-103.0k,
+// 8 99.7-100.3k, 12 94.8-95.2k; a sleep between re-polls of a missing granule instead
+// (LDM_GRAN_SLEEP 1) 90-94k.
+#ifndef SL_PUBSLEEP
+#define SL_PUBSLEEP 4
 #endif
 __device__ __forceinline__ void after_publish() {
     if (SL_PUBFENCE == 1) __builtin_amdgcn_sched_barrier(0);
@@ -574,7 +582,7 @@ __device__ __forceinline__ void after_publish() {
     }
     if (SL_PUBFENCE == 3) {
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(SL_PUBSLEEP);
     }
 }
 // SL_PUBFENCE 4: the round-5 stamp's mark 4 alone, kept in a register (no global stamp buffer):
