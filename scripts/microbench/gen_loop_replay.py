@@ -67,7 +67,18 @@ def _no_loads(body):
     return [t for t in _no_vm(body) if not t.startswith("buffer_load")]
 
 
-VARIANTS = [("L1p1_late_vm", _late_vm), ("L1p1_no_vm", _no_vm), ("L1p1_no_loads", _no_loads)]
+def _bar(every):
+    """a workgroup barrier (the decoder's fs_bar: lgkmcnt(0) + s_barrier) at the top of every
+    `every`-th 4-step group: the body repeated every // 4 times, the barrier before the first
+    copy -- the waves restart in lock step, as after the decoder's in-step barriers"""
+    def f(body):
+        core, tail = body[:-2], body[-2:]
+        return ["s_waitcnt lgkmcnt(0)", "s_barrier"] + core * (every // 4 - 1) + core + tail
+    return f
+
+
+VARIANTS = [("L1p1_late_vm", _late_vm), ("L1p1_no_vm", _no_vm), ("L1p1_no_loads", _no_loads),
+            ("L1p1_bar4", _bar(4)), ("L1p1_bar16", _bar(16)), ("L7p0_bar16", None)]
 
 
 def kernel(name, body):
@@ -138,7 +149,7 @@ def main():
     # variants of L1p1's body: where the ring's vmcnt waits sit
     base = ls[1]
     for vn, f in VARIANTS:
-        print(kernel(vn, f(base)))
+        print(kernel(vn, _bar(16)(ls[8]) if f is None else f(base)))
     names += [vn for vn, _ in VARIANTS]
     print('''typedef void (*KFn)(const void*, unsigned long long*);
 int main() {
