@@ -571,6 +571,17 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 // steps/s): 1 96.3-98.6k, 2 100.6-101.8k, 3 101.8-104.5k, 4 104.1-104.7k, 6 102.1-103.0k,
 // 8 99.7-100.3k, 12 94.8-95.2k; a sleep between re-polls of a missing granule instead
 // (LDM_GRAN_SLEEP 1) 90-94k.
+// Double-buffered activation stage (SL_XSDB 1): layer L stages into xs[L & 1] and its abort
+// flag is slot L % 3, so the workgroup barrier BEFORE a layer's granule polls (the WAR guard on
+// the single xs buffer, and the flag reset) goes.  WAR on xs[L & 1]: its last reads were layer
+// L - 2's rows, and every wave finishes those before it arrives at layer L - 1's post-poll
+// barrier, which every writer of layer L has passed.  Flag slot (L + 1) % 3 is reset during
+// layer L by thread 0: its last readers (layer L - 2, right after their post-poll barrier)
+// passed layer L - 1's barrier before thread 0 could get here, and any layer-(L + 1) failure
+// write comes after layer L's barrier, which thread 0 reaches only after the reset.
+#ifndef SL_XSDB
+#define SL_XSDB 0
+#endif
 #ifndef SL_PUBSLEEP
 #define SL_PUBSLEEP 4
 #endif
@@ -646,14 +657,15 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     constexpr int NV = R * MBX, LB = NV >= 16 ? 4 : NV >= 8 ? 3 : NV >= 4 ? 2 : 1;
     constexpr int NT = 64 * NWV;
     static_assert(RO * MBX <= NV, "out-projection values fit the reduce-scatter");
-    // LDS: [4] flags | xs [MBX][H] | in-proj weights [8 waves][R][NJD][64 lanes] u32x4 |
+    // LDS: [4] flags | xs [1 + SL_XSDB][MBX][H] | in-proj weights [8 waves][R][NJD][64 lanes] u32x4 |
     //      out-proj weights [8 waves][RO][NJH][64] u32x4 | the last SL_LDSBLK blocks' weights
     //      [SL_LDSBLK][8 waves][R][NJH][64] u32x4.  The other residual blocks' weights (32 VGPRs
     //      of bf16 pairs each) live in registers.
     extern __shared__ __attribute__((aligned(16))) float smem[];
     int* ok = reinterpret_cast<int*>(smem);
-    float* xs = smem + 4;
-    u32x4* lwi = reinterpret_cast<u32x4*>(smem + 4 + MBX * H);
+    float* const xsb = smem + 4;                         // [1 + SL_XSDB][MBX][H]
+    float* xs = xsb;
+    u32x4* lwi = reinterpret_cast<u32x4*>(smem + 4 + (1 + SL_XSDB) * MBX * H);
     u32x4* lwo = lwi + NWV * R * NJD * 64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned* sync = a.ctr;
@@ -670,6 +682,9 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     __syncthreads();
     if (!*ok) return;
     const unsigned xcc = s_xcc, nloc = s_nloc;
+    // every wave has read ok[0] above; the slots are set before the first layer's barrier
+    // (the step-0 in-projection stage's)
+    if (threadIdx.x == 0) ok[0] = ok[1] = ok[2] = 1;
     const int B = a.B, D = D_;
     const int nsh = (B > (int)xcc) + (B > (int)xcc + 8);     // shapes of this replica
     if (nsh == 0) return;                                     // idle replica (B < 8)
@@ -732,6 +747,17 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
     };
     // stage this replica's [MBX][K] activations of the layer that published under tag `tg`
     SlStamp stp;
+    // each staged layer's buffer and abort-flag slot (SL_XSDB), in the order every wave stages
+    int lyr = 0;
+    int* okc = ok;
+    auto begin_layer = [&]() {
+        if (SL_XSDB) {
+            xs = xsb + (size_t)(lyr & 1) * MBX * H;
+            okc = ok + lyr % 3;
+            if (threadIdx.x == 0) ok[(lyr + 1) % 3] = 1;
+        }
+        ++lyr;
+    };
     auto stage_act = [&](float* dst, const float* plain, const u64* gran, int K, unsigned tg) {
         if (!tagged || gran == nullptr) {
 #pragma unroll
@@ -739,8 +765,10 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
             __syncthreads();
             return true;
         }
-        if (threadIdx.x == 0) *ok = 1;
-        __syncthreads();
+        if (!SL_XSDB) {
+            if (threadIdx.x == 0) *okc = 1;
+            __syncthreads();
+        }
         // only this replica's nsh shapes are published (rows of a missing second shape are
         // computed on whatever the LDS holds and never written)
 #if SL_PRIO
@@ -751,10 +779,10 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         __builtin_amdgcn_s_setprio(SL_PRIO);
 #endif
         stp.mark(0);
-        if (!good) *ok = 0;
+        if (!good) *okc = 0;
         __syncthreads();
         stp.mark(1);
-        return *ok != 0;
+        return *okc != 0;
     };
     stp.start();
     PubClock pclk;
@@ -775,6 +803,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         const float c1 = a.c1[t], c2 = a.c2[t], sg = a.sg[t];
         // in-projection over this replica's shapes (step 0: the caller's x; later: the
         // previous out-projection's tagged granules)
+        begin_layer();
         if (tagged && s > 0) {
             if (!stage_act(xs, nullptr, xgr + (size_t)(s & 1) * MBX * D, D, phase)) return;
         } else {
@@ -808,6 +837,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
             if (!alive) return;
             const float* hin = hrep + (size_t)(k & 1) * MBX * H;
             float* hout = hrep + (size_t)((k + 1) & 1) * MBX * H;
+            begin_layer();
             if (!stage_act(xs, hin, tagged ? hgr + (size_t)(k & 1) * MBX * H : nullptr, H,
                            phase)) {
                 alive = false;
@@ -843,6 +873,7 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
         block(std::integral_constant<int, 2>{});
         block(std::integral_constant<int, 3>{});
         if (!alive) return;
+        begin_layer();
         if (!stage_act(xs, hrep + (size_t)(NB & 1) * MBX * H,
                        tagged ? hgr + (size_t)(NB & 1) * MBX * H : nullptr, H, phase))
             return;
@@ -923,7 +954,7 @@ int cur_dev() {
 size_t replica_lds(int D, int MBX) {
     const int H = 1024, W = kRepWaves, R = H / (32 * W), RO = D / (32 * W);
     const int NJD = (D + 511) / 512, NJH = 2;
-    return 16 + (size_t)MBX * H * 4 +
+    return 16 + (size_t)(1 + SL_XSDB) * MBX * H * 4 +
            (size_t)W * (R * NJD + RO * NJH + SL_LDSBLK * R * NJH) * 64 * 16;
 }
 

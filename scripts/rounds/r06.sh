@@ -48,6 +48,7 @@ case $B in
     head -12 $O/bench_kernel_stats.csv
     ;;
   sampler)
+    [ -n "${SL_TESTS:-}" ] && TAILN=3 step sampler_tests 600 $PYT tests/test_gpu_ddpm.py tests/test_sampler_codegen.py
     for L in ${SL_LIBS:?}; do
       LDM_SDF_LIB=$LIB/$L TAILN=3 step sampler_${L%.so} 300 python -u scripts/sampler_time.py
     done
