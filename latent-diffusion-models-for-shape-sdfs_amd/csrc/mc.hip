@@ -438,6 +438,44 @@ __global__ __launch_bounds__(256) void mc_vertices_kernel(const float* __restric
 // can reference (its 12 edges, owned by corners 0..6) is formed from ONE round of 14
 // independent gathers (code and vofs of the 7 owner corners), kept in LDS per thread, and the
 // triangles are read off the table.
+// MC_FACES_PAIR (round 6): a thread takes its cubes with triangles two at a time, from a bit
+// mask, with both cubes' 28 gathers issued before either is used.  The earlier form walked the
+// thread's 16 points in order and gathered inside the walk: a wave paid one serial round trip
+// for every point index at which ANY of its lanes had a cube, up to 16 per wave.
+#ifndef MC_FACES_PAIR
+#define MC_FACES_PAIR 1
+#endif
+__device__ __forceinline__ void mc_gather_owners(const unsigned short* __restrict__ code,
+                                                 const int32_t* __restrict__ vofs, int64_t p,
+                                                 int64_t N, int64_t NN, unsigned (&oc)[7],
+                                                 int (&ov)[7]) {
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+        const int64_t o = p + (s & 1) + ((s >> 1) & 1) * N + ((s >> 2) & 1) * NN;
+        oc[s] = code[o];
+        ov[s] = vofs[o];
+    }
+}
+
+// one cube's triangles: vertex ids through the thread's LDS slots, faces at `off` (the cube's
+// first triangle); oc[0] is the cube's own code
+__device__ __forceinline__ void mc_emit_cube(const unsigned (&oc)[7], const int (&ov)[7], int* ev,
+                                             const signed char* s_tri, int off,
+                                             int32_t* __restrict__ faces) {
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+        const int s = mc_edge_start(e), a = e >> 2;
+        ev[e * 256] = ov[s] + __popc(oc[s] & 7u & ((1u << a) - 1u));
+    }
+    const int ntq = ntri_of(oc[0]);
+    const signed char* tr = s_tri + (oc[0] >> 8) * 16;
+    for (int t = 0; t < ntq; ++t) {
+        int32_t* dst = faces + (int64_t)(off + t) * 3;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) dst[r] = ev[tr[3 * t + r] * 256];
+    }
+}
+
 __global__ __launch_bounds__(256) void mc_faces_kernel(int N, const unsigned short* __restrict__ code,
                                                        const int2* __restrict__ boff,
                                                        const int32_t* __restrict__ vofs,
@@ -457,30 +495,41 @@ __global__ __launch_bounds__(256) void mc_faces_kernel(int N, const unsigned sho
     if (nt == 0) return;
     const int64_t p0 = (int64_t)blockIdx.x * kChunk + threadIdx.x * kPer;
     int* ev = &s_ev[0][threadIdx.x];
+    if (MC_FACES_PAIR) {
+        unsigned am = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) am |= (ntri_of(c[q]) ? 1u : 0u) << q;
+        // the first triangle of the cube at point q: the thread's offset + the counts before q
+        auto first = [&](int q) {
+            int f = off;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) f += u < q ? ntri_of(c[u]) : 0;
+            return f;
+        };
+        while (am) {
+            const int qa = __builtin_ctz(am);
+            am &= am - 1u;
+            const bool hb = am != 0u;
+            const int qb = hb ? __builtin_ctz(am) : qa;
+            if (hb) am &= am - 1u;
+            unsigned oa[7], ob[7];
+            int va[7], vb[7];
+            mc_gather_owners(code, vofs, p0 + qa, N, NN, oa, va);   // a cube with triangles:
+            mc_gather_owners(code, vofs, p0 + qb, N, NN, ob, vb);   // every owner in bounds
+            mc_emit_cube(oa, va, ev, s_tri, first(qa), faces);
+            if (hb) mc_emit_cube(ob, vb, ev, s_tri, first(qb), faces);
+        }
+        return;
+    }
     for (int q = 0; q < kPer; ++q) {
         const int ntq = ntri_of(c[q]);
         if (!ntq) continue;
         const int64_t p = p0 + q;            // a cube with triangles: every owner is in bounds
         unsigned oc[7];
         int ov[7];
-#pragma unroll
-        for (int s = 0; s < 7; ++s) {
-            const int64_t o = p + (s & 1) + ((s >> 1) & 1) * (int64_t)N + ((s >> 2) & 1) * NN;
-            oc[s] = code[o];
-            ov[s] = vofs[o];
-        }
-#pragma unroll
-        for (int e = 0; e < 12; ++e) {
-            const int s = mc_edge_start(e), a = e >> 2;
-            ev[e * 256] = ov[s] + __popc(oc[s] & 7u & ((1u << a) - 1u));
-        }
-        const signed char* tr = s_tri + (c[q] >> 8) * 16;
-        for (int t = 0; t < ntq; ++t) {
-            int32_t* dst = faces + (int64_t)off * 3;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) dst[r] = ev[tr[3 * t + r] * 256];
-            ++off;
-        }
+        mc_gather_owners(code, vofs, p, N, NN, oc, ov);
+        mc_emit_cube(oc, ov, ev, s_tri, off, faces);
+        off += ntq;
     }
 }
 

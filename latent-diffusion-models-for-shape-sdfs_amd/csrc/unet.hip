@@ -45,6 +45,8 @@
 namespace ldm {
 namespace {
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
 __host__ __device__ constexpr int round16(int c) { return (c + 15) & ~15; }
 // Position of channel ci inside its 16-group so that lane group g reads channels
 // 16c + 4m + g (m = 0..3: four consecutive MFMAs) as one 16-byte vector.
@@ -439,10 +441,26 @@ __device__ __forceinline__ G make_geo(KConv& a, KPlan& pl) {
 // The tile after its operands are staged (and the staging barrier passed): the MFMA
 // contraction split over the 4 waves, the partial tiles summed in wave order, the fused
 // epilogue.
-template <typename TW, int TP, typename GEO, typename ST>
+// A chunk's A fragment held in registers (MAXC > 0, the fast kernel's register weights): the
+// lane's 4 consecutive weights of row co0 + c16 -- 8 bytes of bf16 or 16 of fp32 -- as loaded.
+template <typename TW>
+struct WFrag {
+    typedef typename std::conditional<sizeof(TW) == 2, u32x2, u32x4>::type V;
+};
+template <typename TW>
+__device__ __forceinline__ f32x4 wfrag_unpack(const typename WFrag<TW>::V& w) {
+    if constexpr (sizeof(TW) == 2)
+        return f32x4{__builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
+                     __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
+    else
+        return __builtin_bit_cast(f32x4, w);
+}
+
+template <typename TW, int TP, int MAXC = 0, typename GEO, typename ST>
 __device__ __forceinline__ void conv_finish(KConv& a, const GEO& geo, const ConvIO& io,
                                             float* sm, int pos0, int co0, int b,
-                                            const EpiOps<TP>& e, ST& st_) {
+                                            const EpiOps<TP>& e, ST& st_,
+                                            const typename WFrag<TW>::V* aw = nullptr) {
     constexpr int NT = TP / 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4, c16 = lane & 15;
@@ -515,9 +533,34 @@ __device__ __forceinline__ void conv_finish(KConv& a, const GEO& geo, const Conv
             for (int t = 0; t < NT; ++t)
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[t][m], acc[t], 0, 0, 0);
     };
+    const int n = c_end - c_beg;
+    if constexpr (MAXC > 0) {
+        // register weights: chunk j of this wave takes its A fragment from aw[j] (loaded at the
+        // kernel's start) and its B fragments from LDS; the same accumulator set per chunk
+        // parity and the same order within a set as the LDS form below, so the same bits
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) {
+            if (j >= n) break;
+            const f32x4 av = wfrag_unpack<TW>(aw[j]);
+            f32x4 bv[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                bv[t] = *reinterpret_cast<const f32x4*>(
+                    sm + xbase + ((t * 16 + c16) * st + k) * xld + cg * 16);
+            if (++cg == ng) {
+                cg = 0;
+                if (++k == ks && si + 1 < n_seg) {
+                    k = 0;
+                    set_seg(++si);
+                }
+            }
+            if (j & 1) mfma4(acc1, av, bv);
+            else mfma4(acc0, av, bv);
+        }
+        st_.mark(8);
+    } else {
     // two pairs in flight (ping-pong, no register copies), chunks alternating between the two
     // accumulator sets so consecutive MFMAs are independent
-    const int n = c_end - c_beg;
     f32x4 pa0, pa1, pb0, pb1, qa0[NT], qa1[NT], qb0[NT], qb1[NT];
     if (n > 0) {
         load_chunk(pa0, qa0);
@@ -552,6 +595,7 @@ __device__ __forceinline__ void conv_finish(KConv& a, const GEO& geo, const Conv
         } else {
             mfma4(acc0, pb0, qb0);
         }
+    }
     }
     f32x4 acc[NT];
 #pragma unroll
@@ -778,10 +822,51 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvKArgs ka) {
 #endif
 }
 
+// Register weights (MAXC > 0, round 6): instead of staging the tile's weights into LDS (fp32,
+// 16 rows x every tap and channel: loads, bf16 unpack, LDS stores and the barrier's share), every
+// lane loads exactly the A fragments its wave's chunks use -- 4 consecutive weights of its row
+// per chunk, 8 bytes (bf16) -- straight from the packed rows into registers, in the staging's
+// single round trip.  The weights are the same values, the contraction the same order: the same
+// bits.  Chunk iteration as conv_finish's.
+template <typename TW, int MAXC, typename GEO>
+__device__ __forceinline__ void wreg_issue(typename WFrag<TW>::V (&aw)[MAXC], KConv& a,
+                                           const GEO& geo, int co0) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int nch = geo.nchunks(), n_seg = geo.n_seg();
+    const int c_beg = nch * wv / 4, c_end = nch * (wv + 1) / 4;
+    int si = 0;
+    while (si + 1 < n_seg && c_beg >= geo.ch0(si + 1)) ++si;
+    int ng = geo.cinp(si) >> 4, ks = geo.ks(si), k = 0, cg = c_beg - geo.ch0(si);
+    while (cg >= ng) { cg -= ng; ++k; }
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+        const bool live = c_beg + j < c_end;
+        KSeg& sg = a.seg[si];
+        const __amdgpu_buffer_rsrc_t rs = rsrc(sg.W, 0x7ffffff0u);
+        uint32_t off = ((uint32_t)(co0 + c16) * (uint32_t)sg.ldw + (uint32_t)(k * sg.kstride) +
+                        (uint32_t)(cg * 16 + 4 * g)) * (uint32_t)sizeof(TW);
+        off = live ? off : 0xfffffff0u;               // past the chunks: no memory access
+        if constexpr (sizeof(TW) == 2)
+            aw[j] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+        else
+            aw[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        if (live && ++cg == ng) {
+            cg = 0;
+            if (++k == ks && si + 1 < n_seg) {
+                k = 0;
+                ++si;
+                ng = geo.cinp(si) >> 4;
+                ks = geo.ks(si);
+            }
+        }
+    }
+}
+
 // The direct-staging launch kernel (see fast_* above): NS segments, all staged in one round
 // trip when they fit the per-thread budgets (the first round of every segment is issued before
 // any store; a segment with more items runs extra rounds after), then conv_finish.
-template <typename TW, int TP, int NS, int NBW>
+template <typename TW, int TP, int NS, int NBW, int MAXC = 0>
 __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const LDM_KC ConvKArgs* k = (const LDM_KC ConvKArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -803,11 +888,15 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     // access, but TA issue), so the slots match the launch: 4-slot weights and windows at every
     // size cost ~1 us per small conv (profiles/r04g).
     constexpr int NBX = TP / 16;
-    u32x4 wv[NS][NBW];
+    constexpr bool WREG = MAXC > 0;
+    constexpr int NBWS = WREG ? 1 : NBW;               // (no weight staging slots)
+    u32x4 wv[NS][NBWS];
+    typename WFrag<TW>::V aw[WREG ? MAXC : 1];
     f32x4 xv[NS][NBX][4];
+    if constexpr (WREG) wreg_issue<TW, MAXC>(aw, a, geo, co0);
 #pragma unroll
     for (int si = 0; si < NS; ++si) {
-        fast_w_issue<TW, NBW>(wv[si], a.seg[si], pl.s[si], co0, 0);
+        if constexpr (!WREG) fast_w_issue<TW, NBW>(wv[si], a.seg[si], pl.s[si], co0, 0);
         fast_x_issue<NBX>(xv[si], a.seg[si], pl.s[si], a.seg[si].X, b, pos0, 0);
     }
     EpiOps<TP> e;
@@ -819,10 +908,16 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     // round trip per part again.  (Empty asm: a memory clobber orders the loads; the register
     // operands make every use of the loaded values come after it.)
     asm volatile("" ::: "memory");
+    if constexpr (WREG) {
+#pragma unroll
+        for (int j = 0; j < MAXC; ++j) asm volatile("" : "+v"(aw[j]));
+    }
 #pragma unroll
     for (int si = 0; si < NS; ++si) {
+        if constexpr (!WREG) {
 #pragma unroll
-        for (int u = 0; u < NBW; ++u) asm volatile("" : "+v"(wv[si][u]));
+            for (int u = 0; u < NBW; ++u) asm volatile("" : "+v"(wv[si][u]));
+        }
 #pragma unroll
         for (int u = 0; u < NBX; ++u)
 #pragma unroll
@@ -834,13 +929,14 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     }
 #pragma unroll
     for (int si = 0; si < NS; ++si) {
-        fast_w_store<TW, NBW>(wv[si], sm, a.seg[si], pl.s[si], 0);
+        if constexpr (!WREG) fast_w_store<TW, NBW>(wv[si], sm, a.seg[si], pl.s[si], 0);
         fast_x_store<NBX>(xv[si], sm, a.seg[si], pl.s[si], pos0, 0);
     }
     sr.mark(3);
     sr.mark(4);
 #pragma unroll
     for (int si = 0; si < NS; ++si) {
+        if constexpr (!WREG)
         for (int base = 256 * NBW; base < pl.s[si].nw; base += 256 * NBW) {
             u32x4 v[NBW];
             fast_w_issue<TW, NBW>(v, a.seg[si], pl.s[si], co0, base);
@@ -855,7 +951,7 @@ __global__ __launch_bounds__(256) void conv1d_fast_kernel(ConvKArgs ka) {
     sr.mark(5);
     __syncthreads();
     sr.mark(1);
-    conv_finish<TW, TP>(a, geo, io, sm, pos0, co0, b, e, sr);
+    conv_finish<TW, TP, MAXC>(a, geo, io, sm, pos0, co0, b, e, sr, aw);
 #if UNET_STAMP
     stamps_flush(sr);
 #endif
@@ -906,15 +1002,24 @@ int make_plan(const ldm_conv1d_args_t& a, int TP, ConvPlan* pl, int* lds_bytes) 
     return *lds_bytes <= kMaxLdsBytes ? 0 : LDM_ENOSPC;
 }
 
-template <typename TW, int TP, int NS, int NBW>
+template <typename TW, int TP, int NS, int NBW, int MAXC = 0>
 int launch_fast(const ConvKArgs& ka, dim3 grid, int lds, hipStream_t s) {
-    LDM_TRY((set_max_lds_once<&conv1d_fast_kernel<TW, TP, NS, NBW>>(kMaxLdsBytes, "conv1d")));
-    hipLaunchKernelGGL((conv1d_fast_kernel<TW, TP, NS, NBW>), grid, dim3(256), lds, s, ka);
+    LDM_TRY((set_max_lds_once<&conv1d_fast_kernel<TW, TP, NS, NBW, MAXC>>(kMaxLdsBytes, "conv1d")));
+    hipLaunchKernelGGL((conv1d_fast_kernel<TW, TP, NS, NBW, MAXC>), grid, dim3(256), lds, s, ka);
     return launch_status("ldm_conv1d");
 }
 
+// register weights (conv1d_fast_kernel MAXC) when every wave's chunks fit kWregChunks
+// (UNET_WREG 0: the LDS-staged weights, the round-5 form)
+#ifndef UNET_WREG
+#define UNET_WREG 1
+#endif
+constexpr int kWregChunks = 8;
+
 template <typename TW, int TP, int NS>
 int launch_fast_nbw(const ConvKArgs& ka, dim3 grid, int lds, hipStream_t s) {
+    if (UNET_WREG && ka.pl.nchunks <= 4 * kWregChunks && dev_knob("LDM_CONV_WREG", 1))
+        return launch_fast<TW, TP, NS, 1, kWregChunks>(ka, grid, lds, s);
     int nw = 0;
     for (int i = 0; i < NS; ++i) nw = ka.pl.s[i].nw > nw ? ka.pl.s[i].nw : nw;
     if (nw <= 256) return launch_fast<TW, TP, NS, 1>(ka, grid, lds, s);

@@ -26,5 +26,8 @@ for _ in range(reps):
     v, f = ldm_sdf.marching_cubes(vol, ws=ws)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / reps
-print(f"N={N}: {v.shape[0]} vertices, {f.shape[0]} faces, {dt * 1e3:.3f} ms per mesh (wall, incl. "
-      f"the count read-back)")
+import hashlib  # noqa: E402
+h = hashlib.sha1(v.cpu().numpy().tobytes() + f.cpu().numpy().tobytes()).hexdigest()[:16]
+print(f"lib {os.path.basename(os.environ.get('LDM_SDF_LIB', 'libldm_sdf.so'))} N={N}: "
+      f"{v.shape[0]} vertices, {f.shape[0]} faces, {dt * 1e3:.3f} ms per mesh (wall, incl. "
+      f"the count read-back), mesh {h}")

@@ -11,6 +11,8 @@
 #   multirank  bench.py --gpus 2 with both ranks on cuda:0 over gloo (the N > 1 control flow)
 #   adam     AdamW tile A/B over the libraries in $AD_LIBS (kernel time, config-2 step)
 #   dlib     decoder build A/B over the libraries in $DEC_LIBS (scripts/decode_time.py)
+#   mc       marching-cubes build A/B over the libraries in $MC_LIBS (+ tests with MC_TESTS=1)
+#   unet     UNet build A/B over the libraries in $UNET_LIBS (+ tests with UNET_TESTS=1)
 #   mregs    scripts/microbench/mfma_regs (a k-step's speed vs the registers of its operands)
 #   lds      scripts/microbench/lds_half_latency (LDS read latency / stream below vs above 64 KiB)
 #            and scripts/microbench/acc_range (a k-step on each of two live accumulator sets)
@@ -79,6 +81,27 @@ case $B in
     for rep in 1 2 3; do
       for L in ${DEC_LIBS:?}; do
         LDM_SDF_LIB=$LIB/$L TAILN=1 step dec_${L%.so}_$rep 120 python -u scripts/decode_time.py 8 256 5
+      done
+    done
+    ;;
+  mc)
+    # marching-cubes build A/B: wall time per mesh and the rocprof kernel stats, per library
+    [ -n "${MC_TESTS:-}" ] && TAILN=3 step mc_tests 300 $PYT tests/test_gpu_mc.py
+    for rep in 1 2; do
+      for L in ${MC_LIBS:?}; do
+        LDM_SDF_LIB=$LIB/$L TAILN=1 step mc_${L%.so}_$rep 120 python -u scripts/mc_once.py 50
+        LDM_SDF_LIB=$LIB/$L TAILN=1 step mcprof_${L%.so}_$rep 300 rocprofv3 --kernel-trace --stats -d $O/mcprof_${L%.so}_$rep -o mc --output-format csv -- python3 scripts/mc_once.py 50
+        find $O/mcprof_${L%.so}_$rep -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/mc_kernel_stats_${L%.so}_$rep.csv
+      done
+    done
+    ;;
+  unet)
+    # UNet build A/B: steps/s at B = 1 and B = 8 and the sample's hash, per library
+    [ -n "${UNET_TESTS:-}" ] && TAILN=3 step unet_tests 600 $PYT tests/test_gpu_unet.py
+    for rep in 1 2; do
+      for L in ${UNET_LIBS:?}; do
+        LDM_SDF_LIB=$LIB/$L UNET_REPS=3 TAILN=3 step unet_${L%.so}_$rep 120 python -u scripts/unet_once.py
+        LDM_SDF_LIB=$LIB/$L UNET_REPS=2 UNET_B=8 TAILN=2 step unet8_${L%.so}_$rep 120 python -u scripts/unet_once.py
       done
     done
     ;;
