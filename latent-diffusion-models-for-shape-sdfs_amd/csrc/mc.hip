@@ -148,8 +148,14 @@ constexpr McTables kMcHost = make_mc_tables();
 __constant__ McTables kMc = make_mc_tables();
 
 // ------------------------------------------------------------------------------ kernels
-constexpr int kChunk = 4096;          // points per scan chunk (256 threads x 16)
-constexpr int kPer = 16;
+// points per thread of the scan-chunk passes (a multiple of 8; MC_PER A/B builds), a chunk =
+// 256 threads x kPer points
+#ifndef MC_PER
+#define MC_PER 16
+#endif
+constexpr int kPer = MC_PER;
+constexpr int kChunk = 256 * kPer;
+static_assert(kPer % 8 == 0 && kPer <= 32, "whole 16-byte code vectors; a 32-bit cube mask");
 
 __device__ __forceinline__ float grid_c(int i, float vs, float origin) {
 #pragma clang fp contract(off)
@@ -263,20 +269,22 @@ __device__ __forceinline__ int block_excl_scan(int v, int* lds /*[4]*/, int* tot
     return base + x - v;
 }
 
-// load the 16 codes of this thread's slice of chunk `blk` (zeros past n)
+// load the kPer codes of this thread's slice of chunk `blk` (zeros past n)
 __device__ __forceinline__ void load_codes(const unsigned short* __restrict__ code, int64_t n,
                                            int blk, unsigned (&c)[kPer]) {
     const int64_t p0 = (int64_t)blk * kChunk + threadIdx.x * kPer;
     if (p0 + kPer <= n) {
         const u32x4* src = reinterpret_cast<const u32x4*>(code + p0);
-        const u32x4 a = src[0], b = src[1];
+        u32x4 a[kPer / 8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            c[2 * q] = a[q] & 0xffffu;
-            c[2 * q + 1] = a[q] >> 16;
-            c[8 + 2 * q] = b[q] & 0xffffu;
-            c[8 + 2 * q + 1] = b[q] >> 16;
-        }
+        for (int h = 0; h < kPer / 8; ++h) a[h] = src[h];
+#pragma unroll
+        for (int h = 0; h < kPer / 8; ++h)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[8 * h + 2 * q] = a[h][q] & 0xffffu;
+                c[8 * h + 2 * q + 1] = a[h][q] >> 16;
+            }
     } else {
 #pragma unroll
         for (int q = 0; q < kPer; ++q) c[q] = p0 + q < n ? code[p0 + q] : 0u;
