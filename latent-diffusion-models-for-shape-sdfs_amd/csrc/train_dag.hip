@@ -32,6 +32,12 @@
 
 #include <mutex>
 
+// DAG_EPI_WT 0 (timing-only A/B builds, results WRONG): the GEMM jobs' epilogue stores plain
+// instead of write-through -- what the plain-store hand-off lever could gain at
+// most, before any same-XCD / cross-XCD split of the stores
+#ifndef DAG_EPI_WT
+#define DAG_EPI_WT 1
+#endif
 namespace ldm {
 namespace dag {
 namespace {
@@ -300,7 +306,7 @@ __device__ __forceinline__ void gemm_job(KNode& N, int job, const float* eps,
 #pragma unroll
         for (int bb = 1; bb < RM * RN; ++bb)
             if (b == bb) c = acc[bb / RN][bb % RN];
-        epi_lds_block<BM, true>(smem, 0, wl, lane, wr, h, r32, L, c, i, nb, e);
+        epi_lds_block<BM, DAG_EPI_WT != 0>(smem, 0, wl, lane, wr, h, r32, L, c, i, nb, e);
     }
 }
 

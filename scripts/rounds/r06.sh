@@ -105,6 +105,14 @@ case $B in
       done
     done
     ;;
+  dagab)
+    # one-launch training step A/B (timing) over the libraries in $DAG_LIBS, alternating
+    for rep in 1 2; do
+      for L in ${DAG_LIBS:?}; do
+        LDM_SDF_LIB=$LIB/$L AB_FORMS=dag TAILN=2 step dag_${L%.so}_$rep 300 python -u scripts/train_form_ab.py 3 128
+      done
+    done
+    ;;
   mregs)
     TAILN=30 step mfma_regs 120 ./scripts/microbench/mfma_regs
     TAILN=28 step loop_replay 120 ./scripts/microbench/loop_replay
