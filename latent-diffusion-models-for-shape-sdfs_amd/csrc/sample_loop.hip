@@ -582,6 +582,9 @@ constexpr int kRepWaves = 8;      // 2 waves per SIMD: 4 rows of each layer per 
 #ifndef SL_XSDB
 #define SL_XSDB 0
 #endif
+#ifndef SL_POLLW
+#define SL_POLLW 8
+#endif
 #ifndef SL_PUBSLEEP
 #define SL_PUBSLEEP 4
 #endif
@@ -774,7 +777,15 @@ __global__ __launch_bounds__(64 * kRepWaves) void sample_replica_kernel(LoopArgs
 #if SL_PRIO
         __builtin_amdgcn_s_setprio(0);           // (A/B) polling waves yield issue to computing ones
 #endif
-        const bool good = stage_tagged<NT, 2>(dst, gran, nsh * K, tg, status, a.spin_limit);
+        // (SL_POLLW < 8, A/B builds: only the first SL_POLLW waves poll, more granules each)
+        bool good = true;
+        if constexpr (SL_POLLW >= kRepWaves) {
+            good = stage_tagged<NT, 2>(dst, gran, nsh * K, tg, status, a.spin_limit);
+        } else {
+            if (wave < SL_POLLW)
+                good = stage_tagged<64 * SL_POLLW, 2 * kRepWaves / SL_POLLW>(
+                    dst, gran, nsh * K, tg, status, a.spin_limit);
+        }
 #if SL_PRIO
         __builtin_amdgcn_s_setprio(SL_PRIO);
 #endif
