@@ -78,6 +78,7 @@ case $B in
     ;;
   dlib)
     # decoder build A/B: scripts/decode_time.py per library in $DEC_LIBS, alternating
+    [ -n "${DEC_TESTS:-}" ] && TAILN=3 step dec_tests 600 $PYT tests/test_gpu_decoder.py tests/test_gpu_configs.py
     for rep in 1 2 3; do
       for L in ${DEC_LIBS:?}; do
         LDM_SDF_LIB=$LIB/$L TAILN=1 step dec_${L%.so}_$rep 120 python -u scripts/decode_time.py 8 256 5
