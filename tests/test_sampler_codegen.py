@@ -7,10 +7,10 @@ scratch and reloaded them SERIALLY every step (scratch_load + s_waitcnt vmcnt(0)
 and the diagnostic stamps merely changed which values spilled.  Round 6 keeps the last residual
 block's weights in LDS (SL_LDSBLK), which leaves the kernel without any scratch; and what the
 stamps really bought -- the wave pausing right after a layer's publish before it polls for the
-next layer -- is now built on purpose (SL_PUBFENCE: a scheduling barrier + s_sleep 1).  This test
-fails if a change (or a compiler update) brings the spills back to the bench's configuration
-(D = 256, B <= 8: sample_replica_kernel<256, 1>), with or without the stamps, or separates a
-publish from its pause."""
+next layer -- is now built on purpose (SL_PUBFENCE: a scheduling barrier + s_sleep SL_PUBSLEEP,
+4 after the round-6 sweep).  This test fails if a change (or a compiler update) brings the
+spills back to the bench's configuration (D = 256, B <= 8: sample_replica_kernel<256, 1>), with
+or without the stamps, or separates a publish from its pause."""
 import os
 import re
 import shutil
