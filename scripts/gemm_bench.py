@@ -49,8 +49,15 @@ for (M, N, K) in SHAPES:
     Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     CbT = torch.empty(N, M, device=dev, dtype=torch.bfloat16)
     cs = torch.empty((M + 31) // 32, N, device=dev)
+    # adfwd / adbwd: the auto-decoder's big products (C19): ReLU with the bf16
+    # output in both layouts (the transposed one k-blocked by 8192), and the ReLU backward with
+    # the mask operand, both layouts and the 32-row column sums
+    CbTb = torch.empty((M + 8191) // 8192 * N * 8192, device=dev, dtype=torch.bfloat16)
+    Rb = torch.randn(M, N, device=dev, generator=g).bfloat16() if OUT == "adbwd" else None
     outs = {"none": dict(colsum=cs), "c": dict(C=C), "cb": dict(Cb=Cb), "cbt": dict(CbT=CbT),
-            "all": dict(C=C, Cb=Cb, CbT=CbT, colsum=cs)}[OUT]
+            "all": dict(C=C, Cb=Cb, CbT=CbT, colsum=cs),
+            "adfwd": dict(mode="relu", Cb=Cb, CbT=CbTb, ct_blk=8192),
+            "adbwd": dict(mode="relu_bwd", Rb=Rb, Cb=Cb, CbT=CbTb, ct_blk=8192, colsum=cs)}[OUT]
     res["out"] = OUT
     SPLIT = int(os.environ.get("SPLITK", "1"))      # emulate split-K: one problem per K slice
     parts = [torch.empty(M, N, device=dev) for _ in range(SPLIT)] if SPLIT > 1 else None
@@ -65,6 +72,10 @@ for (M, N, K) in SHAPES:
         us = timed(lambda: ops.gemm_launch(args, dev))
         res[f"gemm_t{tile}_us"] = round(us, 2)
         res[f"gemm_t{tile}_tflops"] = round(fl / us / 1e6, 1)
+        if os.environ.get("CHECK") and SPLIT == 1 and "C" in outs:   # this tile's fp32 result
+            ref = A.float() @ B.float().T
+            res[f"gemm_t{tile}_err"] = float((C - ref).abs().max())
+            del ref
     if NO_REF:
         print(json.dumps(res), flush=True)
         continue
