@@ -311,12 +311,15 @@ def silu_bwd(dy: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] = No
 
 
 def colsum(G: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
-    """``out (+)= G.sum(0)``, deterministic.  Tall G (>= 64k rows, e.g. C19's 1M samples) goes
-    in two passes -- per-segment sums over up to 256 row segments in parallel, then their sum --
-    because the one-pass kernel has only ceil(M/64) workgroups."""
+    """``out (+)= G.sum(0)``, deterministic.  Tall G goes in two passes -- per-segment sums
+    over up to 256 row segments in parallel, then their sum -- because the one-pass kernel has
+    only ceil(M/64) workgroups: >= 64k rows (C19's 1M samples), and since round 6 >= 16k rows
+    when that is under 64 workgroups (C19's per-32-row bias partials, 32k x 512: 8 workgroups,
+    0.27 ms a call, 5 % of the auto-decoder step).  Config 2's partials (ceil(B/32) rows) stay
+    one-pass, so the one-launch training step still sums them in this order."""
     _contig(G)
     Bn, M = G.shape
-    if Bn >= 65536:
+    if Bn >= 65536 or (Bn >= 16384 and (M + 63) // 64 < 64):
         segs = next((s for s in (256, 128, 64, 32, 16) if Bn % s == 0), 0)
         if segs:
             part = torch.empty(segs, M, device=G.device, dtype=torch.float32)

@@ -53,6 +53,20 @@ def test_colsum_segments(dev):
     assert (got.double() - want).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("rows,cols", [(32768, 512), (20000, 300), (16000, 512), (16384, 4096)])
+def test_colsum_tall(dev, rows, cols):
+    """ops.colsum on tall inputs: the two-pass form (C19's 32-row bias partials, 32k x 512; a
+    row count with only 32-row segments) and the one-pass form on either side of its rule, all
+    against the fp64 sum; accumulate adds to what out holds."""
+    from ldm_sdf import ops
+    g = torch.Generator().manual_seed(rows + cols)
+    G = torch.randn(rows, cols, generator=g)
+    out = torch.full((cols,), 0.5)
+    got = ops.colsum(G.to(dev), out.to(dev), accumulate=True).cpu()
+    want = 0.5 + G.double().sum(0)
+    assert (got.double() - want).abs().max() < 2e-7 * rows ** 0.5 * 8
+
+
 def test_latent_reg(dev):
     from ldm_sdf import ops
     g = torch.Generator().manual_seed(2)
