@@ -220,6 +220,39 @@ WGRAD_TILE = 3
 _KSEG = 64         # column padding of [z || xyz] (a GEMM K segment)
 
 
+def _ad_inputs(z, xyz, S, P, Np, zw, KT, gather=False):
+    """The bf16 step's input operand in both layouts: ``Zx`` [Np, zw] = [z_s || xyz || 0] per
+    sample (rows >= N zero) and ``ZxT`` [Np / KT, zw, KT], its k-blocked transpose.  Samples are
+    shape-major (sample m belongs to shape m // P), so the code columns are a broadcast of z per
+    shape: when P is a multiple of KT every block lies in one shape and both layouts are written
+    by broadcast copies (round 6: the index gathers of [N, L] took ≈ 1 ms of the 64 x 16384
+    step); else (or ``gather``) by the per-sample gathers.  Same values either way
+    (``tests/test_autodecoder_inputs.py``)."""
+    L = z.shape[1]
+    N = S * P
+    nblk = Np // KT
+    dev = z.device
+    bf = dict(device=dev, dtype=torch.bfloat16)
+    Zx = torch.zeros(Np, zw, **bf)
+    ZxT = torch.zeros(nblk, zw, KT, **bf)
+    if not gather and P % KT == 0:
+        zb = z.to(torch.bfloat16)
+        Zx[:N].view(S, P, zw)[:, :, :L] = zb[:, None, :]
+        ZxT[:N // KT].view(S, P // KT, zw, KT)[:, :, :L, :] = zb[:, None, :, None]
+    else:
+        owner_pad = torch.full((Np,), S, device=dev, dtype=torch.long)
+        owner_pad[:N] = torch.arange(S, device=dev).repeat_interleave(P)
+        Zx[:N, :L] = z[owner_pad[:N]]
+        zT = torch.zeros(L, S + 1, **bf)          # column S: the padding rows' zero code
+        zT[:, :S] = z.t()
+        ZxT.permute(1, 0, 2)[:L] = zT[:, owner_pad.view(nblk, KT)]
+    Zx[:N, L:L + 3] = xyz.reshape(N, 3)
+    xyz_pad = torch.zeros(Np, 3, device=dev, dtype=torch.float32)
+    xyz_pad[:N] = xyz.reshape(N, 3)
+    ZxT.permute(1, 0, 2)[L:L + 3] = xyz_pad.t().reshape(3, nblk, KT).to(torch.bfloat16)
+    return Zx, ZxT
+
+
 def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda, epoch,
                           grads, wgrad_tile=WGRAD_TILE):
     """bf16 matrix-core step on ``ldm_gemm_bf16`` (include/ldm_sdf.h).
@@ -279,19 +312,7 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
     # instead of 2 MB apart (one memory page per row: measured 9 us per k-step, TLB-bound).
     KT = next(kt for kt in (8192, 4096, 2048, 1024, 512, 256, 128) if Np % kt == 0)
     nblk = Np // KT
-    owner = torch.arange(S, device=dev).repeat_interleave(P)
-    owner_pad = torch.full((Np,), S, device=dev, dtype=torch.long)
-    owner_pad[:N] = owner
-    Zx = torch.zeros(Np, zw, **bf)
-    Zx[:N, :L] = z[owner]
-    Zx[:N, L:L + 3] = xyz.reshape(N, 3)
-    ZxT = torch.zeros(nblk, zw, KT, **bf)
-    zT = torch.zeros(L, S + 1, **bf)              # column S: the padding rows' zero code
-    zT[:, :S] = z.t()
-    ZxT.permute(1, 0, 2)[:L] = zT[:, owner_pad.view(nblk, KT)]
-    xyz_pad = torch.zeros(Np, 3, **f32)
-    xyz_pad[:N] = xyz.reshape(N, 3)
-    ZxT.permute(1, 0, 2)[L:L + 3] = xyz_pad.t().reshape(3, nblk, KT).to(torch.bfloat16)
+    Zx, ZxT = _ad_inputs(z, xyz, S, P, Np, zw, KT)
 
     # ---- forward: h_l = ReLU(...) in bf16, both layouts (rows >= N written as zeros)
     h, hT = [], []
@@ -355,6 +376,8 @@ def _train_step_gemm_bf16(masters, z, xyz, sdf, *, L, H, skip, delta, reg_lambda
     onehot = None
     if P % 32:                                     # 32-row blocks straddle shapes: a one-hot
         sid = torch.arange(S, device=dev)[:, None, None]   # product sums each shape's rows
+        owner_pad = torch.full((Np,), S, device=dev, dtype=torch.long)
+        owner_pad[:N] = torch.arange(S, device=dev).repeat_interleave(P)
         onehot = (owner_pad.view(1, nblk, KT) == sid).to(torch.bfloat16).permute(1, 0, 2)
         onehot = onehot.contiguous()               # blocked [nblk][S][KT]
     for l in range(7, -1, -1):
