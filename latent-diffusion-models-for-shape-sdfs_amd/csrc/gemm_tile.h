@@ -299,7 +299,32 @@ __device__ __forceinline__ void epi_lds_block(unsigned short* smem, int epi_off,
                 }
             }
             const int n = nb + r32;
-            if (CbTp) {                   // [n][b]: 4 consecutive rows per 8-byte store
+            // [n][b] from the row-layout tile: lane = (column n, 8 consecutive rows), one
+            // 16-byte store, so a store instruction writes 16 columns x 64 contiguous bytes
+            // instead of 32 columns x 16 bytes (round 6).  Whole blocks whose rows keep 8-row
+            // runs together and 16-byte aligned; the others take the accumulator-layout stores
+            // below.  Same bf16 values, only the store grouping differs.  Launch kernels only
+            // (!WT): in the one-launch step (train_dag.hip) the extra code spilled.
+            const bool tvec = !WT && CbTp && !LS && rb + 32 <= Mr &&
+                              (kt ? (kt & 7) == 0 : (ldct & 7) == 0) &&
+                              ((uintptr_t)CbTp & 15) == 0;
+            if (!WT && tvec) {
+                const int q8 = (lane & 3) * 8;
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    const int nl = (lane >> 2) + 16 * half;       // block-local column
+                    float t8[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) t8[e] = sc[(q8 + e) * 32 + nl];
+                    const u32x4 w = {pack2_bf16(t8[0], t8[1]), pack2_bf16(t8[2], t8[3]),
+                                     pack2_bf16(t8[4], t8[5]), pack2_bf16(t8[6], t8[7])};
+                    const int b = rb + q8, nn = nb + nl;
+                    const int64_t at = kt ? ((int64_t)(b / kt) * Nc + nn) * kt + b % kt
+                                          : (int64_t)nn * ldct + b;
+                    vst_at<WT>(CbTp, xCbT(), at, w);
+                }
+            }
+            if (CbTp && !tvec) {          // [n][b]: 4 consecutive rows per 8-byte store
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int b = rb + 8 * g + 4 * h;
