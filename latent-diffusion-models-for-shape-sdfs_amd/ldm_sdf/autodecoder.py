@@ -215,8 +215,10 @@ def autodecoder_train_step(masters: Dict[str, torch.Tensor], z: torch.Tensor, xy
 _KQ = 128          # row padding of the sample axis (the K of the weight-gradient products)
 # ldm_gemm_bf16 tile of the weight-gradient products (128 x 128: each slice walks KT = 8192
 # samples, long enough for the bigger tile's per-CU operand economy); tuning runs pass
-# ``wgrad_tile`` to autodecoder_train_step (the product reads no environment variable)
-WGRAD_TILE = 3
+# ``wgrad_tile`` to autodecoder_train_step (the product reads no environment variable).
+# Round 6 sweep (scripts/ad_wgrad_ab.py, profiles/r06am): the persistent 128 x 128 tile on a
+# 2-deep ring (17) 30.9-31.1 ms/step, 14 31.0, the earlier 3 31.3-31.9, others 32-34; same bits
+WGRAD_TILE = 17
 _KSEG = 64         # column padding of [z || xyz] (a GEMM K segment)
 
 
